@@ -1,0 +1,18 @@
+"""hnsw_amd -- MI355X-native engine for the TFMV/hnsw hot path.
+
+Distance sweep -> layer-0 greedy/beam search -> M-neighbour selection on insert,
+as hand-written HIP kernels for gfx950 behind a C ABI (include/mhnsw.h,
+hnsw_amd/libmhnsw.so).  This package is the host-side mirror of the reference's
+Go API (Graph, Node, CosineDistance, ...).  There is no CPU fallback.
+"""
+from ._lib import (BUILD_BATCH, BUILD_COMPAT, COSINE, EUCLIDEAN, MODE_BEAM, MODE_COMPAT, MODE_EXACT, HnswError,
+                   LIB_PATH, SIGNATURES, load)
+from .graph import (CosineDistance, DistanceFunc, EuclideanDistance, Graph, MakeNode, NewGraph, NewGraphWithConfig,
+                    Node, RegisterDistanceFunc, Vector, distance_func_to_name, merge_topk_device)
+
+__all__ = [
+    "BUILD_BATCH", "BUILD_COMPAT", "COSINE", "EUCLIDEAN", "MODE_BEAM", "MODE_COMPAT", "MODE_EXACT", "HnswError",
+    "LIB_PATH", "SIGNATURES", "load", "CosineDistance", "DistanceFunc", "EuclideanDistance", "Graph", "MakeNode",
+    "NewGraph", "NewGraphWithConfig", "Node", "RegisterDistanceFunc", "Vector", "distance_func_to_name",
+    "merge_topk_device",
+]

@@ -1,0 +1,1011 @@
+// api.cpp -- C ABI (include/mhnsw.h) over the HIP kernels.
+//
+// Host side of the engine: owns the device-resident index (row-major vector
+// store, per-layer fixed-stride adjacency, norms, keys), draws levels like
+// graph.go:388-417, schedules the compat or batched build, and runs searches.
+// The graph lives in HBM; the host keeps only the key -> internal-id map,
+// per-node levels and per-layer counts/entries.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mhnsw.h"
+#include "engine.hpp"
+
+using namespace mh;
+
+namespace {
+
+thread_local std::string g_create_err;
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+};
+
+struct Layer {
+    int32_t* deg = nullptr;
+    int32_t* adj = nullptr;
+    float* adjd = nullptr;
+    int cap = 0;
+    int64_t count = 0;
+    int32_t entry = -1;
+};
+
+}  // namespace
+
+struct mhnsw_index {
+    // public fields (graph.go:305-326)
+    int metric = COSINE;
+    int M = 16;
+    double ml = 0.25;
+    int ef = 20;
+    uint64_t rng = 0;
+    // engine options
+    int build_mode = MHNSW_BUILD_COMPAT;
+    int m0 = 0;  // 0 => 2*M in batch mode, M in compat mode
+    int efc = 0; // 0 => EfSearch
+    int heuristic = 1;
+    int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
+    int vis_log2 = 12;
+    int exact_kk = 0;
+    // shape
+    int dim = 0, pitch = 0, lpr = 0, vpl = 0;
+    bool layers_exist = false;
+    int64_t n = 0, capn = 0;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // device state
+    float* vecs = nullptr;
+    float* norms = nullptr;
+    int64_t* keys = nullptr;
+    int32_t* levels = nullptr;
+    uint32_t* cur_entry = nullptr;
+    int32_t* inc_cnt = nullptr;
+    uint32_t* inc_src = nullptr;
+    float* inc_dist = nullptr;
+    int inc_cap = 64;
+    uint32_t* touched = nullptr;
+    size_t touched_cap = 0;
+    int32_t* touched_cnt = nullptr;
+    int32_t* d_layer_entry = nullptr;
+    unsigned long long* d_stats = nullptr;
+    int* d_err = nullptr;
+    std::vector<Layer> layers;
+    // scratch
+    DevBuf<float> qpad, qnorm, scores, tmp;
+    DevBuf<uint32_t> cand;
+    DevBuf<int64_t> okeys;
+    DevBuf<float> odist;
+    DevBuf<int32_t> on;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool have_timing = false;
+    // host mirrors
+    std::unordered_map<int64_t, int32_t> key2id;
+    std::vector<int32_t> hlevels;
+    int64_t stats_host[8] = {0};
+    std::string err;
+    mutable std::shared_mutex mu;
+};
+
+namespace {
+
+int fail(mhnsw_index* h, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (h)
+        h->err = buf;
+    else
+        g_create_err = buf;
+    return code;
+}
+
+#define HIPCHK(h, x)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) return fail(h, MHNSW_EDEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+#define LCHK(h, x)                                                              \
+    do {                                                                        \
+        int r_ = (x);                                                           \
+        if (r_ != 0) return fail(h, r_ == -4 ? MHNSW_EUNSUPPORTED : MHNSW_EDEVICE, "kernel launch failed (%d) at %s", r_, #x); \
+    } while (0)
+
+// graph.go:916-937
+int validate(mhnsw_index* h) {
+    if (h->M <= 0) return fail(h, MHNSW_EINVAL, "M must be greater than 0, got %d", h->M);
+    if (h->ml <= 0 || h->ml >= 1) return fail(h, MHNSW_EINVAL, "Ml must be between 0 and 1 (exclusive), got %f", h->ml);
+    if (h->ef <= 0) return fail(h, MHNSW_EINVAL, "EfSearch must be greater than 0, got %d", h->ef);
+    if (h->metric != COSINE && h->metric != EUCLIDEAN) return fail(h, MHNSW_EINVAL, "Distance function must be set");
+    return MHNSW_OK;
+}
+
+// graph.go:370-385
+int max_level(double ml, int64_t num) {
+    if (ml == 0) return -1;
+    if (num == 0) return 1;
+    double l = std::log((double)num);
+    l /= std::log(1.0 / ml);
+    return (int)std::round(l) + 1;
+}
+
+// SplitMix64 draw (same stream as oracle/oracle.c og_rng_next)
+double rng_next(uint64_t* s) {
+    uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z = z ^ (z >> 31);
+    return (double)(z >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// graph.go:388-417 randomLevel with the layer-0 size before this insert
+int random_level(double ml, bool layers_exist, int64_t count, uint64_t* rng) {
+    int max = 1;
+    if (layers_exist) max = max_level(ml, count);
+    for (int level = 0; level < max; ++level) {
+        double r = rng_next(rng);
+        if (r > ml) return level;
+    }
+    return max;
+}
+
+int m0_of(const mhnsw_index* h) {
+    if (h->build_mode == MHNSW_BUILD_COMPAT) return h->M;
+    return h->m0 > 0 ? h->m0 : 2 * h->M;
+}
+int cap_of(const mhnsw_index* h, int l) {
+    const int m = l == 0 ? m0_of(h) : h->M;
+    return m + 1;  // addNeighbor overflows by one before evicting (graph.go:50-53)
+}
+
+template <class T>
+int ensure_buf(mhnsw_index* h, DevBuf<T>& b, size_t n) {
+    if (b.n >= n) return 0;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+    size_t want = std::max(n, b.n * 2);
+    if (hipMalloc(&b.p, want * sizeof(T)) != hipSuccess) return fail(h, MHNSW_ENOMEM, "device allocation of %zu bytes failed", want * sizeof(T));
+    b.n = want;
+    return 0;
+}
+
+template <class T>
+int grow(mhnsw_index* h, T*& p, int64_t old_elems, int64_t new_elems, int fill_byte, bool fill32 = false,
+         uint32_t fill_val = 0) {
+    T* np = nullptr;
+    if (hipMalloc(&np, (size_t)new_elems * sizeof(T)) != hipSuccess)
+        return fail(h, MHNSW_ENOMEM, "device allocation of %lld bytes failed", (long long)(new_elems * sizeof(T)));
+    if (fill32)
+        HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)np, (int)fill_val, (size_t)new_elems * sizeof(T) / 4, h->stream));
+    else if (fill_byte >= 0)
+        HIPCHK(h, hipMemsetAsync(np, fill_byte, (size_t)new_elems * sizeof(T), h->stream));
+    if (p && old_elems > 0) HIPCHK(h, hipMemcpyAsync(np, p, (size_t)old_elems * sizeof(T), hipMemcpyDeviceToDevice, h->stream));
+    if (p) {
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        (void)hipFree(p);
+    }
+    p = np;
+    return 0;
+}
+
+int ensure_layer(mhnsw_index* h, int l) {
+    while ((int)h->layers.size() <= l) {
+        if ((int)h->layers.size() >= MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "more than %d layers", MH_MAXL);
+        Layer L;
+        L.cap = cap_of(h, (int)h->layers.size());
+        const int64_t c = std::max<int64_t>(h->capn, 1);
+        int r;
+        if ((r = grow(h, L.deg, 0, c, -1, true, 0xFFFFFFFEu))) return r;
+        if ((r = grow(h, L.adj, 0, c * L.cap, 0xFF))) return r;
+        if ((r = grow(h, L.adjd, 0, c * L.cap, 0))) return r;
+        h->layers.push_back(L);
+    }
+    return 0;
+}
+
+// re-stride adjacency when M (or M0) grew beyond the allocated row width
+int ensure_caps(mhnsw_index* h) {
+    for (int l = 0; l < (int)h->layers.size(); ++l) {
+        Layer& L = h->layers[l];
+        const int need = cap_of(h, l);
+        if (need <= L.cap) continue;
+        const int64_t c = std::max<int64_t>(h->capn, 1);
+        int32_t* na = nullptr;
+        float* nd = nullptr;
+        if (hipMalloc(&na, (size_t)c * need * 4) != hipSuccess || hipMalloc(&nd, (size_t)c * need * 4) != hipSuccess)
+            return fail(h, MHNSW_ENOMEM, "device allocation failed");
+        HIPCHK(h, hipMemsetAsync(na, 0xFF, (size_t)c * need * 4, h->stream));
+        HIPCHK(h, hipMemcpy2DAsync(na, need * 4, L.adj, L.cap * 4, L.cap * 4, c, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(h, hipMemcpy2DAsync(nd, need * 4, L.adjd, L.cap * 4, L.cap * 4, c, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        (void)hipFree(L.adj);
+        (void)hipFree(L.adjd);
+        L.adj = na;
+        L.adjd = nd;
+        L.cap = need;
+    }
+    return 0;
+}
+
+int ensure_capacity(mhnsw_index* h, int64_t need) {
+    if (need <= h->capn) return 0;
+    int64_t nc = std::max<int64_t>(need, std::max<int64_t>(1024, h->capn * 2));
+    if (h->capn > 0) nc = std::max<int64_t>(need, h->capn + h->capn / 2);
+    const int64_t oc = h->capn;
+    int r;
+    if ((r = grow(h, h->vecs, oc * h->pitch, nc * h->pitch, 0))) return r;
+    if ((r = grow(h, h->norms, oc, nc, 0))) return r;
+    if ((r = grow(h, h->keys, oc, nc, 0))) return r;
+    if ((r = grow(h, h->levels, oc, nc, 0))) return r;
+    if ((r = grow(h, h->cur_entry, 0, nc, 0))) return r;
+    if ((r = grow(h, h->inc_cnt, 0, nc, 0))) return r;
+    if (h->build_mode == MHNSW_BUILD_BATCH || h->inc_src) {
+        if ((r = grow(h, h->inc_src, 0, nc * h->inc_cap, 0))) return r;
+        if ((r = grow(h, h->inc_dist, 0, nc * h->inc_cap, 0))) return r;
+    }
+    for (auto& L : h->layers) {
+        if ((r = grow(h, L.deg, oc, nc, -1, true, 0xFFFFFFFEu))) return r;
+        if ((r = grow(h, L.adj, oc * L.cap, nc * L.cap, 0xFF))) return r;
+        if ((r = grow(h, L.adjd, oc * L.cap, nc * L.cap, 0))) return r;
+    }
+    h->capn = nc;
+    return 0;
+}
+
+GraphDev graph_view(const mhnsw_index* h) {
+    GraphDev g;
+    memset(&g, 0, sizeof(g));
+    g.vecs = h->vecs;
+    g.norms = h->norms;
+    g.keys = h->keys;
+    for (int l = 0; l < (int)h->layers.size(); ++l) {
+        g.deg[l] = h->layers[l].deg;
+        g.adj[l] = h->layers[l].adj;
+        g.adjd[l] = h->layers[l].adjd;
+        g.cap[l] = h->layers[l].cap;
+    }
+    g.pitch = h->pitch;
+    g.dim = h->dim;
+    g.metric = h->metric;
+    g.nlayers = (int)h->layers.size();
+    return g;
+}
+
+int set_shape(mhnsw_index* h, int dim) {
+    int lpr, vpl;
+    if (!pick_cfg(dim, lpr, vpl)) return fail(h, MHNSW_EUNSUPPORTED, "dimension %d not supported (1..2048)", dim);
+    h->dim = dim;
+    h->lpr = lpr;
+    h->vpl = vpl;
+    h->pitch = pitch_of(lpr, vpl);
+    return 0;
+}
+
+int set_deg(mhnsw_index* h, int l, int64_t id, int32_t v) {
+    HIPCHK(h, hipMemcpyAsync(h->layers[l].deg + id, &v, 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int sync_layer_entries(mhnsw_index* h) {
+    int32_t e[MH_MAXL];
+    for (int l = 0; l < MH_MAXL; ++l) e[l] = l < (int)h->layers.size() ? h->layers[l].entry : -1;
+    HIPCHK(h, hipMemcpyAsync(h->d_layer_entry, e, sizeof(e), hipMemcpyHostToDevice, h->stream));
+    return 0;
+}
+
+int zero_err(mhnsw_index* h) {
+    HIPCHK(h, hipMemsetAsync(h->d_err, 0, sizeof(int), h->stream));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// build drivers
+// ---------------------------------------------------------------------------
+int run_build_compat(mhnsw_index* h, int64_t n0, int64_t n1) {
+    if (h->M + 1 > 64) return fail(h, MHNSW_EUNSUPPORTED, "compat build supports M <= 63");
+    int r;
+    if ((r = sync_layer_entries(h))) return r;
+    if ((r = zero_err(h))) return r;
+    CompatBuildArgs a;
+    a.g = graph_view(h);
+    a.n0 = n0;
+    a.n1 = n1;
+    a.levels = h->levels;
+    a.layer_entry = h->d_layer_entry;
+    a.M = h->M;
+    a.ef = h->ef;
+    a.stats = h->d_stats + 4;
+    a.err = h->d_err;
+    a.vis_log2 = h->vis_log2;
+    int lr = launch_build_compat(a, h->lpr, h->vpl, h->stream);
+    if (lr == -2) return fail(h, MHNSW_EUNSUPPORTED, "compat build LDS budget exceeded (ef=%d, M=%d)", h->ef, h->M);
+    LCHK(h, lr);
+    int err = 0;
+    HIPCHK(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (err & 1) return fail(h, MHNSW_EINTERNAL, "visited set overflow (raise vis_log2)");
+    if (err & 2) return fail(h, MHNSW_EINTERNAL, "no nodes found in neighborhood search");
+    return 0;
+}
+
+int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t entry) {
+    if (a1 <= a0) return 0;
+    HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(h->cur_entry + a0), (int)entry, (size_t)(a1 - a0), h->stream));
+    int maxlvl = 0;
+    for (int64_t i = a0; i < a1; ++i) maxlvl = std::max(maxlvl, h->hlevels[i]);
+    const int efc = h->efc > 0 ? h->efc : h->ef;
+    for (int l = top; l >= 0; --l) {
+        const int mcap = l == 0 ? m0_of(h) : h->M;
+        BatchBuildArgs a;
+        a.g = graph_view(h);
+        a.layer = l;
+        a.n0 = a0;
+        a.n1 = a1;
+        a.levels = h->levels;
+        a.cur_entry = h->cur_entry;
+        a.ef = std::max(efc, mcap);
+        a.mcap = mcap;
+        a.heuristic = h->heuristic;
+        a.inc_cnt = h->inc_cnt;
+        a.inc_src = h->inc_src;
+        a.inc_dist = h->inc_dist;
+        a.inc_cap = h->inc_cap;
+        a.touched = h->touched;
+        a.touched_cnt = h->touched_cnt;
+        a.stats = h->d_stats + 4;
+        a.vis_log2 = h->vis_log2;
+        HIPCHK(h, hipMemsetAsync(h->touched_cnt, 0, 4, h->stream));
+        LCHK(h, launch_build_batch_search(a, h->lpr, h->vpl, h->stream));
+        if (maxlvl >= l) LCHK(h, launch_build_batch_commit(a, (a1 - a0) * mcap, h->stream));
+    }
+    return 0;
+}
+
+int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1) {
+    int r;
+    if (!h->inc_src) {
+        if ((r = grow(h, h->inc_src, 0, h->capn * h->inc_cap, 0))) return r;
+        if ((r = grow(h, h->inc_dist, 0, h->capn * h->inc_cap, 0))) return r;
+    }
+    const size_t tneed = (size_t)h->batch_max * (size_t)std::max(m0_of(h), h->M) + 64;
+    if (h->touched_cap < tneed) {
+        if (h->touched) (void)hipFree(h->touched);
+        if (hipMalloc(&h->touched, tneed * 4) != hipSuccess) return fail(h, MHNSW_ENOMEM, "device allocation failed");
+        h->touched_cap = tneed;
+    }
+    // top layer / entry before this call, from the levels of nodes < n0
+    int top = -1;
+    uint32_t entry = EMPTY_ID;
+    for (int64_t i = 0; i < n0; ++i)
+        if (h->hlevels[i] > top) {
+            top = h->hlevels[i];
+            entry = (uint32_t)i;
+        }
+    int64_t i = n0;
+    while (i < n1) {
+        const int lv = h->hlevels[i];
+        if (top < 0) {  // first node of the graph: alone in every layer
+            for (int l = 0; l <= lv; ++l)
+                if ((r = set_deg(h, l, i, 0))) return r;
+            top = lv;
+            entry = (uint32_t)i;
+            ++i;
+            continue;
+        }
+        if (lv > top) {  // new top layers: insert alone, then it becomes the entry
+            for (int l = top + 1; l <= lv; ++l)
+                if ((r = set_deg(h, l, i, 0))) return r;
+            if ((r = run_batch_layers(h, i, i + 1, top, entry))) return r;
+            top = lv;
+            entry = (uint32_t)i;
+            ++i;
+            continue;
+        }
+        int64_t bsz = std::max<int64_t>(h->batch_min, (int64_t)((double)i * h->batch_ratio_pct / 100.0));
+        bsz = std::min<int64_t>(bsz, h->batch_max);
+        int64_t j = i;
+        while (j < n1 && j - i < bsz && h->hlevels[j] <= top) ++j;
+        if ((r = run_batch_layers(h, i, j, top, entry))) return r;
+        i = j;
+    }
+    return 0;
+}
+
+int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_on_device, int64_t n, int dim,
+             const int32_t* levels) {
+    int r = validate(h);
+    if (r) return r;
+    if (n <= 0) return 0;
+    if (h->layers_exist && h->dim != dim)  // graph.go:450-455
+        return fail(h, MHNSW_EDIM, "embedding dimension mismatch: %d != %d", h->dim, dim);
+    if (!h->layers_exist && (r = set_shape(h, dim))) return r;
+    // reject duplicates (reference Add deadlocks on them, graph.go:511-513 -> :844)
+    {
+        std::unordered_map<int64_t, int> seen;
+        for (int64_t i = 0; i < n; ++i) {
+            if (h->key2id.count(keys[i]) || seen.count(keys[i]))
+                return fail(h, MHNSW_EUNSUPPORTED, "duplicate key %lld: replacement not supported",
+                            (long long)keys[i]);
+            seen[keys[i]] = 1;
+        }
+    }
+    if (h->build_mode == MHNSW_BUILD_COMPAT && h->M + 1 > 64)
+        return fail(h, MHNSW_EUNSUPPORTED, "compat build supports M <= 63");
+    if (m0_of(h) + 1 > 64 || h->M + 1 > 64) return fail(h, MHNSW_EUNSUPPORTED, "degree caps above 63 unsupported");
+    if ((r = ensure_caps(h))) return r;
+    const int64_t n0 = h->n, n1 = h->n + n;
+    // levels (graph.go:457): count before each insert grows by one
+    std::vector<int32_t> lv(n);
+    bool le = h->layers_exist;
+    for (int64_t i = 0; i < n; ++i) {
+        if (levels) {
+            lv[i] = levels[i];
+            if (lv[i] < 0) return fail(h, MHNSW_EINVAL, "invalid level: %d", lv[i]);
+        } else {
+            lv[i] = random_level(h->ml, le, n0 + i, &h->rng);
+        }
+        if (lv[i] >= MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "level %d >= %d", lv[i], MH_MAXL);
+        le = true;
+    }
+    if ((r = ensure_capacity(h, n1))) return r;
+    int maxl = 0;
+    for (auto v : lv) maxl = std::max(maxl, v);
+    if ((r = ensure_layer(h, maxl))) return r;
+    // upload keys, levels, vectors (padded), norms
+    HIPCHK(h, hipMemcpyAsync(h->keys + n0, keys, n * sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->levels + n0, lv.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+    const float* src = vecs;
+    if (!vecs_on_device) {
+        if ((r = ensure_buf(h, h->tmp, (size_t)n * dim))) return r;
+        HIPCHK(h, hipMemcpyAsync(h->tmp.p, vecs, (size_t)n * dim * 4, hipMemcpyHostToDevice, h->stream));
+        src = h->tmp.p;
+    }
+    LCHK(h, launch_pad_rows(src, n, dim, h->vecs + (size_t)n0 * h->pitch, h->pitch, h->stream));
+    LCHK(h, launch_norms(h->vecs, n0, n1, h->pitch, h->lpr, h->vpl, h->norms, h->stream));
+    // host bookkeeping
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t id = (int32_t)(n0 + i);
+        h->key2id[keys[i]] = id;
+        h->hlevels.push_back(lv[i]);
+        for (int l = 0; l <= lv[i]; ++l) {
+            if (h->layers[l].count == 0) h->layers[l].entry = id;
+            h->layers[l].count++;
+        }
+    }
+    h->layers_exist = true;
+    h->n = n1;
+    if (h->build_mode == MHNSW_BUILD_COMPAT)
+        r = run_build_compat(h, n0, n1);
+    else
+        r = run_build_batch(h, n0, n1);
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return r;
+}
+
+int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B, int dim, int k, int mode, int ef,
+                const int64_t* entry_key, int64_t* okeys, float* odist, int32_t* on, hipStream_t s, bool timing) {
+    int r = validate(h);
+    if (r) return r;
+    if (k <= 0) return fail(h, MHNSW_EK, "k must be greater than 0, got %d", k);  // graph.go:542-544
+    if (h->layers_exist && h->dim != dim) {                                          // graph.go:547-552
+        if (B == 1) return fail(h, MHNSW_EDIM, "embedding dimension mismatch: %d != %d", h->dim, dim);
+        return fail(h, MHNSW_EDIM, "embedding dimension mismatch for query %d: %d != %d", 0, h->dim, dim);
+    }
+    if (mode < 0 || mode > 2) return fail(h, MHNSW_EINVAL, "unknown search mode %d", mode);
+    if (B <= 0) return 0;
+    if (!h->layers_exist || h->n == 0) {  // graph.go:554-556: nil, nil
+        if (on_device)
+            HIPCHK(h, hipMemsetAsync(on, 0, B * 4, s));
+        else
+            memset(on, 0, B * 4);
+        return 0;
+    }
+    if (ef <= 0) ef = h->ef;
+    int top = (int)h->layers.size() - 1;
+    while (top > 0 && h->layers[top].count == 0) --top;
+    uint32_t entry = (uint32_t)h->layers[top].entry;
+    if (entry_key) {
+        auto it = h->key2id.find(*entry_key);
+        if (it == h->key2id.end() || h->hlevels[it->second] < top)
+            return fail(h, MHNSW_EINVAL, "entry key %lld not in top layer", (long long)*entry_key);
+        entry = (uint32_t)it->second;
+    }
+    if ((r = ensure_buf(h, h->qpad, (size_t)B * h->pitch))) return r;
+    const float* qsrc = queries;
+    if (!on_device) {
+        if ((r = ensure_buf(h, h->tmp, (size_t)B * dim))) return r;
+        HIPCHK(h, hipMemcpyAsync(h->tmp.p, queries, (size_t)B * dim * 4, hipMemcpyHostToDevice, s));
+        qsrc = h->tmp.p;
+    }
+    LCHK(h, launch_pad_rows(qsrc, B, dim, h->qpad.p, h->pitch, s));
+    int64_t* dk = okeys;
+    float* dd = odist;
+    int32_t* dn = on;
+    if (!on_device) {
+        if ((r = ensure_buf(h, h->okeys, (size_t)B * k)) || (r = ensure_buf(h, h->odist, (size_t)B * k)) ||
+            (r = ensure_buf(h, h->on, (size_t)B)))
+            return r;
+        dk = h->okeys.p;
+        dd = h->odist.p;
+        dn = h->on.p;
+    }
+    HIPCHK(h, hipMemsetAsync(h->d_err, 0, sizeof(int), s));
+    if (mode == MHNSW_MODE_EXACT) {
+        if (k > 64) return fail(h, MHNSW_EUNSUPPORTED, "exact mode supports k <= 64");
+        const int kk = h->exact_kk > 0 ? std::min(64, std::max(h->exact_kk, k)) : std::min(64, std::max(2 * k, k + 16));
+        const int64_t ldS = (h->n + 255) / 256 * 256;
+        const int64_t budget = (int64_t)4 << 30;  // score workspace bytes
+        int64_t qc = std::max<int64_t>(1, std::min<int64_t>(B, budget / (ldS * 4)));
+        qc = std::min<int64_t>(qc, 4096);
+        if ((r = ensure_buf(h, h->scores, (size_t)qc * ldS)) || (r = ensure_buf(h, h->qnorm, (size_t)B)) ||
+            (r = ensure_buf(h, h->cand, (size_t)qc * kk)))
+            return r;
+        LCHK(h, launch_norms(h->qpad.p, 0, B, h->pitch, h->lpr, h->vpl, h->qnorm.p, s));
+        GraphDev g = graph_view(h);
+        if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
+        for (int64_t q0 = 0; q0 < B; q0 += qc) {
+            const int64_t nb = std::min(qc, B - q0);
+            ExactArgs a;
+            a.X = h->vecs;
+            a.xnorm = h->norms;
+            a.deg0 = h->layers[0].deg;
+            a.N = h->n;
+            a.Q = h->qpad.p + (size_t)q0 * h->pitch;
+            a.qnorm = h->qnorm.p + q0;
+            a.B = nb;
+            a.pitch = h->pitch;
+            a.dim = h->dim;
+            a.metric = h->metric;
+            a.scores = h->scores.p;
+            a.ldS = ldS;
+            a.kk = kk;
+            a.cand = h->cand.p;
+            LCHK(h, launch_exact_scores(a, s));
+            LCHK(h, launch_exact_select(a, s));
+            LCHK(h, launch_rerank(a.Q, g, h->cand.p, kk, nb, h->lpr, h->vpl, k, dk + q0 * k, dd + q0 * k, dn + q0,
+                                  nullptr, s));
+        }
+        if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));
+    } else {
+        if ((r = sync_layer_entries(h))) return r;
+        SearchArgs a;
+        a.g = graph_view(h);
+        a.q = h->qpad.p;
+        a.B = B;
+        a.k = k;
+        a.ef = ef;
+        a.top = top;
+        a.entry = entry;
+        a.layer_entry = h->d_layer_entry;
+        a.out_keys = dk;
+        a.out_dist = dd;
+        a.out_n = dn;
+        a.out_ids = nullptr;
+        a.stats = h->d_stats;
+        a.err = h->d_err;
+        a.vis_log2 = h->vis_log2;
+        if (mode == MHNSW_MODE_BEAM) {
+            if (std::max(ef, k) > 256) return fail(h, MHNSW_EUNSUPPORTED, "beam mode supports max(ef,k) <= 256");
+            if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
+            LCHK(h, launch_search_beam(a, h->lpr, h->vpl, s));
+            if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));
+        } else {
+            if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
+            int lr = launch_search_compat(a, h->lpr, h->vpl, s);
+            if (lr == -2) return fail(h, MHNSW_EUNSUPPORTED, "compat search LDS budget exceeded (ef=%d, k=%d)", ef, k);
+            LCHK(h, lr);
+            if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));
+        }
+    }
+    h->have_timing = timing;
+    h->stats_host[6] += B;
+    if (!on_device) {
+        HIPCHK(h, hipMemcpyAsync(okeys, dk, (size_t)B * k * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipMemcpyAsync(odist, dd, (size_t)B * k * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipMemcpyAsync(on, dn, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+        int err = 0;
+        HIPCHK(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipStreamSynchronize(s));
+        if (err) return fail(h, MHNSW_EINTERNAL, "visited set overflow (raise vis_log2)");
+    }
+    return 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int mhnsw_create(int metric, int M, double ml, int ef_search, uint64_t seed, mhnsw_index** out) {
+    if (!out) return MHNSW_EINVAL;
+    *out = nullptr;
+    mhnsw_index* h = new (std::nothrow) mhnsw_index();
+    if (!h) return fail(nullptr, MHNSW_ENOMEM, "out of memory");
+    h->metric = metric;
+    h->M = M;
+    h->ml = ml;
+    h->ef = ef_search;
+    h->rng = seed;
+    int r = validate(h);  // NewGraphWithConfig (graph.go:352-366)
+    if (r) {
+        g_create_err = h->err;
+        delete h;
+        return r;
+    }
+    if (hipGetDevice(&h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return fail(nullptr, MHNSW_EDEVICE, "no HIP device available");
+    }
+    if (hipMalloc(&h->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&h->d_err, sizeof(int)) != hipSuccess || hipMalloc(&h->touched_cnt, 16) != hipSuccess ||
+        hipMalloc(&h->d_layer_entry, MH_MAXL * 4) != hipSuccess || hipEventCreate(&h->ev0) != hipSuccess ||
+        hipEventCreate(&h->ev1) != hipSuccess || hipMemset(h->d_stats, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
+        mhnsw_destroy(h);
+        return fail(nullptr, MHNSW_EDEVICE, "device initialisation failed");
+    }
+    *out = h;
+    return MHNSW_OK;
+}
+
+void mhnsw_destroy(mhnsw_index* h) {
+    if (!h) return;
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    auto F = [](void* p) {
+        if (p) (void)hipFree(p);
+    };
+    F(h->vecs);
+    F(h->norms);
+    F(h->keys);
+    F(h->levels);
+    F(h->cur_entry);
+    F(h->inc_cnt);
+    F(h->inc_src);
+    F(h->inc_dist);
+    F(h->touched);
+    F(h->touched_cnt);
+    F(h->d_layer_entry);
+    F(h->d_stats);
+    F(h->d_err);
+    for (auto& L : h->layers) {
+        F(L.deg);
+        F(L.adj);
+        F(L.adjd);
+    }
+    F(h->qpad.p);
+    F(h->qnorm.p);
+    F(h->scores.p);
+    F(h->tmp.p);
+    F(h->cand.p);
+    F(h->okeys.p);
+    F(h->odist.p);
+    F(h->on.p);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+const char* mhnsw_last_error(const mhnsw_index* h) { return h ? h->err.c_str() : g_create_err.c_str(); }
+
+int mhnsw_set_params(mhnsw_index* h, int metric, int M, double ml, int ef_search) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    h->metric = metric;
+    h->M = M;
+    h->ml = ml;
+    h->ef = ef_search;
+    return MHNSW_OK;
+}
+
+int mhnsw_get_params(const mhnsw_index* h, int* metric, int* M, double* ml, int* ef_search) {
+    if (metric) *metric = h->metric;
+    if (M) *M = h->M;
+    if (ml) *ml = h->ml;
+    if (ef_search) *ef_search = h->ef;
+    return MHNSW_OK;
+}
+
+int mhnsw_seed(mhnsw_index* h, uint64_t seed) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    h->rng = seed;
+    return MHNSW_OK;
+}
+
+int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    std::string n(name ? name : "");
+    if (n == "build_mode") {
+        if (v != MHNSW_BUILD_COMPAT && v != MHNSW_BUILD_BATCH) return fail(h, MHNSW_EINVAL, "bad build_mode");
+        if (h->n > 0 && v != h->build_mode) return fail(h, MHNSW_EINVAL, "build_mode must be set before the first Add");
+        h->build_mode = (int)v;
+    } else if (n == "m0") {
+        if (h->n > 0) return fail(h, MHNSW_EINVAL, "m0 must be set before the first Add");
+        h->m0 = (int)v;
+    } else if (n == "ef_construction") {
+        h->efc = (int)v;
+    } else if (n == "heuristic") {
+        h->heuristic = (int)(v != 0);
+    } else if (n == "batch_min") {
+        h->batch_min = (int)std::max<int64_t>(1, v);
+    } else if (n == "batch_max") {
+        h->batch_max = (int)std::max<int64_t>(1, v);
+    } else if (n == "batch_ratio_pct") {
+        h->batch_ratio_pct = (int)std::max<int64_t>(0, v);
+    } else if (n == "vis_log2") {
+        if (v < 8 || v > 15) return fail(h, MHNSW_EINVAL, "vis_log2 must be in [8, 15]");
+        h->vis_log2 = (int)v;
+    } else if (n == "exact_kk") {
+        h->exact_kk = (int)v;
+    } else {
+        return fail(h, MHNSW_EINVAL, "unknown option '%s'", n.c_str());
+    }
+    return MHNSW_OK;
+}
+
+int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
+    std::string n(name ? name : "");
+    if (n == "build_mode") *v = h->build_mode;
+    else if (n == "m0") *v = m0_of(h);
+    else if (n == "ef_construction") *v = h->efc > 0 ? h->efc : h->ef;
+    else if (n == "heuristic") *v = h->heuristic;
+    else if (n == "batch_min") *v = h->batch_min;
+    else if (n == "batch_max") *v = h->batch_max;
+    else if (n == "batch_ratio_pct") *v = h->batch_ratio_pct;
+    else if (n == "vis_log2") *v = h->vis_log2;
+    else if (n == "exact_kk") *v = h->exact_kk;
+    else if (n == "pitch") *v = h->pitch;
+    else if (n == "capacity") *v = h->capn;
+    else return MHNSW_EINVAL;
+    return MHNSW_OK;
+}
+
+int mhnsw_validate(mhnsw_index* h) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    return validate(h);
+}
+
+int mhnsw_reserve(mhnsw_index* h, int64_t n, int dim) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    int r;
+    if (!h->layers_exist) {
+        if ((r = set_shape(h, dim))) return r;
+    } else if (dim != h->dim) {
+        return fail(h, MHNSW_EDIM, "embedding dimension mismatch: %d != %d", h->dim, dim);
+    }
+    if ((r = ensure_capacity(h, n))) return r;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int mhnsw_add(mhnsw_index* h, const int64_t* keys, const float* vecs, int64_t n, int dim, const int32_t* levels) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    return add_impl(h, keys, vecs, false, n, dim, levels);
+}
+
+int mhnsw_add_device(mhnsw_index* h, const int64_t* keys, const float* d_vecs, int64_t n, int dim,
+                     const int32_t* levels) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    return add_impl(h, keys, d_vecs, true, n, dim, levels);
+}
+
+int mhnsw_search(mhnsw_index* h, const float* queries, int64_t B, int dim, int k, int mode, int ef,
+                 const int64_t* entry_key, int64_t* out_keys, float* out_dist, int32_t* out_n) {
+    // scratch buffers are per handle: serialise host-pointer searches
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    return search_impl(h, queries, false, B, dim, k, mode, ef, entry_key, out_keys, out_dist, out_n, h->stream, true);
+}
+
+int mhnsw_search_device(mhnsw_index* h, const float* d_queries, int64_t B, int dim, int k, int mode, int ef,
+                        int64_t* d_keys, float* d_dist, int32_t* d_n, void* stream) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    return search_impl(h, d_queries, true, B, dim, k, mode, ef, nullptr, d_keys, d_dist, d_n, s, true);
+}
+
+int64_t mhnsw_len(const mhnsw_index* h) { return h->layers.empty() ? 0 : h->layers[0].count; }
+int mhnsw_dims(const mhnsw_index* h) { return h->layers_exist ? h->dim : 0; }
+int mhnsw_num_layers(const mhnsw_index* h) { return (int)h->layers.size(); }
+int64_t mhnsw_layer_count(const mhnsw_index* h, int l) {
+    return l >= 0 && l < (int)h->layers.size() ? h->layers[l].count : 0;
+}
+
+int mhnsw_lookup(mhnsw_index* h, int64_t key, float* out) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    auto it = h->key2id.find(key);
+    if (it == h->key2id.end()) return 0;
+    HIPCHK(h, hipMemcpy(out, h->vecs + (size_t)it->second * h->pitch, (size_t)h->dim * 4, hipMemcpyDeviceToHost));
+    return 1;
+}
+
+int mhnsw_distance_device(int metric, const float* d_q, const float* d_X, int64_t n, int dim, float* d_out,
+                          void* stream) {
+    int lpr, vpl;
+    if (metric != COSINE && metric != EUCLIDEAN) return fail(nullptr, MHNSW_EINVAL, "Distance function must be set");
+    if (!pick_cfg(dim, lpr, vpl)) return fail(nullptr, MHNSW_EUNSUPPORTED, "dimension %d not supported", dim);
+    if (n <= 0) return 0;
+    const int pitch = pitch_of(lpr, vpl);
+    hipStream_t s = (hipStream_t)stream;
+    float *qp = nullptr, *xp = nullptr;
+    if (hipMallocAsync((void**)&qp, (size_t)pitch * 4, s) != hipSuccess ||
+        hipMallocAsync((void**)&xp, (size_t)n * pitch * 4, s) != hipSuccess)
+        return fail(nullptr, MHNSW_ENOMEM, "device allocation failed");
+    int r = 0;
+    if (launch_pad_rows(d_q, 1, dim, qp, pitch, s) || launch_pad_rows(d_X, n, dim, xp, pitch, s) ||
+        launch_sweep(qp, xp, n, pitch, lpr, vpl, metric, d_out, s))
+        r = fail(nullptr, MHNSW_EDEVICE, "sweep launch failed");
+    (void)hipFreeAsync(qp, s);
+    (void)hipFreeAsync(xp, s);
+    return r;
+}
+
+int mhnsw_distance(int metric, const float* q, const float* X, int64_t n, int dim, float* out) {
+    if (n <= 0) return 0;
+    float *dq = nullptr, *dx = nullptr, *dout = nullptr;
+    if (hipMalloc(&dq, (size_t)dim * 4) != hipSuccess || hipMalloc(&dx, (size_t)n * dim * 4) != hipSuccess ||
+        hipMalloc(&dout, (size_t)n * 4) != hipSuccess)
+        return fail(nullptr, MHNSW_ENOMEM, "device allocation failed");
+    int r = 0;
+    if (hipMemcpy(dq, q, (size_t)dim * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dx, X, (size_t)n * dim * 4, hipMemcpyHostToDevice) != hipSuccess)
+        r = fail(nullptr, MHNSW_EDEVICE, "copy failed");
+    if (!r) r = mhnsw_distance_device(metric, dq, dx, n, dim, dout, nullptr);
+    if (!r && (hipDeviceSynchronize() != hipSuccess ||
+               hipMemcpy(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess))
+        r = fail(nullptr, MHNSW_EDEVICE, "sweep failed");
+    (void)hipFree(dq);
+    (void)hipFree(dx);
+    (void)hipFree(dout);
+    return r;
+}
+
+int mhnsw_export_sizes(mhnsw_index* h, int64_t* N, int* dim, int* L, int* cap) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    *N = h->n;
+    *dim = h->dim;
+    *L = (int)h->layers.size();
+    int c = 0;
+    for (auto& Ly : h->layers) c = std::max(c, Ly.cap);
+    *cap = c;
+    return 0;
+}
+
+int mhnsw_export(mhnsw_index* h, int64_t* keys, float* vecs, int32_t* deg, int32_t* adj, int cap, int32_t* entry) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    const int64_t N = h->n;
+    if (N == 0) return 0;
+    HIPCHK(h, hipMemcpy(keys, h->keys, N * 8, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy2D(vecs, (size_t)h->dim * 4, h->vecs, (size_t)h->pitch * 4, (size_t)h->dim * 4, N,
+                          hipMemcpyDeviceToHost));
+    std::vector<int32_t> row;
+    for (int l = 0; l < (int)h->layers.size(); ++l) {
+        const Layer& L = h->layers[l];
+        entry[l] = L.entry;
+        HIPCHK(h, hipMemcpy(deg + (size_t)l * N, L.deg, N * 4, hipMemcpyDeviceToHost));
+        row.resize((size_t)N * L.cap);
+        HIPCHK(h, hipMemcpy(row.data(), L.adj, (size_t)N * L.cap * 4, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < N; ++i) {
+            const int d = deg[(size_t)l * N + i];
+            if (d > cap) return fail(h, MHNSW_EINVAL, "export cap %d smaller than degree %d", cap, d);
+            int32_t* o = adj + ((size_t)l * N + i) * cap;
+            for (int j = 0; j < cap; ++j) o[j] = (j < d) ? row[(size_t)i * L.cap + j] : -1;
+        }
+    }
+    return 0;
+}
+
+int mhnsw_import(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t* keys, const float* vecs,
+                 const int32_t* deg, const int32_t* adj, const int32_t* entry) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    if (h->n > 0) return fail(h, MHNSW_EINVAL, "import requires an empty index");
+    if (L > MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "more than %d layers", MH_MAXL);
+    if (cap > 64) return fail(h, MHNSW_EUNSUPPORTED, "degree cap above 64 unsupported");
+    int r;
+    if ((r = set_shape(h, dim))) return r;
+    if ((r = ensure_capacity(h, std::max<int64_t>(N, 1)))) return r;
+    if ((r = ensure_layer(h, L - 1))) return r;
+    // make every layer at least `cap` wide
+    for (int l = 0; l < L; ++l) {
+        Layer& Ly = h->layers[l];
+        if (Ly.cap < cap) {
+            (void)hipFree(Ly.adj);
+            (void)hipFree(Ly.adjd);
+            Ly.adj = nullptr;
+            Ly.adjd = nullptr;
+            Ly.cap = cap;
+            if ((r = grow(h, Ly.adj, 0, h->capn * cap, 0xFF)) || (r = grow(h, Ly.adjd, 0, h->capn * cap, 0))) return r;
+        }
+    }
+    HIPCHK(h, hipMemcpy(h->keys, keys, N * 8, hipMemcpyHostToDevice));
+    if ((r = ensure_buf(h, h->tmp, (size_t)N * dim))) return r;
+    HIPCHK(h, hipMemcpy(h->tmp.p, vecs, (size_t)N * dim * 4, hipMemcpyHostToDevice));
+    LCHK(h, launch_pad_rows(h->tmp.p, N, dim, h->vecs, h->pitch, h->stream));
+    LCHK(h, launch_norms(h->vecs, 0, N, h->pitch, h->lpr, h->vpl, h->norms, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    std::vector<int32_t> row;
+    h->hlevels.assign(N, 0);
+    for (int l = 0; l < L; ++l) {
+        Layer& Ly = h->layers[l];
+        HIPCHK(h, hipMemcpy(Ly.deg, deg + (size_t)l * N, N * 4, hipMemcpyHostToDevice));
+        row.assign((size_t)N * Ly.cap, -1);
+        Ly.count = 0;
+        for (int64_t i = 0; i < N; ++i) {
+            const int d = deg[(size_t)l * N + i];
+            if (d != -2) {
+                Ly.count++;
+                h->hlevels[i] = std::max(h->hlevels[i], l);
+            }
+            for (int j = 0; j < d && j < cap; ++j) row[(size_t)i * Ly.cap + j] = adj[((size_t)l * N + i) * cap + j];
+        }
+        HIPCHK(h, hipMemcpy(Ly.adj, row.data(), row.size() * 4, hipMemcpyHostToDevice));
+        Ly.entry = entry[l];
+    }
+    HIPCHK(h, hipMemcpy(h->levels, h->hlevels.data(), N * 4, hipMemcpyHostToDevice));
+    h->key2id.clear();
+    for (int64_t i = 0; i < N; ++i)
+        if (!h->key2id.count(keys[i])) h->key2id[keys[i]] = (int32_t)i;
+    h->n = N;
+    h->layers_exist = L > 0;
+    return 0;
+}
+
+int mhnsw_preview_levels(mhnsw_index* h, int64_t n, int32_t* out) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    uint64_t s = h->rng;
+    bool le = h->layers_exist;
+    for (int64_t i = 0; i < n; ++i) {
+        out[i] = random_level(h->ml, le, h->n + i, &s);
+        le = true;
+    }
+    return 0;
+}
+
+int mhnsw_stats(const mhnsw_index* h, int64_t* out, int n) {
+    mhnsw_index* hh = const_cast<mhnsw_index*>(h);
+    unsigned long long d[8];
+    HIPCHK(hh, hipDeviceSynchronize());
+    HIPCHK(hh, hipMemcpy(d, h->d_stats, sizeof(d), hipMemcpyDeviceToHost));
+    const int64_t v[7] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4],
+                          (int64_t)d[5], (int64_t)d[6], h->stats_host[6]};
+    for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
+    return 0;
+}
+
+int mhnsw_reset_stats(mhnsw_index* h) {
+    HIPCHK(h, hipDeviceSynchronize());
+    HIPCHK(h, hipMemset(h->d_stats, 0, 8 * sizeof(unsigned long long)));
+    for (auto& v : h->stats_host) v = 0;
+    return 0;
+}
+
+int mhnsw_last_kernel_ms(mhnsw_index* h, float* ms) {
+    if (!h->have_timing) return fail(h, MHNSW_EINVAL, "no timed search yet");
+    HIPCHK(h, hipEventSynchronize(h->ev1));
+    HIPCHK(h, hipEventElapsedTime(ms, h->ev0, h->ev1));
+    return 0;
+}
+
+int mhnsw_merge_topk_device(const int64_t* keys_in, const float* dist_in, const int32_t* n_in, int shards, int64_t B,
+                            int k, int64_t* out_keys, float* out_dist, int32_t* out_n, void* stream) {
+    int r = launch_merge_topk(keys_in, dist_in, n_in, shards, B, k, out_keys, out_dist, out_n, (hipStream_t)stream);
+    if (r) return fail(nullptr, r == -4 ? MHNSW_EUNSUPPORTED : MHNSW_EDEVICE, "merge launch failed (%d)", r);
+    return 0;
+}
+
+}  // extern "C"

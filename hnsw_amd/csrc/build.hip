@@ -1,0 +1,425 @@
+// build.hip -- insert path (Graph.Add / BatchAdd, graph.go:437-531, 942-1042).
+//
+// k_build_compat: the reference's strictly sequential insert, verbatim
+//   semantics (per-layer compat search with k = M, bidirectional addNeighbor
+//   with "evict the worst of M+1" (graph.go:41-81) and one-directional
+//   replenish from neighbours-of-neighbours ranked by CosineDistance
+//   (graph.go:172-219)).  One wave walks the inserts in order; every distance
+//   batch is spread over the 64 lanes.  Graph state is rewritten while it is
+//   searched, so adjacency goes through relaxed atomics + __syncthreads.
+//
+// k_batch_search / k_batch_commit: throughput insert.  A batch of new nodes is
+//   searched in parallel against the graph as it stood before the batch (one
+//   wave per node, beam search with efConstruction), each node selects its
+//   neighbours (HNSW heuristic or closest-M) and writes its own row; reverse
+//   edges are proposed into per-target slots and committed by one wave per
+//   touched node, keeping the best cap by (distance, id) -- the M-neighbour
+//   selection of graph.go:55-80 generalised to a set of proposals, and
+//   independent of arrival order.
+#include "device_search.hpp"
+#include "engine.hpp"
+
+namespace mh {
+
+__device__ __forceinline__ void build_sync() { __syncthreads(); }
+
+// ---------------------------------------------------------------------------
+// compat build
+// ---------------------------------------------------------------------------
+struct BuildSmem {
+    CompatSmem cs;
+    float* hd;  // replenish heap
+    uint32_t* hi;
+};
+
+template <class C, int G>
+__device__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v) {
+    const int lane = lane_id();
+    const int capl = g.cap[l];
+    int32_t* row = g.adj[l] + (size_t)n * capl;
+    const int d = ld_i32<true>(g.deg[l] + n);
+    if (d <= 0) return;
+    const bool hit = lane < d && (uint32_t)ld_i32<true>(row + lane) == v;
+    const unsigned long long m = __ballot(hit);
+    if (!m) return;
+    const int pos = __ffsll((long long)m) - 1;
+    const int32_t last = ld_i32<true>(row + d - 1);
+    build_sync();
+    if (lane == 0) {
+        st_i32(row + pos, last);
+        st_i32(g.deg[l] + n, d - 1);
+    }
+    build_sync();
+}
+
+// append nw to n's neighbour set if absent; returns the new degree
+__device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw) {
+    const int lane = lane_id();
+    const int capl = g.cap[l];
+    int32_t* row = g.adj[l] + (size_t)n * capl;
+    int d = ld_i32<true>(g.deg[l] + n);
+    if (d < 0) d = 0;  // graph.go:46-48 allocate the map
+    const bool pres = lane < d && (uint32_t)ld_i32<true>(row + lane) == nw;
+    const bool present = __ballot(pres) != 0;
+    build_sync();
+    if (lane == 0) {
+        if (!present) st_i32(row + d, (int32_t)nw);
+        st_i32(g.deg[l] + n, present ? d : d + 1);
+    }
+    build_sync();
+    return present ? d : d + 1;
+}
+
+// graph.go:172-219
+template <class C, int G>
+__device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err) {
+    const int lane = lane_id();
+    const int capl = g.cap[l];
+    int dn = ld_i32<true>(g.deg[l] + n);
+    if (dn < 0) dn = 0;
+    if (dn >= m) return;
+    const int vsize = 1 << S.cs.vlog2, vmask = vsize - 1;
+    vis_clear(S.cs.vis, vsize);
+    build_sync();
+    if (lane == 0) vis_probe(S.cs.vis, vmask, n);  // graph.go:184
+    uint32_t mine = 0xFFFFFFFFu;
+    int64_t key = INT64_MAX;
+    if (lane < dn) {
+        mine = (uint32_t)ld_i32<true>(g.adj[l] + (size_t)n * capl + lane);
+        key = g.keys[mine];
+    }
+    bitonic64(key, mine);
+    if (lane < dn) vis_probe(S.cs.vis, vmask, mine);  // graph.go:187-189
+    QReg<C> q;
+    load_query(q, g.vecs + (size_t)n * g.pitch);
+    const float qn = g.norms[n];
+    GHeap h{S.hd, S.hi, 0};
+    for (int j = 0; j < dn; ++j) {  // graph.go:192-210
+        const uint32_t nb = rl_u(mine, j);
+        const int dnb = ld_i32<true>(g.deg[l] + nb);
+        if (dnb < 0) continue;
+        uint32_t th = 0xFFFFFFFFu;
+        int64_t tk = INT64_MAX;
+        if (lane < dnb) {
+            th = (uint32_t)ld_i32<true>(g.adj[l] + (size_t)nb * capl + lane);
+            tk = g.keys[th];
+        }
+        bitonic64(tk, th);
+        int pr = 0;
+        if (lane < dnb) pr = vis_probe(S.cs.vis, vmask, th);
+        if (__ballot(pr == 2)) err = 1;
+        int cnt;
+        const uint32_t cid = compact(th, pr == 1, cnt);
+        st.E += cnt;
+        eval_list<C, G>(g, q, qn, cid, cnt, COSINE,  // graph.go:204 hard-coded cosine
+                        [&](float d, uint32_t u) { gh_push(h, d, u); });
+    }
+    // graph.go:213-218 (len < m before every add: addNeighbor cannot evict)
+    while (h.n > 0) {
+        int cur = ld_i32<true>(g.deg[l] + n);
+        if (cur < 0) cur = 0;
+        if (cur >= m) break;
+        float bd;
+        uint32_t best;
+        gh_pop(h, bd, best);
+        list_append(g, l, n, best);
+    }
+}
+
+// graph.go:41-81
+template <class C, int G>
+__device__ void add_neighbor(const GraphDev& g, int l, uint32_t n, uint32_t nw, int m, BuildSmem& S, WaveStats& st,
+                             int& err) {
+    const int lane = lane_id();
+    const int capl = g.cap[l];
+    const int d = list_append(g, l, n, nw);
+    if (d <= m) return;
+    uint32_t nb = 0xFFFFFFFFu;
+    int64_t key = INT64_MAX;
+    if (lane < d) {
+        nb = (uint32_t)ld_i32<true>(g.adj[l] + (size_t)n * capl + lane);
+        key = g.keys[nb];
+    }
+    bitonic64(key, nb);  // Go map order -> ascending key
+    QReg<C> q;
+    load_query(q, g.vecs + (size_t)n * g.pitch);
+    const float qn = g.norms[n];
+    float worst_d = -__int_as_float(0x7f800000);
+    uint32_t worst = EMPTY_ID;
+    st.E += d;
+    eval_list<C, G>(g, q, qn, nb, d, g.metric, [&](float dd, uint32_t u) {  // graph.go:60-71
+        if (dd > worst_d || worst == EMPTY_ID) {
+            worst_d = dd;
+            worst = u;
+        }
+    });
+    if (worst == EMPTY_ID) return;
+    list_remove<C, G>(g, l, n, worst);  // graph.go:74
+    if (ld_i32<true>(g.deg[l] + worst) >= 0) list_remove<C, G>(g, l, worst, n);  // graph.go:76-78
+    replenish<C, G>(g, l, worst, m, S, st, err);  // graph.go:79
+}
+
+template <class C, int G>
+__global__ __launch_bounds__(64) void k_build_compat(CompatBuildArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int lane = lane_id();
+    const int vsize = 1 << a.vis_log2;
+    BuildSmem S;
+    S.cs.vis = smem;
+    S.cs.vlog2 = a.vis_log2;
+    uint32_t* p = smem + vsize;
+    S.cs.cd = reinterpret_cast<float*>(p);
+    p += a.ef + 2;
+    S.cs.ci = p;
+    p += a.ef + 2;
+    S.cs.rd = reinterpret_cast<float*>(p);
+    p += a.M + 2;
+    S.cs.ri = p;
+    p += a.M + 2;
+    const int hcap = a.M * (a.M + 1) + 2;
+    S.hd = reinterpret_cast<float*>(p);
+    p += hcap;
+    S.hi = p;
+    WaveStats st;
+    int err = 0;
+    int top = -1;
+    for (int64_t i = 0; i < a.n0; ++i) top = max(top, a.levels[i]);
+    for (int64_t i = a.n0; i < a.n1; ++i) {
+        const uint32_t id = (uint32_t)i;
+        const int level = a.levels[i];
+        top = max(top, level);
+        QReg<C> q;
+        load_query(q, a.g.vecs + (size_t)id * a.g.pitch);
+        const float qn = a.g.norms[id];
+        uint32_t elevator = EMPTY_ID;
+        for (int l = top; l >= 0; --l) {  // graph.go:475
+            const int32_t ent = a.layer_entry[l];
+            if (ent == (int32_t)id) {  // graph.go:485-488: empty layer, no search
+                build_sync();
+                if (lane == 0) st_i32(a.g.deg[l] + id, -1);
+                build_sync();
+                continue;
+            }
+            const uint32_t sp = elevator != EMPTY_ID ? elevator : (uint32_t)ent;  // graph.go:492-498
+            const int cnt = compat_layer<C, G, true>(a.g, l, sp, a.M, a.ef, q, qn, S.cs, st, err);  // :500
+            if (cnt == 0) {
+                err |= 2;
+                break;
+            }
+            elevator = S.cs.ri[0];  // graph.go:508
+            if (level >= l) {       // graph.go:510-521
+                const uint32_t nbh = lane < cnt ? S.cs.ri[lane] : 0u;
+                build_sync();
+                if (lane == 0) st_i32(a.g.deg[l] + id, -1);
+                build_sync();
+                for (int j = 0; j < cnt; ++j) {
+                    const uint32_t c = rl_u(nbh, j);
+                    add_neighbor<C, G>(a.g, l, c, id, a.M, S, st, err);
+                    add_neighbor<C, G>(a.g, l, id, c, a.M, S, st, err);
+                }
+            }
+        }
+        if (err) break;
+    }
+    if (lane == 0) {
+        atomicAdd(&a.stats[0], st.E);
+        atomicAdd(&a.stats[1], st.X);
+        if (err) atomicOr(a.err, err);
+    }
+}
+
+template <class C, int G>
+static int launch_build_compat_t(const CompatBuildArgs& a, hipStream_t s) {
+    const size_t words = ((size_t)1 << a.vis_log2) + 2 * (size_t)(a.ef + 2) + 2 * (size_t)(a.M + 2) +
+                         2 * (size_t)(a.M * (a.M + 1) + 2);
+    const size_t lds = words * 4;
+    if (lds > 160 * 1024) return -2;
+    hipLaunchKernelGGL((k_build_compat<C, G>), dim3(1), dim3(64), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------
+// batched build
+// ---------------------------------------------------------------------------
+template <class C, int R, int G>
+__global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int64_t u64 = a.n0 + blockIdx.x;
+    if (u64 >= a.n1) return;
+    const uint32_t u = (uint32_t)u64;
+    const int lane = lane_id();
+    const int l = a.layer;
+    WaveStats st;
+    QReg<C> q;
+    load_query(q, a.g.vecs + (size_t)u * a.g.pitch);
+    const float qn = a.g.norms[u];
+    const uint32_t ep = a.cur_entry[u];
+    if (a.levels[u] < l) {  // above the node's level: greedy descent only
+        BList<1> L1;
+        beam_layer<C, 1, G>(a.g, l, ep, 1, q, qn, L1, smem, a.vis_log2, st);
+        float d;
+        uint32_t id;
+        bl_at(L1, 0, d, id);
+        if (lane == 0 && id != EMPTY_ID) a.cur_entry[u] = id & ID_MASK;
+    } else {
+        BList<R> L;
+        beam_layer<C, R, G>(a.g, l, ep, a.ef, q, qn, L, smem, a.vis_log2, st);
+        float d0;
+        uint32_t i0;
+        bl_at(L, 0, d0, i0);
+        if (lane == 0 && i0 != EMPTY_ID) a.cur_entry[u] = i0 & ID_MASK;
+        // neighbour selection
+        uint32_t sel = 0;
+        float seld = 0.f;
+        int nsel = 0;
+        const int nl = a.ef;
+        for (int i = 0; i < nl && nsel < a.mcap; ++i) {
+            float dc;
+            uint32_t c;
+            bl_at(L, i, dc, c);
+            if (c == EMPTY_ID) break;
+            c &= ID_MASK;
+            bool good = true;
+            if (a.heuristic && nsel > 0) {  // HNSW Alg. 4: drop c if closer to a kept neighbour than to u
+                QReg<C> qc;
+                load_query(qc, a.g.vecs + (size_t)c * a.g.pitch);
+                const float cn = a.g.norms[c];
+                st.E += nsel;
+                eval_list<C, G>(a.g, qc, cn, sel, nsel, a.g.metric, [&](float dcs, uint32_t) {
+                    if (dcs < dc) good = false;
+                });
+            }
+            if (good) {
+                if (lane == nsel) {
+                    sel = c;
+                    seld = dc;
+                }
+                ++nsel;
+            }
+        }
+        const int capl = a.g.cap[l];
+        if (lane < nsel) {
+            a.g.adj[l][(size_t)u * capl + lane] = (int32_t)sel;
+            a.g.adjd[l][(size_t)u * capl + lane] = seld;
+            const int slot = atomicAdd(&a.inc_cnt[sel], 1);
+            if (slot < a.inc_cap) {
+                a.inc_src[(size_t)sel * a.inc_cap + slot] = u;
+                a.inc_dist[(size_t)sel * a.inc_cap + slot] = seld;
+            } else {
+                atomicAdd(&a.stats[2], 1ull);
+            }
+            if (slot == 0) {
+                const int t = atomicAdd(a.touched_cnt, 1);
+                a.touched[t] = sel;
+            }
+        }
+        if (lane == 0) a.g.deg[l][u] = nsel;
+    }
+    if (lane == 0) {
+        atomicAdd(&a.stats[0], st.E);
+        atomicAdd(&a.stats[1], st.X);
+    }
+}
+
+// one wave per touched node: keep the best cap of (existing U proposals) by (dist, id)
+__global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
+    __shared__ float sd[128];
+    __shared__ uint32_t si[128];
+    const int lane = lane_id();
+    const int n_t = *a.touched_cnt;
+    if ((int)blockIdx.x >= n_t) return;
+    const uint32_t v = a.touched[blockIdx.x];
+    const int l = a.layer;
+    const int capl = a.g.cap[l];
+    int d = a.g.deg[l][v];
+    if (d < 0) d = 0;
+    int nin = a.inc_cnt[v];
+    if (nin > a.inc_cap) nin = a.inc_cap;
+    const int tot = d + nin;
+    for (int e = lane; e < 128; e += 64) {
+        float dd = __int_as_float(0x7f800000);
+        uint32_t ii = EMPTY_ID;
+        if (e < d) {
+            ii = (uint32_t)a.g.adj[l][(size_t)v * capl + e];
+            dd = a.g.adjd[l][(size_t)v * capl + e];
+        } else if (e < tot) {
+            ii = a.inc_src[(size_t)v * a.inc_cap + (e - d)];
+            dd = a.inc_dist[(size_t)v * a.inc_cap + (e - d)];
+        }
+        sd[e] = dd;
+        si[e] = ii;
+    }
+    __syncthreads();
+    int rank[2] = {0, 0};
+    float md[2];
+    uint32_t mi[2];
+    for (int h = 0; h < 2; ++h) {
+        md[h] = sd[lane + 64 * h];
+        mi[h] = si[lane + 64 * h];
+    }
+    for (int e = 0; e < tot; ++e) {
+        const float od = sd[e];
+        const uint32_t oi = si[e];
+        for (int h = 0; h < 2; ++h) rank[h] += lt_di(od, oi, md[h], mi[h]) ? 1 : 0;
+    }
+    const int keep = tot < capl ? tot : capl;
+    for (int h = 0; h < 2; ++h) {
+        const int e = lane + 64 * h;
+        if (e < tot && rank[h] < keep) {
+            a.g.adj[l][(size_t)v * capl + rank[h]] = (int32_t)mi[h];
+            a.g.adjd[l][(size_t)v * capl + rank[h]] = md[h];
+        }
+    }
+    if (lane == 0) {
+        a.g.deg[l][v] = keep;
+        a.inc_cnt[v] = 0;
+    }
+}
+
+template <class C, int R, int G>
+static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
+    const size_t lds = (size_t)4 << a.vis_log2;
+    const int64_t n = a.n1 - a.n0;
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL((k_batch_search<C, R, G>), dim3((unsigned)n), dim3(64), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+#define MH_FOR_EACH_CFG(X) \
+    X(16, 1, 2)            \
+    X(32, 1, 4)            \
+    X(64, 1, 8)            \
+    X(64, 2, 8)            \
+    X(64, 3, 8)            \
+    X(64, 4, 4)            \
+    X(64, 6, 4)            \
+    X(64, 8, 2)
+
+int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, hipStream_t s) {
+#define X_(L, V, G) \
+    if (lpr == L && vpl == V) return launch_build_compat_t<Cfg<L, V>, G>(a, s);
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return -3;
+}
+
+int launch_build_batch_search(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s) {
+#define X_(L, V, G)                                                          \
+    if (lpr == L && vpl == V) {                                              \
+        if (a.ef <= 64) return launch_batch_search_t<Cfg<L, V>, 1, G>(a, s); \
+        if (a.ef <= 128) return launch_batch_search_t<Cfg<L, V>, 2, G>(a, s); \
+        if (a.ef <= 256) return launch_batch_search_t<Cfg<L, V>, 4, G>(a, s); \
+        return -4;                                                           \
+    }
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return -3;
+}
+
+int launch_build_batch_commit(const BatchBuildArgs& a, int64_t max_touched, hipStream_t s) {
+    if (max_touched <= 0) return 0;
+    hipLaunchKernelGGL(k_batch_commit, dim3((unsigned)max_touched), dim3(64), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace mh

@@ -1,0 +1,428 @@
+// device_common.hpp -- wave64 building blocks shared by every HIP kernel of the
+// engine (gfx950 / CDNA4 only).
+//
+//  * Row-distance engine: one query held in VGPRs (float4 per lane), candidate
+//    rows gathered straight from the row-major HBM vector store with 16-B
+//    coalesced loads (a 768-d row = 3 x 1 KiB wave-instructions), per-lane
+//    fmaf accumulation, then a transposed reduce-scatter over the lanes of a
+//    row so that G rows finish in log2(lanes) shuffle steps instead of G*6.
+//    The summation tree is the canonical order restated in oracle/oracle.c
+//    (og_dev_sum): element e -> lane (e/4) mod 64, fmaf in ascending e,
+//    butterfly over offsets 32..1 -- so distances are bitwise reproducible.
+//  * Sorted candidate list across lanes (ef <= 64*R entries, R per lane),
+//    ballot/popcount insertion, used by beam search and top-k merges.
+//  * LDS open-addressing visited set (CAS probes, bounded).
+//  * Go container/heap restatement on LDS arrays (compat semantics,
+//    heap/heap.go + graph.go:94-170), executed redundantly by every lane.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MH_MAXL 32
+
+namespace mh {
+
+constexpr uint32_t ID_MASK = 0x7FFFFFFFu;
+constexpr uint32_t EXP_BIT = 0x80000000u;
+constexpr uint32_t EMPTY_ID = 0x7FFFFFFFu;
+constexpr uint32_t VIS_EMPTY = 0xFFFFFFFFu;
+
+enum Metric { COSINE = 0, EUCLIDEAN = 1 };
+
+struct GraphDev {
+    const float* vecs;   // [cap_nodes * pitch] row-major, zero padded
+    const float* norms;  // [cap_nodes] canonical |x|
+    const int64_t* keys; // [cap_nodes]
+    int32_t* deg[MH_MAXL];  // per layer [cap_nodes]: -2 absent, -1 nil map, >=0 degree
+    int32_t* adj[MH_MAXL];  // per layer [cap_nodes * cap[l]] internal ids
+    float* adjd[MH_MAXL];   // per layer [cap_nodes * cap[l]] edge distances (batch build)
+    int cap[MH_MAXL];
+    int pitch;
+    int dim;
+    int metric;
+    int nlayers;
+};
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ float rl_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ uint32_t rl_u(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ int rl_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ int64_t rl_i64(int64_t v, int l) {
+    int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, l);
+    int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ uint32_t shfl_u(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
+__device__ __forceinline__ int64_t shfl_xor_i64(int64_t v, int m) {
+    int lo = __shfl_xor((int)(uint32_t)(uint64_t)v, m, 64);
+    int hi = __shfl_xor((int)(uint32_t)((uint64_t)v >> 32), m, 64);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+// push-style permute: lane l's value lands in lane dst(l)
+__device__ __forceinline__ uint32_t push_to(uint32_t v, int dst) {
+    return (uint32_t)__builtin_amdgcn_ds_permute(dst << 2, (int)v);
+}
+
+__device__ __forceinline__ bool lt_di(float d1, uint32_t i1, float d2, uint32_t i2) {
+    return d1 < d2 || (d1 == d2 && i1 < i2);
+}
+
+constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x >> 1); }
+
+// ---------------------------------------------------------------------------
+// dimension configuration: LPR lanes per row, VPL float4 per lane
+// ---------------------------------------------------------------------------
+template <int LPR_, int VPL_>
+struct Cfg {
+    static constexpr int LPR = LPR_;
+    static constexpr int VPL = VPL_;
+    static constexpr int RPI = 64 / LPR_;          // rows per wave-instruction
+    static constexpr int PITCH = LPR_ * 4 * VPL_;  // floats per stored row
+    static constexpr int LOG_LPR = ilog2(LPR_);
+};
+
+template <class C>
+struct QReg {
+    float4 v[C::VPL];
+};
+
+template <class C>
+__device__ __forceinline__ void load_query(QReg<C>& q, const float* qp) {
+    const int sub = lane_id() & (C::LPR - 1);
+#pragma unroll
+    for (int v = 0; v < C::VPL; ++v) q.v[v] = *reinterpret_cast<const float4*>(qp + sub * 4 + v * C::LPR * 4);
+}
+
+// butterfly within an LPR-lane segment, offsets LPR/2 .. 1 (canonical tree; the
+// 64-lane levels above LPR only ever add +0.0f for d <= 4*LPR)
+template <int LPR>
+__device__ __forceinline__ float seg_allreduce(float x) {
+#pragma unroll
+    for (int o = LPR / 2; o >= 1; o >>= 1) x = x + __shfl_xor(x, o, 64);
+    return x;
+}
+
+template <class C>
+__device__ __forceinline__ float query_norm(const QReg<C>& q) {
+    float acc = 0.f;
+#pragma unroll
+    for (int v = 0; v < C::VPL; ++v) {
+        acc = fmaf(q.v[v].x, q.v[v].x, acc);
+        acc = fmaf(q.v[v].y, q.v[v].y, acc);
+        acc = fmaf(q.v[v].z, q.v[v].z, acc);
+        acc = fmaf(q.v[v].w, q.v[v].w, acc);
+    }
+    return sqrtf(seg_allreduce<C::LPR>(acc));
+}
+
+// Transposed reduce-scatter of G per-lane partials over an LPR-lane segment.
+// On return lane l holds the full sum of row g(l) = (l % LPR) >> (LOG_LPR - log2 G).
+template <int G, int LPR>
+__device__ __forceinline__ float reduce_rows(float (&p)[G]) {
+    static_assert(G >= 1 && G <= LPR && (G & (G - 1)) == 0, "G must be a power of two <= LPR");
+    const int lane = lane_id();
+#pragma unroll
+    for (int s = 0; (LPR >> (s + 1)) >= 1; ++s) {
+        const int o = LPR >> (s + 1);
+        const int cnt = G >> s;
+        if (cnt > 1) {
+            const int half = cnt >> 1;
+            const bool up = (lane & o) != 0;
+#pragma unroll
+            for (int i = 0; i < half; ++i) {
+                float send = up ? p[i] : p[i + half];
+                float keep = up ? p[i + half] : p[i];
+                p[i] = keep + __shfl_xor(send, o, 64);
+            }
+        } else {
+            p[0] = p[0] + __shfl_xor(p[0], o, 64);
+        }
+    }
+    return p[0];
+}
+
+template <class C, int G>
+struct RowMap {
+    static constexpr int LG = ilog2(G);
+    static constexpr int T = G * C::RPI;  // rows per group
+    // row-in-group index that lane l owns after reduce_rows
+    __device__ static __forceinline__ int owned_row(int l) {
+        const int g = (l & (C::LPR - 1)) >> (C::LOG_LPR - LG);
+        return g * C::RPI + l / C::LPR;
+    }
+    // lane that owns row t of the group
+    __device__ static __forceinline__ int owner(int t) {
+        const int g = t / C::RPI, s = t % C::RPI;
+        return s * C::LPR + (g << (C::LOG_LPR - LG));
+    }
+    // row-in-group index that register g of lane l computes
+    __device__ static __forceinline__ int reg_row(int g, int l) { return g * C::RPI + l / C::LPR; }
+};
+
+// Evaluate up to T = G*RPI rows.  row_id(t) supplies the internal id of row t
+// (t < n); returns, in every lane, the canonical dot (or squared L2) sum of the
+// row the lane owns (RowMap::owned_row).
+template <class C, int G, bool L2>
+__device__ __forceinline__ float eval_rows(const QReg<C>& q, const float* __restrict__ X, int pitch,
+                                           const uint32_t (&ids)[G], const bool (&valid)[G]) {
+    const int sub = lane_id() & (C::LPR - 1);
+    float4 x[G][C::VPL];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const float* rp = X + (size_t)ids[g] * (size_t)pitch + sub * 4;
+#pragma unroll
+        for (int v = 0; v < C::VPL; ++v) {
+            if (valid[g])
+                x[g][v] = *reinterpret_cast<const float4*>(rp + v * C::LPR * 4);
+            else
+                x[g][v] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    float p[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        float acc = 0.f;
+#pragma unroll
+        for (int v = 0; v < C::VPL; ++v) {
+            if (L2) {
+                float t0 = x[g][v].x - q.v[v].x, t1 = x[g][v].y - q.v[v].y;
+                float t2 = x[g][v].z - q.v[v].z, t3 = x[g][v].w - q.v[v].w;
+                acc = fmaf(t0, t0, acc);
+                acc = fmaf(t1, t1, acc);
+                acc = fmaf(t2, t2, acc);
+                acc = fmaf(t3, t3, acc);
+            } else {
+                acc = fmaf(x[g][v].x, q.v[v].x, acc);
+                acc = fmaf(x[g][v].y, q.v[v].y, acc);
+                acc = fmaf(x[g][v].z, q.v[v].z, acc);
+                acc = fmaf(x[g][v].w, q.v[v].w, acc);
+            }
+        }
+        p[g] = acc;
+    }
+    return reduce_rows<G, C::LPR>(p);
+}
+
+// finalize a canonical sum into a distance (distance.go:15-23 semantics)
+__device__ __forceinline__ float finalize(int metric, float s, float xn, float qn) {
+    if (metric == COSINE) return 1.0f - s / (xn * qn);
+    return sqrtf(s);
+}
+
+// ---------------------------------------------------------------------------
+// LDS visited set
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void vis_clear(uint32_t* tab, int size) {
+    uint4* t4 = reinterpret_cast<uint4*>(tab);
+    const uint4 e = make_uint4(VIS_EMPTY, VIS_EMPTY, VIS_EMPTY, VIS_EMPTY);
+    for (int i = lane_id(); i < size / 4; i += 64) t4[i] = e;
+}
+
+// 0 = already visited, 1 = newly recorded, 2 = table congested (not recorded)
+__device__ __forceinline__ int vis_probe(uint32_t* tab, int mask, uint32_t id) {
+    uint32_t h = (id * 0x9E3779B1u) ^ (id >> 15);
+    h &= (uint32_t)mask;
+#pragma unroll 1
+    for (int p = 0; p < 48; ++p) {
+        uint32_t old = atomicCAS(&tab[h], VIS_EMPTY, id);
+        if (old == VIS_EMPTY) return 1;
+        if (old == id) return 0;
+        h = (h + 1) & (uint32_t)mask;
+    }
+    return 2;
+}
+
+// ---------------------------------------------------------------------------
+// sorted list across lanes: entry index i = r*64 + lane, ordered by (d, id)
+// ---------------------------------------------------------------------------
+template <int R>
+struct BList {
+    float d[R];
+    uint32_t i[R];  // id | EXP_BIT when expanded; EMPTY_ID when empty
+};
+
+template <int R>
+__device__ __forceinline__ void bl_init(BList<R>& L) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        L.d[r] = __int_as_float(0x7f800000);
+        L.i[r] = EMPTY_ID;
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void bl_at(const BList<R>& L, int idx, float& d, uint32_t& id) {
+    const int rr = idx >> 6, ll = idx & 63;
+    d = __int_as_float(0x7f800000);
+    id = EMPTY_ID;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (r == rr) {
+            d = rl_f(L.d[r], ll);
+            id = rl_u(L.i[r], ll);
+        }
+}
+
+// insert (d,u) keeping the best `ef` entries; returns true when inserted
+template <int R>
+__device__ __forceinline__ bool bl_insert(BList<R>& L, int ef, float d, uint32_t u) {
+    if (!(d == d)) return false;  // NaN never enters the list
+    float wd;
+    uint32_t wi;
+    bl_at(L, ef - 1, wd, wi);
+    if (!lt_di(d, u, wd, wi & ID_MASK)) return false;
+    bool dup = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) dup |= ((L.i[r] & ID_MASK) == u);
+    if (__ballot(dup)) return false;
+    int pos = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) pos += __popcll(__ballot(lt_di(L.d[r], L.i[r] & ID_MASK, d, u)));
+    const int lane = lane_id();
+    float pd[R];
+    uint32_t pi[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        pd[r] = __shfl_up(L.d[r], 1, 64);
+        pi[r] = (uint32_t)__shfl_up((int)L.i[r], 1, 64);
+        if (r > 0) {
+            float cd = rl_f(L.d[r - 1], 63);
+            uint32_t ci = rl_u(L.i[r - 1], 63);
+            if (lane == 0) {
+                pd[r] = cd;
+                pi[r] = ci;
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int idx = r * 64 + lane;
+        if (idx > pos) {
+            L.d[r] = pd[r];
+            L.i[r] = pi[r];
+        } else if (idx == pos) {
+            L.d[r] = d;
+            L.i[r] = u;
+        }
+        if (idx >= ef) {
+            L.d[r] = __int_as_float(0x7f800000);
+            L.i[r] = EMPTY_ID;
+        }
+    }
+    return true;
+}
+
+// pick the first unexpanded entry, mark it expanded; returns EMPTY_ID if none
+template <int R>
+__device__ __forceinline__ uint32_t bl_next(BList<R>& L) {
+    const int lane = lane_id();
+    int sel_r = -1, sel_l = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        unsigned long long m = __ballot(((L.i[r] & EXP_BIT) == 0) && (L.i[r] != EMPTY_ID));
+        if (sel_r < 0 && m) {
+            sel_r = r;
+            sel_l = __ffsll((long long)m) - 1;
+        }
+    }
+    if (sel_r < 0) return EMPTY_ID;
+    uint32_t id = EMPTY_ID;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (r == sel_r) {
+            id = rl_u(L.i[r], sel_l);
+            if (lane == sel_l) L.i[r] |= EXP_BIT;
+        }
+    return id;
+}
+
+// ---------------------------------------------------------------------------
+// Go container/heap on LDS arrays (heap/heap.go + container/heap), executed
+// identically by every lane (uniform control flow, same-address LDS traffic).
+// ---------------------------------------------------------------------------
+struct GHeap {
+    float* d;
+    uint32_t* id;
+    int n;
+};
+
+__device__ __forceinline__ bool gh_less(const GHeap& h, int i, int j) { return h.d[i] < h.d[j]; }
+__device__ __forceinline__ void gh_swap(GHeap& h, int i, int j) {
+    float td = h.d[i];
+    uint32_t ti = h.id[i];
+    float jd = h.d[j];
+    uint32_t ji = h.id[j];
+    h.d[i] = jd;
+    h.id[i] = ji;
+    h.d[j] = td;
+    h.id[j] = ti;
+}
+__device__ __forceinline__ void gh_up(GHeap& h, int j) {
+    for (;;) {
+        int i = (j - 1) / 2;
+        if (i == j || !gh_less(h, j, i)) break;
+        gh_swap(h, i, j);
+        j = i;
+    }
+}
+__device__ __forceinline__ bool gh_down(GHeap& h, int i0, int n) {
+    int i = i0;
+    for (;;) {
+        int j1 = 2 * i + 1;
+        if (j1 >= n || j1 < 0) break;
+        int j = j1;
+        int j2 = j1 + 1;
+        if (j2 < n && gh_less(h, j2, j1)) j = j2;
+        if (!gh_less(h, j, i)) break;
+        gh_swap(h, i, j);
+        i = j;
+    }
+    return i > i0;
+}
+__device__ __forceinline__ void gh_push(GHeap& h, float d, uint32_t id) {
+    h.d[h.n] = d;
+    h.id[h.n] = id;
+    h.n++;
+    gh_up(h, h.n - 1);
+}
+__device__ __forceinline__ void gh_pop(GHeap& h, float& d, uint32_t& id) {
+    int n = h.n - 1;
+    gh_swap(h, 0, n);
+    gh_down(h, 0, n);
+    h.n--;
+    d = h.d[h.n];
+    id = h.id[h.n];
+}
+// PopLast == Remove(Len()-1): i == n, no swap (heap/heap.go:73-81)
+__device__ __forceinline__ void gh_poplast(GHeap& h) { h.n--; }
+
+// ---------------------------------------------------------------------------
+// bitonic sort of (key, id) across the 64 lanes, ascending
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void bitonic64(int64_t& key, uint32_t& id) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            int64_t ok = shfl_xor_i64(key, j);
+            uint32_t oi = (uint32_t)__shfl_xor((int)id, j, 64);
+            const bool take_min = ((lane & j) == 0) == ((lane & k) == 0);
+            const bool other_less = ok < key || (ok == key && oi < id);
+            if (take_min == other_less) {
+                key = ok;
+                id = oi;
+            }
+        }
+    }
+}
+
+}  // namespace mh

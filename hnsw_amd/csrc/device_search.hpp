@@ -1,0 +1,195 @@
+// device_search.hpp -- per-wave layer searches shared by the search kernels
+// (search.hip) and the build kernels (build.hip).
+//
+//   beam_layer   : sorted-list best-first search (standard HNSW Alg. 2 stop
+//                  rule), restated in oracle/oracle.c beam_layer_search.
+//   compat_layer : graph.go:94-170 layerNode.search with the reference's heap
+//                  quirks (Max()/PopLast() act on the last array slot, result
+//                  in heap order, greedy stop), restated in oracle/oracle.c
+//                  compat_layer_search.
+#pragma once
+#include "device_common.hpp"
+
+namespace mh {
+
+// Loads of mutable graph state.  COH = true inside the single-workgroup build
+// kernel, which rewrites adjacency while searching: relaxed atomics keep the
+// compiler off the (incoherent) scalar cache; __syncthreads orders lanes.
+template <bool COH>
+__device__ __forceinline__ int32_t ld_i32(const int32_t* p) {
+    if constexpr (COH)
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else
+        return *p;
+}
+__device__ __forceinline__ void st_i32(int32_t* p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Evaluate the distances of candidate ids held in lanes 0..cnt-1 of `cid`
+// against the query; sink(dist, id) is called in row order (uniformly).
+template <class C, int G, class Sink>
+__device__ __forceinline__ void eval_list(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int cnt,
+                                          int metric, Sink&& sink) {
+    using RM = RowMap<C, G>;
+    const int lane = lane_id();
+    for (int base = 0; base < cnt; base += RM::T) {
+        uint32_t ids[G];
+        bool valid[G];
+#pragma unroll
+        for (int gg = 0; gg < G; ++gg) {
+            const int t = base + RM::reg_row(gg, lane);
+            valid[gg] = t < cnt;
+            if constexpr (C::RPI == 1)
+                ids[gg] = rl_u(cid, (base + gg) & 63);
+            else
+                ids[gg] = shfl_u(cid, t & 63);
+            if (!valid[gg]) ids[gg] = 0;
+        }
+        float s;
+        if (metric == EUCLIDEAN)
+            s = eval_rows<C, G, true>(q, g.vecs, g.pitch, ids, valid);
+        else
+            s = eval_rows<C, G, false>(q, g.vecs, g.pitch, ids, valid);
+        const int town = base + RM::owned_row(lane);
+        const uint32_t idown = shfl_u(cid, town & 63);
+        float xn = 1.f;
+        if (metric == COSINE && town < cnt) xn = g.norms[idown];
+        const float dist = finalize(metric, s, xn, qn);
+#pragma unroll
+        for (int t = 0; t < RM::T; ++t) {
+            if (base + t >= cnt) break;
+            sink(rl_f(dist, RM::owner(t)), rl_u(cid, (base + t) & 63));
+        }
+    }
+}
+
+// compact the lanes where `keep` holds into lanes 0..popc-1 (order preserving)
+__device__ __forceinline__ uint32_t compact(uint32_t v, bool keep, int& cnt) {
+    const unsigned long long m = __ballot(keep);
+    cnt = __popcll(m);
+    const int lane = lane_id();
+    const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+    const int dst = keep ? before : cnt + (lane - before);
+    return push_to(v, dst);
+}
+
+struct WaveStats {
+    unsigned long long E = 0, X = 0, resets = 0;
+};
+
+// ---------------------------------------------------------------------------
+// beam: sorted list of <= ef entries; stop when every entry is expanded
+// ---------------------------------------------------------------------------
+template <class C, int R, int G, bool COH = false>
+__device__ void beam_layer(const GraphDev& g, int layer, uint32_t entry, int ef, const QReg<C>& q, float qn,
+                           BList<R>& L, uint32_t* vis, int vlog2, WaveStats& st) {
+    const int lane = lane_id();
+    const int vsize = 1 << vlog2, vmask = vsize - 1;
+    bl_init(L);
+    if (entry == EMPTY_ID) return;
+    vis_clear(vis, vsize);
+    __syncthreads();
+    if (lane == 0) vis_probe(vis, vmask, entry);
+    int vcount = 1;
+    eval_list<C, G>(g, q, qn, entry, 1, g.metric, [&](float d, uint32_t u) { bl_insert(L, ef, d, u); });
+    st.E += 1;
+    const int32_t* degp = g.deg[layer];
+    const int32_t* adjp = g.adj[layer];
+    const int capl = g.cap[layer];
+    for (;;) {
+        const uint32_t cur = bl_next(L);
+        if (cur == EMPTY_ID) break;
+        st.X += 1;
+        const int deg = ld_i32<COH>(degp + cur);
+        if (deg <= 0) continue;
+        const bool have = lane < deg;
+        uint32_t nb = 0;
+        if (have) nb = (uint32_t)ld_i32<COH>(adjp + (size_t)cur * capl + lane);
+        int pr = 0;
+        if (have && nb != 0xFFFFFFFFu) pr = vis_probe(vis, vmask, nb);
+        vcount += __popcll(__ballot(pr == 1));
+        int cnt;
+        const uint32_t cid = compact(nb, pr != 0, cnt);
+        if (cnt == 0) continue;
+        st.E += cnt;
+        eval_list<C, G>(g, q, qn, cid, cnt, g.metric, [&](float d, uint32_t u) { bl_insert(L, ef, d, u); });
+        if (vcount > (vsize >> 1) + (vsize >> 2)) {  // forget: results unchanged
+            __syncthreads();
+            vis_clear(vis, vsize);
+            __syncthreads();
+            vcount = 0;
+            st.resets += 1;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// compat: graph.go:94-170 verbatim semantics on LDS Go-heaps
+// ---------------------------------------------------------------------------
+struct CompatSmem {
+    uint32_t* vis;
+    int vlog2;
+    float* cd;
+    uint32_t* ci;  // candidates heap [ef+2]
+    float* rd;
+    uint32_t* ri;  // result heap [k+2]
+};
+
+template <class C, int G, bool COH = false>
+__device__ int compat_layer(const GraphDev& g, int layer, uint32_t entry, int k, int ef, const QReg<C>& q, float qn,
+                            CompatSmem& S, WaveStats& st, int& err) {
+    const int lane = lane_id();
+    if (entry == EMPTY_ID) return 0;
+    const int vsize = 1 << S.vlog2, vmask = vsize - 1;
+    vis_clear(S.vis, vsize);
+    __syncthreads();
+    GHeap cand{S.cd, S.ci, 0}, res{S.rd, S.ri, 0};
+    float d0 = 0.f;
+    eval_list<C, G>(g, q, qn, entry, 1, g.metric, [&](float d, uint32_t) { d0 = d; });  // graph.go:112
+    st.E += 1;
+    if (lane == 0) vis_probe(S.vis, vmask, entry);  // graph.go:123
+    gh_push(cand, d0, entry);                        // graph.go:109-114
+    gh_push(res, cand.d[0], cand.id[0]);             // graph.go:122
+    const int32_t* degp = g.deg[layer];
+    const int32_t* adjp = g.adj[layer];
+    const int capl = g.cap[layer];
+    while (cand.n > 0) {
+        float cdist;
+        uint32_t cur;
+        gh_pop(cand, cdist, cur);  // graph.go:127
+        bool improved = false;
+        const int deg = ld_i32<COH>(degp + cur);
+        if (deg < 0) continue;  // graph.go:131-133 (nil neighbor map)
+        st.X += 1;
+        const bool have = lane < deg;
+        uint32_t nb = 0xFFFFFFFFu;
+        int64_t key = INT64_MAX;
+        if (have) {
+            nb = (uint32_t)ld_i32<COH>(adjp + (size_t)cur * capl + lane);
+            key = g.keys[nb];
+        }
+        bitonic64(key, nb);  // graph.go:137-138 ascending key order
+        int pr = 0;
+        if (lane < deg) pr = vis_probe(S.vis, vmask, nb);  // graph.go:141-144
+        if (__ballot(pr == 2)) err = 1;                   // exact visited set required here
+        int cnt;
+        const uint32_t cid = compact(nb, pr == 1, cnt);
+        st.E += cnt;
+        eval_list<C, G>(g, q, qn, cid, cnt, g.metric, [&](float dist, uint32_t u) {  // graph.go:146-159
+            improved = improved || (res.n > 0 && dist < res.d[0]);
+            if (res.n < k) {
+                gh_push(res, dist, u);
+            } else if (dist < res.d[res.n - 1]) {
+                gh_poplast(res);
+                gh_push(res, dist, u);
+            }
+            gh_push(cand, dist, u);
+            if (cand.n > ef) gh_poplast(cand);
+        });
+        if (!improved && res.n >= k) break;  // graph.go:164-166
+    }
+    return res.n;
+}
+
+}  // namespace mh

@@ -1,0 +1,110 @@
+// engine.hpp -- host-side launch interface between the C ABI (api.cpp) and the
+// HIP kernels (search.hip, build.hip, exact.hip).  No torch types anywhere.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_common.hpp"
+
+namespace mh {
+
+// supported dimension configurations (lanes per row, float4 per lane)
+struct DimCfgId {
+    int lpr, vpl;
+};
+inline bool pick_cfg(int dim, int& lpr, int& vpl) {
+    if (dim <= 0) return false;
+    if (dim <= 64) { lpr = 16; vpl = 1; return true; }
+    if (dim <= 128) { lpr = 32; vpl = 1; return true; }
+    if (dim <= 256) { lpr = 64; vpl = 1; return true; }
+    if (dim <= 512) { lpr = 64; vpl = 2; return true; }
+    if (dim <= 768) { lpr = 64; vpl = 3; return true; }
+    if (dim <= 1024) { lpr = 64; vpl = 4; return true; }
+    if (dim <= 1536) { lpr = 64; vpl = 6; return true; }
+    if (dim <= 2048) { lpr = 64; vpl = 8; return true; }
+    return false;
+}
+inline int pitch_of(int lpr, int vpl) { return lpr * 4 * vpl; }
+
+struct SearchArgs {
+    GraphDev g;
+    const float* q;  // padded queries [B * pitch]
+    int64_t B;
+    int k, ef, top;
+    uint32_t entry;               // top-layer entry (internal id)
+    const int32_t* layer_entry;   // [nlayers] policy entry per layer (compat)
+    int64_t* out_keys;            // [B*k]
+    float* out_dist;              // [B*k]
+    int32_t* out_n;               // [B]
+    int32_t* out_ids;             // [B*k] internal ids (nullable)
+    unsigned long long* stats;    // [0]=dist evals [1]=expansions [2]=visited resets
+    int* err;                     // set to nonzero on visited overflow (compat)
+    int vis_log2;
+};
+
+int launch_pad_rows(const float* src, int64_t n, int dim, float* dst, int pitch, hipStream_t s);
+int launch_norms(const float* X, int64_t n0, int64_t n1, int pitch, int lpr, int vpl, float* out, hipStream_t s);
+int launch_sweep(const float* q, const float* X, int64_t n, int pitch, int lpr, int vpl, int metric, float* out,
+                 hipStream_t s);
+int launch_search_beam(const SearchArgs& a, int lpr, int vpl, hipStream_t s);
+int launch_search_compat(const SearchArgs& a, int lpr, int vpl, hipStream_t s);
+
+// ---- build ----
+struct CompatBuildArgs {
+    GraphDev g;
+    int64_t n0, n1;               // insert internal ids [n0, n1) in order
+    const int32_t* levels;        // [cap_nodes] level of each node
+    const int32_t* layer_entry;   // [MH_MAXL] first node id of each layer (-1 none)
+    int M, ef;
+    unsigned long long* stats;    // [0]=dist evals [1]=expansions
+    int* err;
+    int vis_log2;
+};
+int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, hipStream_t s);
+
+struct BatchBuildArgs {
+    GraphDev g;
+    int layer;
+    int64_t n0, n1;               // batch of new internal ids
+    const int32_t* levels;
+    uint32_t* cur_entry;          // [cap_nodes] per-node descent entry (in/out)
+    int ef;                       // efConstruction
+    int mcap;                     // neighbors to select on this layer
+    int heuristic;
+    int32_t* inc_cnt;             // [cap_nodes] incoming request counters (zero between batches)
+    uint32_t* inc_src;            // [cap_nodes * inc_cap]
+    float* inc_dist;              // [cap_nodes * inc_cap]
+    int inc_cap;
+    uint32_t* touched;            // [batch * mcap]
+    int32_t* touched_cnt;         // [1]
+    unsigned long long* stats;    // [0]=dist evals [1]=expansions [2]=dropped requests
+    int vis_log2;
+};
+int launch_build_batch_search(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s);
+int launch_build_batch_commit(const BatchBuildArgs& a, int64_t n_touched, hipStream_t s);
+
+// ---- exact / merge ----
+struct ExactArgs {
+    const float* X;       // [N * pitch]
+    const float* xnorm;   // [N]
+    const int32_t* deg0;  // [N] layer-0 membership (-2 absent)
+    int64_t N;
+    const float* Q;       // [B * pitch]
+    const float* qnorm;   // [B] canonical |q|
+    int64_t B;
+    int pitch, dim, metric;
+    float* scores;        // [B * ldS] workspace
+    int64_t ldS;          // row stride of scores (multiple of 4, >= N)
+    int kk;               // preselect width (<= 64)
+    uint32_t* cand;       // [B * kk]
+};
+int launch_exact_scores(const ExactArgs& a, hipStream_t s);
+int launch_exact_select(const ExactArgs& a, hipStream_t s);
+
+int launch_rerank(const float* Q, const GraphDev& g, const uint32_t* cand, int kk, int64_t B, int lpr, int vpl, int k,
+                  int64_t* out_keys, float* out_dist, int32_t* out_n, int32_t* out_ids, hipStream_t s);
+
+int launch_merge_topk(const int64_t* keys_in, const float* dist_in, const int32_t* n_in, int shards, int64_t B,
+                      int k, int64_t* out_keys, float* out_dist, int32_t* out_n, hipStream_t s);
+
+}  // namespace mh

@@ -1,0 +1,291 @@
+// search.hip -- query-side kernels: row padding, canonical norms, the batched
+// distance sweep (DistanceFunc, distance.go:12-23) and the batched layer
+// descent + layer-0 search (Graph.Search / BatchSearch, graph.go:534-625,
+// 1047-1110) in compat and beam modes.  One wave64 workgroup per query: the
+// query lives in VGPRs, the visited set in LDS, the candidate list in VGPRs
+// across lanes; candidate rows are gathered from HBM with 1-KiB coalesced
+// wave loads.
+#include "device_search.hpp"
+#include "engine.hpp"
+
+namespace mh {
+
+__global__ void k_pad_rows(const float* __restrict__ src, int64_t n, int dim, float* __restrict__ dst, int pitch) {
+    const int64_t total = n * (int64_t)pitch;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / pitch;
+        const int c = (int)(i - r * pitch);
+        dst[i] = c < dim ? src[r * dim + c] : 0.f;
+    }
+}
+
+int launch_pad_rows(const float* src, int64_t n, int dim, float* dst, int pitch, hipStream_t s) {
+    if (n <= 0) return 0;
+    int64_t total = n * pitch;
+    int grid = (int)((total + 255) / 256);
+    if (grid > 65536) grid = 65536;
+    hipLaunchKernelGGL(k_pad_rows, dim3(grid), dim3(256), 0, s, src, n, dim, dst, pitch);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// canonical |x| per row: one wave handles RPI rows per step
+template <class C>
+__global__ __launch_bounds__(256) void k_norms(const float* __restrict__ X, int64_t n0, int64_t n1, int pitch,
+                                               float* __restrict__ out) {
+    const int lane = lane_id();
+    const int wave = threadIdx.x >> 6;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t row = n0 + gw * C::RPI + lane / C::LPR;
+    const int sub = lane & (C::LPR - 1);
+    float acc = 0.f;
+    if (row < n1) {
+        const float* rp = X + (size_t)row * pitch + sub * 4;
+#pragma unroll
+        for (int v = 0; v < C::VPL; ++v) {
+            float4 x = *reinterpret_cast<const float4*>(rp + v * C::LPR * 4);
+            acc = fmaf(x.x, x.x, acc);
+            acc = fmaf(x.y, x.y, acc);
+            acc = fmaf(x.z, x.z, acc);
+            acc = fmaf(x.w, x.w, acc);
+        }
+    }
+    acc = seg_allreduce<C::LPR>(acc);
+    if (row < n1 && sub == 0) out[row] = sqrtf(acc);
+}
+
+// distance of one query against n rows (mhnsw_distance)
+template <class C, int G>
+__global__ __launch_bounds__(256) void k_sweep(const float* __restrict__ qp, const float* __restrict__ X, int64_t n,
+                                               int pitch, int metric, float* __restrict__ out) {
+    using RM = RowMap<C, G>;
+    const int lane = lane_id();
+    const int wave = threadIdx.x >> 6;
+    const int64_t base = ((int64_t)blockIdx.x * 4 + wave) * RM::T;
+    QReg<C> q;
+    load_query(q, qp);
+    const float qn = query_norm(q);
+    uint32_t ids[G];
+    bool valid[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int64_t r = base + RM::reg_row(g, lane);
+        valid[g] = r < n;
+        ids[g] = valid[g] ? (uint32_t)r : 0u;
+    }
+    // rows of the sweep operand are addressed relative to X directly
+    float s = metric == EUCLIDEAN ? eval_rows<C, G, true>(q, X, pitch, ids, valid)
+                                  : eval_rows<C, G, false>(q, X, pitch, ids, valid);
+    const int64_t rown = base + RM::owned_row(lane);
+    float xn = 1.f;
+    // canonical |x| of the owned row: a second transposed pass (L1/L2-hot rows)
+    if (metric == COSINE) {
+        float p[G];
+        const int sub = lane & (C::LPR - 1);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float acc = 0.f;
+            if (valid[g]) {
+                const float* rp = X + (size_t)ids[g] * pitch + sub * 4;
+#pragma unroll
+                for (int v = 0; v < C::VPL; ++v) {
+                    float4 x = *reinterpret_cast<const float4*>(rp + v * C::LPR * 4);
+                    acc = fmaf(x.x, x.x, acc);
+                    acc = fmaf(x.y, x.y, acc);
+                    acc = fmaf(x.z, x.z, acc);
+                    acc = fmaf(x.w, x.w, acc);
+                }
+            }
+            p[g] = acc;
+        }
+        xn = sqrtf(reduce_rows<G, C::LPR>(p));
+    }
+    const float d = finalize(metric, s, xn, qn);
+    // the owning lane of each row is the first lane of its reduction group
+    constexpr int GROUP = C::LPR >> RM::LG;
+    if (rown < n && (lane & (GROUP - 1)) == 0) out[rown] = d;
+}
+
+template <class C>
+static int launch_norms_t(const float* X, int64_t n0, int64_t n1, int pitch, float* out, hipStream_t s) {
+    const int64_t rows = n1 - n0;
+    if (rows <= 0) return 0;
+    const int64_t waves = (rows + C::RPI - 1) / C::RPI;
+    const int grid = (int)((waves + 3) / 4);
+    hipLaunchKernelGGL(k_norms<C>, dim3(grid), dim3(256), 0, s, X, n0, n1, pitch, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <class C, int G>
+static int launch_sweep_t(const float* q, const float* X, int64_t n, int pitch, int metric, float* out,
+                          hipStream_t s) {
+    if (n <= 0) return 0;
+    constexpr int T = G * C::RPI;
+    const int64_t waves = (n + T - 1) / T;
+    const int grid = (int)((waves + 3) / 4);
+    hipLaunchKernelGGL((k_sweep<C, G>), dim3(grid), dim3(256), 0, s, q, X, n, pitch, metric, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------
+// batched search: one wave per query
+// ---------------------------------------------------------------------------
+template <class C, int R, int G>
+__global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int64_t b = blockIdx.x;
+    if (b >= a.B) return;
+    const int lane = lane_id();
+    QReg<C> q;
+    load_query(q, a.q + (size_t)b * C::PITCH);
+    const float qn = query_norm(q);
+    WaveStats st;
+    uint32_t ep = a.entry;
+    {
+        BList<1> L1;
+        for (int l = a.top; l >= 1; --l) {  // greedy descent, ef = 1
+            beam_layer<C, 1, G>(a.g, l, ep, 1, q, qn, L1, smem, a.vis_log2, st);
+            float d;
+            uint32_t id;
+            bl_at(L1, 0, d, id);
+            if (id != EMPTY_ID) ep = id & ID_MASK;
+        }
+    }
+    BList<R> L;
+    const int efl = a.ef > a.k ? a.ef : a.k;
+    beam_layer<C, R, G>(a.g, 0, ep, efl, q, qn, L, smem, a.vis_log2, st);
+    int nvalid = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int idx = r * 64 + lane;
+        const bool ok = idx < a.k && L.i[r] != EMPTY_ID;
+        nvalid += __popcll(__ballot(ok));
+        if (idx < a.k) {
+            const uint32_t id = L.i[r] & ID_MASK;
+            a.out_keys[b * a.k + idx] = ok ? a.g.keys[id] : (int64_t)-1;
+            a.out_dist[b * a.k + idx] = ok ? L.d[r] : __int_as_float(0x7f800000);
+            if (a.out_ids) a.out_ids[b * a.k + idx] = ok ? (int32_t)id : -1;
+        }
+    }
+    if (lane == 0) {
+        a.out_n[b] = nvalid;
+        atomicAdd(&a.stats[0], st.E);
+        atomicAdd(&a.stats[1], st.X);
+        if (st.resets) atomicAdd(&a.stats[2], st.resets);
+    }
+}
+
+template <class C, int G>
+__global__ __launch_bounds__(64) void k_search_compat(SearchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int64_t b = blockIdx.x;
+    if (b >= a.B) return;
+    const int lane = lane_id();
+    const int vsize = 1 << a.vis_log2;
+    CompatSmem S;
+    S.vis = smem;
+    S.vlog2 = a.vis_log2;
+    S.cd = reinterpret_cast<float*>(smem + vsize);
+    S.ci = smem + vsize + (a.ef + 2);
+    S.rd = reinterpret_cast<float*>(smem + vsize + 2 * (a.ef + 2));
+    S.ri = smem + vsize + 2 * (a.ef + 2) + (a.k + 2);
+    QReg<C> q;
+    load_query(q, a.q + (size_t)b * C::PITCH);
+    const float qn = query_norm(q);
+    WaveStats st;
+    int err = 0;
+    uint32_t elevator = EMPTY_ID;
+    int nres = 0;
+    for (int l = a.top; l >= 0; --l) {  // graph.go:571-622
+        uint32_t p = elevator != EMPTY_ID ? elevator
+                                          : (l == a.top ? a.entry : (uint32_t)a.layer_entry[l]);
+        if (l > 0) {
+            const int c = compat_layer<C, G>(a.g, l, p, 1, a.ef, q, qn, S, st, err);
+            if (c == 0) continue;
+            elevator = S.ri[0];
+            continue;
+        }
+        nres = compat_layer<C, G>(a.g, 0, p, a.k, a.ef, q, qn, S, st, err);
+    }
+    for (int i = lane; i < a.k; i += 64) {
+        const bool ok = i < nres;
+        const uint32_t id = ok ? S.ri[i] : 0u;
+        a.out_keys[b * a.k + i] = ok ? a.g.keys[id] : (int64_t)-1;
+        a.out_dist[b * a.k + i] = ok ? S.rd[i] : __int_as_float(0x7f800000);
+        if (a.out_ids) a.out_ids[b * a.k + i] = ok ? (int32_t)id : -1;
+    }
+    if (lane == 0) {
+        a.out_n[b] = nres;
+        atomicAdd(&a.stats[0], st.E);
+        atomicAdd(&a.stats[1], st.X);
+        if (err) atomicOr(a.err, 1);
+    }
+}
+
+template <class C, int R, int G>
+static int launch_beam_t(const SearchArgs& a, hipStream_t s) {
+    const size_t lds = (size_t)4 << a.vis_log2;
+    hipLaunchKernelGGL((k_search_beam<C, R, G>), dim3((unsigned)a.B), dim3(64), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <class C, int G>
+static int launch_compat_t(const SearchArgs& a, hipStream_t s) {
+    const size_t lds = ((size_t)1 << a.vis_log2) * 4 + (size_t)(a.ef + 2) * 8 + (size_t)(a.k + 2) * 8;
+    if (lds > 160 * 1024) return -2;
+    hipLaunchKernelGGL((k_search_compat<C, G>), dim3((unsigned)a.B), dim3(64), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// group width per configuration (rows in flight per wave step)
+#define MH_FOR_EACH_CFG(X)      \
+    X(16, 1, 2)                 \
+    X(32, 1, 4)                 \
+    X(64, 1, 8)                 \
+    X(64, 2, 8)                 \
+    X(64, 3, 8)                 \
+    X(64, 4, 4)                 \
+    X(64, 6, 4)                 \
+    X(64, 8, 2)
+
+int launch_norms(const float* X, int64_t n0, int64_t n1, int pitch, int lpr, int vpl, float* out, hipStream_t s) {
+#define X_(L, V, G) \
+    if (lpr == L && vpl == V) return launch_norms_t<Cfg<L, V>>(X, n0, n1, pitch, out, s);
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return -3;
+}
+
+int launch_sweep(const float* q, const float* X, int64_t n, int pitch, int lpr, int vpl, int metric, float* out,
+                 hipStream_t s) {
+#define X_(L, V, G) \
+    if (lpr == L && vpl == V) return launch_sweep_t<Cfg<L, V>, G>(q, X, n, pitch, metric, out, s);
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return -3;
+}
+
+int launch_search_beam(const SearchArgs& a, int lpr, int vpl, hipStream_t s) {
+    if (a.B <= 0) return 0;
+    const int efl = a.ef > a.k ? a.ef : a.k;
+#define X_(L, V, G)                                                              \
+    if (lpr == L && vpl == V) {                                                  \
+        if (efl <= 64) return launch_beam_t<Cfg<L, V>, 1, G>(a, s);              \
+        if (efl <= 128) return launch_beam_t<Cfg<L, V>, 2, G>(a, s);             \
+        if (efl <= 256) return launch_beam_t<Cfg<L, V>, 4, G>(a, s);             \
+        return -4;                                                               \
+    }
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return -3;
+}
+
+int launch_search_compat(const SearchArgs& a, int lpr, int vpl, hipStream_t s) {
+    if (a.B <= 0) return 0;
+#define X_(L, V, G) \
+    if (lpr == L && vpl == V) return launch_compat_t<Cfg<L, V>, G>(a, s);
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return -3;
+}
+
+}  // namespace mh

@@ -1,0 +1,334 @@
+"""Host-side mirror of the reference's Graph[K] API (graph.go:17-27, 305-366,
+437-1110; distance.go:12-46) over the C ABI of libmhnsw.so.
+
+Names, argument meaning and error messages follow the Go package so that code
+(and tests) written against TFMV/hnsw read the same.  Keys are Go `int`
+(int64).  Distances are the built-in CosineDistance / EuclideanDistance; they
+run on the GPU (a custom Python callable cannot, and is rejected).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, List, NamedTuple, Optional, Sequence
+
+import numpy as np
+
+from ._lib import (BUILD_BATCH, BUILD_COMPAT, COSINE, EUCLIDEAN, MODE_BEAM, MODE_COMPAT, MODE_EXACT, HnswError,
+                   check, load)
+
+Vector = np.ndarray
+
+
+class Node(NamedTuple):
+    """graph.go:19-23 Node[K]{Key, Value}."""
+    Key: int
+    Value: Vector
+
+
+def MakeNode(key: int, vec) -> Node:  # graph.go:25-27
+    return Node(int(key), np.asarray(vec, dtype=np.float32))
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _ptr(a: np.ndarray, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+class DistanceFunc:
+    """distance.go:12 `type DistanceFunc func(a, b []float32) float32`, backed by
+    the GPU sweep kernel (mhnsw_distance)."""
+
+    def __init__(self, name: str, metric: int):
+        self.name = name
+        self.metric = metric
+
+    def __call__(self, a, b) -> float:
+        a, b = _f32(a).ravel(), _f32(b).ravel()
+        out = np.zeros(1, np.float32)
+        check(load().mhnsw_distance(self.metric, _ptr(a, C.c_float), _ptr(b, C.c_float), 1, a.size,
+                                    _ptr(out, C.c_float)))
+        return float(out[0])
+
+    def sweep(self, q, X) -> np.ndarray:
+        """Batched form: distance of q to every row of X (the hot-path kernel)."""
+        q = _f32(q).ravel()
+        X = _f32(X).reshape(-1, q.size)
+        out = np.zeros(X.shape[0], np.float32)
+        check(load().mhnsw_distance(self.metric, _ptr(q, C.c_float), _ptr(X, C.c_float), X.shape[0], q.size,
+                                    _ptr(out, C.c_float)))
+        return out
+
+    def __repr__(self):
+        return f"<DistanceFunc {self.name}>"
+
+
+CosineDistance = DistanceFunc("cosine", COSINE)  # distance.go:15-17
+EuclideanDistance = DistanceFunc("euclidean", EUCLIDEAN)  # distance.go:20-23
+
+_distance_funcs = {"euclidean": EuclideanDistance, "cosine": CosineDistance}  # distance.go:25-28
+
+
+def RegisterDistanceFunc(name: str, fn: DistanceFunc):  # distance.go:44-46
+    _distance_funcs[name] = fn
+
+
+def distance_func_to_name(fn) -> Optional[str]:  # distance.go:30-39
+    for name, f in _distance_funcs.items():
+        if f is fn:
+            return name
+    return None
+
+
+def _metric_of(fn) -> int:
+    if fn is None:
+        return -1
+    if isinstance(fn, DistanceFunc):
+        return fn.metric
+    raise HnswError(-6, "custom DistanceFunc is not supported by the GPU engine (use CosineDistance or "
+                        "EuclideanDistance)")
+
+
+class Graph:
+    """graph.go:305-332 Graph[K].  Public fields M, Ml, EfSearch, Distance and
+    Rng (a seed) are read by every call, like the Go struct fields."""
+
+    def __init__(self, M: int = 16, Ml: float = 0.25, EfSearch: int = 20, Distance=CosineDistance,
+                 Rng: int = 0, build_mode: int = BUILD_COMPAT, _handle=None, **options):
+        lib = load()
+        h = _handle
+        if h is None:
+            # a Go struct literal may hold an invalid config; Validate() errors
+            # surface at call time, so create with a valid one and apply fields
+            h = C.c_void_p()
+            check(lib.mhnsw_create(COSINE, 16, 0.25, 20, int(Rng) & (2**64 - 1), C.byref(h)))
+        self._h = h
+        self.M, self.Ml, self.EfSearch, self.Distance = M, Ml, EfSearch, Distance
+        self._rng = int(Rng)
+        self._values = {}
+        self.set_option("build_mode", build_mode)
+        for k, v in options.items():
+            self.set_option(k, v)
+
+    # -- lifecycle --------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            load().mhnsw_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _sync(self):
+        check(load().mhnsw_set_params(self._h, _metric_of(self.Distance), int(self.M), float(self.Ml),
+                                      int(self.EfSearch)), self._h)
+
+    def _check(self, rc):
+        return check(rc, self._h)
+
+    @property
+    def Rng(self):
+        return self._rng
+
+    @Rng.setter
+    def Rng(self, seed: int):
+        self._rng = int(seed)
+        self._check(load().mhnsw_seed(self._h, int(seed) & (2**64 - 1)))
+
+    def set_option(self, name: str, value: int):
+        self._check(load().mhnsw_set_option(self._h, name.encode(), int(value)))
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int64()
+        self._check(load().mhnsw_get_option(self._h, name.encode(), C.byref(v)))
+        return v.value
+
+    # -- graph.go:916-937 ---------------------------------------------------
+    def Validate(self):
+        self._sync()
+        self._check(load().mhnsw_validate(self._h))
+
+    # -- graph.go:437-531 / 942-1042 --------------------------------------------
+    def Add(self, *nodes: Node):
+        self.BatchAdd(list(nodes))
+
+    def BatchAdd(self, nodes: Sequence[Node], levels=None):
+        if not nodes:
+            self.Validate()
+            return
+        keys = np.array([int(n.Key) for n in nodes], dtype=np.int64)
+        vecs = [np.asarray(n.Value, dtype=np.float32).ravel() for n in nodes]
+        dims = {v.size for v in vecs}
+        if len(dims) != 1:
+            # first mismatch is reported with the reference wording
+            d0 = self.Dims() or vecs[0].size
+            for v in vecs:
+                if v.size != d0:
+                    raise HnswError(-2, f"embedding dimension mismatch: {d0} != {v.size}")
+        self.add_arrays(keys, np.stack(vecs), levels=levels)
+        for n, v in zip(nodes, vecs):
+            self._values[int(n.Key)] = v
+
+    def add_arrays(self, keys, vecs, levels=None):
+        """Array form of BatchAdd: keys int64[n], vecs float32[n, dim] (host)."""
+        self._sync()
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        vecs = _f32(vecs).reshape(len(keys), -1)
+        lv = None if levels is None else np.ascontiguousarray(levels, dtype=np.int32)
+        self._check(load().mhnsw_add(self._h, _ptr(keys, C.c_int64), _ptr(vecs, C.c_float), len(keys),
+                                     vecs.shape[1], None if lv is None else _ptr(lv, C.c_int32)))
+
+    def add_device(self, keys, vecs_dev_ptr: int, n: int, dim: int, levels=None):
+        """BatchAdd with vectors already resident in HBM (device pointer)."""
+        self._sync()
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        lv = None if levels is None else np.ascontiguousarray(levels, dtype=np.int32)
+        self._check(load().mhnsw_add_device(self._h, _ptr(keys, C.c_int64), C.c_void_p(vecs_dev_ptr), n, dim,
+                                            None if lv is None else _ptr(lv, C.c_int32)))
+
+    def reserve(self, n: int, dim: int):
+        self._check(load().mhnsw_reserve(self._h, n, dim))
+
+    # -- graph.go:534-625 / 1047-1110 --------------------------------------------
+    def search_arrays(self, queries, k: int, mode: int = MODE_COMPAT, ef: int = 0, entry_key: Optional[int] = None):
+        """Batched search, array form -> (keys int64[B,k], dist float32[B,k], n int32[B])."""
+        self._sync()
+        q = _f32(queries)
+        if q.ndim == 1:
+            q = q.reshape(1, -1)
+        B, d = q.shape
+        kk = max(int(k), 1)
+        ok = np.zeros((B, kk), np.int64)
+        od = np.zeros((B, kk), np.float32)
+        on = np.zeros(B, np.int32)
+        ek = None if entry_key is None else C.byref(C.c_int64(int(entry_key)))
+        self._check(load().mhnsw_search(self._h, _ptr(q, C.c_float), B, d, int(k), mode, int(ef), ek,
+                                        _ptr(ok, C.c_int64), _ptr(od, C.c_float), _ptr(on, C.c_int32)))
+        return ok, od, on
+
+    def search_device(self, q_ptr: int, B: int, dim: int, k: int, keys_ptr: int, dist_ptr: int, n_ptr: int,
+                      mode: int = MODE_BEAM, ef: int = 0, stream: int = 0):
+        """Batched search on device buffers, enqueued on `stream` (no host sync)."""
+        self._check(load().mhnsw_search_device(self._h, C.c_void_p(q_ptr), B, dim, k, mode, ef,
+                                               C.c_void_p(keys_ptr), C.c_void_p(dist_ptr), C.c_void_p(n_ptr),
+                                               C.c_void_p(stream)))
+
+    def _node(self, key: int) -> Node:
+        v = self._values.get(key)
+        if v is None:
+            v, _ = self.Lookup(key)
+        return Node(key, v)
+
+    def Search(self, near, k: int, mode: int = MODE_COMPAT) -> List[Node]:
+        ok, _, on = self.search_arrays(np.asarray(near, np.float32).reshape(1, -1), k, mode)
+        return [self._node(int(x)) for x in ok[0, : on[0]]]
+
+    def BatchSearch(self, queries: Iterable, k: int, mode: int = MODE_COMPAT) -> List[List[Node]]:
+        qs = [np.asarray(q, np.float32).ravel() for q in queries]
+        if not qs:
+            self._sync()
+            if k <= 0:
+                raise HnswError(-3, f"k must be greater than 0, got {k}")
+            return []
+        d0 = self.Dims()
+        if d0:
+            for i, q in enumerate(qs):
+                if q.size != d0:
+                    raise HnswError(-2, f"embedding dimension mismatch for query {i}: {d0} != {q.size}")
+        ok, _, on = self.search_arrays(np.stack(qs), k, mode)
+        return [[self._node(int(x)) for x in ok[b, : on[b]]] for b in range(len(qs))]
+
+    # -- graph.go:829, 421, 898 --------------------------------------------------
+    def Len(self) -> int:
+        return int(load().mhnsw_len(self._h))
+
+    __len__ = Len
+
+    def Dims(self) -> int:
+        return int(load().mhnsw_dims(self._h))
+
+    def Lookup(self, key: int):
+        v = self._values.get(int(key))
+        if v is not None:
+            return v, True
+        out = np.zeros(max(self.Dims(), 1), np.float32)
+        found = self._check(load().mhnsw_lookup(self._h, int(key), _ptr(out, C.c_float)))
+        return (out if found else None), bool(found)
+
+    def Topography(self) -> List[int]:  # analyzer.go:41-49
+        lib = load()
+        return [int(lib.mhnsw_layer_count(self._h, l)) for l in range(lib.mhnsw_num_layers(self._h))]
+
+    # -- levels / stats / exchange ------------------------------------------------
+    def preview_levels(self, n: int) -> np.ndarray:
+        out = np.zeros(n, np.int32)
+        self._sync()
+        self._check(load().mhnsw_preview_levels(self._h, n, _ptr(out, C.c_int32)))
+        return out
+
+    def stats(self) -> dict:
+        o = np.zeros(7, np.int64)
+        self._check(load().mhnsw_stats(self._h, _ptr(o, C.c_int64), 7))
+        names = ["search_dist_evals", "search_expansions", "visited_resets", "build_dist_evals",
+                 "build_expansions", "dropped_proposals", "searches"]
+        return dict(zip(names, o.tolist()))
+
+    def reset_stats(self):
+        self._check(load().mhnsw_reset_stats(self._h))
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float()
+        self._check(load().mhnsw_last_kernel_ms(self._h, C.byref(ms)))
+        return ms.value
+
+    def export(self) -> dict:
+        lib = load()
+        N, dim, L, cap = C.c_int64(), C.c_int(), C.c_int(), C.c_int()
+        self._check(lib.mhnsw_export_sizes(self._h, C.byref(N), C.byref(dim), C.byref(L), C.byref(cap)))
+        N, dim, L, cap = N.value, dim.value, L.value, cap.value
+        keys = np.zeros(N, np.int64)
+        vecs = np.zeros((N, dim), np.float32)
+        deg = np.zeros((L, N), np.int32)
+        adj = np.zeros((L, N, cap), np.int32)
+        entry = np.zeros(max(L, 1), np.int32)
+        self._check(lib.mhnsw_export(self._h, _ptr(keys, C.c_int64), _ptr(vecs, C.c_float), _ptr(deg, C.c_int32),
+                                     _ptr(adj, C.c_int32), cap, _ptr(entry, C.c_int32)))
+        return dict(keys=keys, vecs=vecs, deg=deg, adj=adj, entry=entry[:L])
+
+    def import_graph(self, keys, vecs, deg, adj, entry):
+        keys = np.ascontiguousarray(keys, np.int64)
+        vecs = _f32(vecs)
+        deg = np.ascontiguousarray(deg, np.int32)
+        adj = np.ascontiguousarray(adj, np.int32)
+        entry = np.ascontiguousarray(entry, np.int32)
+        L, N = deg.shape
+        self._sync()
+        self._check(load().mhnsw_import(self._h, N, vecs.shape[1], L, adj.shape[2], _ptr(keys, C.c_int64),
+                                        _ptr(vecs, C.c_float), _ptr(deg, C.c_int32), _ptr(adj, C.c_int32),
+                                        _ptr(entry, C.c_int32)))
+
+
+def NewGraph() -> Graph:  # graph.go:340-348
+    import time
+    return Graph(M=16, Ml=0.25, EfSearch=20, Distance=CosineDistance, Rng=time.time_ns())
+
+
+def NewGraphWithConfig(m: int, ml: float, efSearch: int, distance) -> Graph:  # graph.go:352-366
+    import time
+    seed = time.time_ns()
+    h = C.c_void_p()
+    check(load().mhnsw_create(_metric_of(distance), int(m), float(ml), int(efSearch), seed & (2**64 - 1),
+                              C.byref(h)))  # validates before touching the device
+    return Graph(M=m, Ml=ml, EfSearch=efSearch, Distance=distance, Rng=seed, _handle=h)
+
+
+def merge_topk_device(keys_ptr, dist_ptr, n_ptr, shards, B, k, out_keys, out_dist, out_n, stream=0):
+    """Merge per-shard top-k lists (device pointers) -> global top-k by (dist, key)."""
+    check(load().mhnsw_merge_topk_device(C.c_void_p(keys_ptr), C.c_void_p(dist_ptr), C.c_void_p(n_ptr), shards,
+                                         B, k, C.c_void_p(out_keys), C.c_void_p(out_dist), C.c_void_p(out_n),
+                                         C.c_void_p(stream)))

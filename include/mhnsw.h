@@ -1,0 +1,135 @@
+/*
+ * mhnsw.h -- C ABI of the MI355X-native HNSW engine (libmhnsw.so).
+ *
+ * This is the drop-in boundary for the hot path of TFMV/hnsw (Go): the
+ * distance sweep -> layer-0 greedy/beam search -> M-neighbour selection on
+ * insert.  Every entry point is plain C (pointers + sizes, no torch types) so
+ * the Go package can bind it through cgo; see INTEGRATION.md for the binding
+ * a maintainer would add.  Each declaration names the reference interface it
+ * replaces (paths relative to the reference repository root).
+ *
+ * Conventions
+ *  - Keys are int64 (the reference's Graph[int]); vectors are float32,
+ *    row-major, `dim` contiguous floats per row.
+ *  - Host-pointer entry points copy their inputs before returning (the cgo
+ *    rule forbids C from retaining Go pointers).  *_device entry points take
+ *    device pointers and enqueue on the given HIP stream (NULL = library stream).
+ *  - Return value: MHNSW_OK (0) or a negative error class; the message, with
+ *    the reference's wording where one exists, is mhnsw_last_error(h).
+ *  - Concurrency mirrors graph.go:328 (sync.RWMutex): searches may run
+ *    concurrently on one handle; add/import are exclusive.
+ */
+#ifndef MHNSW_H
+#define MHNSW_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mhnsw_index mhnsw_index;
+
+/* DistanceFunc identities (distance.go:25-28 distanceFuncs registry) */
+#define MHNSW_NO_DISTANCE (-1) /* Graph.Distance == nil */
+#define MHNSW_COSINE 0         /* distance.go:15 CosineDistance */
+#define MHNSW_EUCLIDEAN 1      /* distance.go:20 EuclideanDistance */
+
+/* search modes */
+#define MHNSW_MODE_COMPAT 0 /* graph.go:94-170 semantics, results in heap order */
+#define MHNSW_MODE_BEAM 1   /* standard HNSW best-first (ef), sorted results   */
+#define MHNSW_MODE_EXACT 2  /* brute force (MFMA scores + canonical re-rank)   */
+
+/* build modes (option "build_mode") */
+#define MHNSW_BUILD_COMPAT 0 /* graph.go:437-531 sequential Add semantics */
+#define MHNSW_BUILD_BATCH 1  /* batched parallel insert (throughput)      */
+
+/* error classes */
+#define MHNSW_OK 0
+#define MHNSW_EINVAL (-1)       /* Validate() failure / bad argument          */
+#define MHNSW_EDIM (-2)         /* "embedding dimension mismatch: %d != %d"   */
+#define MHNSW_EK (-3)           /* "k must be greater than 0, got %d"         */
+#define MHNSW_ENOMEM (-4)
+#define MHNSW_EDEVICE (-5)      /* HIP runtime / kernel launch failure         */
+#define MHNSW_EUNSUPPORTED (-6) /* outside this build's supported envelope     */
+#define MHNSW_EINTERNAL (-7)
+
+/* ---- lifecycle: NewGraph / NewGraphWithConfig (graph.go:340-366) ----
+ * Binds the handle to the current HIP device.  Fails with the Validate()
+ * message (graph.go:916-937) when the configuration is invalid; the message is
+ * then available from mhnsw_last_error(NULL). */
+int mhnsw_create(int metric, int M, double ml, int ef_search, uint64_t seed, mhnsw_index **out);
+void mhnsw_destroy(mhnsw_index *h);
+const char *mhnsw_last_error(const mhnsw_index *h);
+
+/* ---- public Graph fields (graph.go:305-326): Distance, M, Ml, EfSearch, Rng ---- */
+int mhnsw_set_params(mhnsw_index *h, int metric, int M, double ml, int ef_search);
+int mhnsw_get_params(const mhnsw_index *h, int *metric, int *M, double *ml, int *ef_search);
+int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(seed)) analogue */
+/* engine options: "build_mode", "m0" (layer-0 degree cap, batch mode),
+ * "ef_construction", "heuristic", "batch_min", "batch_max", "batch_ratio_pct",
+ * "vis_log2", "exact_kk" */
+int mhnsw_set_option(mhnsw_index *h, const char *name, int64_t value);
+int mhnsw_get_option(const mhnsw_index *h, const char *name, int64_t *value);
+/* Graph.Validate (graph.go:916-937) */
+int mhnsw_validate(mhnsw_index *h);
+/* pre-size device storage for n vectors of `dim` floats */
+int mhnsw_reserve(mhnsw_index *h, int64_t n, int dim);
+
+/* ---- Graph.Add / Graph.BatchAdd (graph.go:437-531, 942-1042) ----
+ * levels: NULL draws each level like randomLevel (graph.go:388-417) from the
+ * handle's RNG; non-NULL injects them (parity testing). */
+int mhnsw_add(mhnsw_index *h, const int64_t *keys, const float *vecs, int64_t n, int dim, const int32_t *levels);
+/* same, vectors already in HBM (keys/levels stay host pointers) */
+int mhnsw_add_device(mhnsw_index *h, const int64_t *keys, const float *d_vecs, int64_t n, int dim,
+                     const int32_t *levels);
+
+/* ---- Graph.Search / Graph.BatchSearch (graph.go:534-625, 1047-1110) ----
+ * B queries of `dim` floats; outputs hold B*k slots; out_n[b] results for
+ * query b.  ef <= 0 uses EfSearch.  entry_key (nullable) replaces the
+ * arbitrary layer.entry() (graph.go:250-258) of the top layer. */
+int mhnsw_search(mhnsw_index *h, const float *queries, int64_t B, int dim, int k, int mode, int ef,
+                 const int64_t *entry_key, int64_t *out_keys, float *out_dist, int32_t *out_n);
+int mhnsw_search_device(mhnsw_index *h, const float *d_queries, int64_t B, int dim, int k, int mode, int ef,
+                        int64_t *d_keys, float *d_dist, int32_t *d_n, void *stream);
+
+/* ---- Len / Dims / Lookup / Analyzer.Topography (graph.go:829, 421, 898; analyzer.go:41) ---- */
+int64_t mhnsw_len(const mhnsw_index *h);
+int mhnsw_dims(const mhnsw_index *h);
+int mhnsw_lookup(mhnsw_index *h, int64_t key, float *out_vec); /* 1 found, 0 absent, <0 error */
+int mhnsw_num_layers(const mhnsw_index *h);
+int64_t mhnsw_layer_count(const mhnsw_index *h, int layer);
+
+/* ---- DistanceFunc (distance.go:12-23): batched sweep of one query over n rows ---- */
+int mhnsw_distance(int metric, const float *q, const float *X, int64_t n, int dim, float *out);
+int mhnsw_distance_device(int metric, const float *d_q, const float *d_X, int64_t n, int dim, float *d_out,
+                          void *stream);
+
+/* ---- graph exchange (CSR view of encode.go's layer/neighbour structure) ----
+ * keys[N], vecs[N*dim], deg[L*N] (-2 absent, -1 nil map, >=0 degree),
+ * adj[L*N*cap] internal ids (row-major, -1 padded), entry[L]. */
+int mhnsw_export_sizes(mhnsw_index *h, int64_t *N, int *dim, int *L, int *cap);
+int mhnsw_export(mhnsw_index *h, int64_t *keys, float *vecs, int32_t *deg, int32_t *adj, int cap, int32_t *entry);
+int mhnsw_import(mhnsw_index *h, int64_t N, int dim, int L, int cap, const int64_t *keys, const float *vecs,
+                 const int32_t *deg, const int32_t *adj, const int32_t *entry);
+
+/* levels randomLevel() would draw for the next n Adds (does not consume the RNG) */
+int mhnsw_preview_levels(mhnsw_index *h, int64_t n, int32_t *out);
+
+/* counters: [0] search distance evals, [1] search expansions, [2] visited-set
+ * resets, [3] build distance evals, [4] build expansions, [5] dropped reverse
+ * proposals, [6] searches issued */
+int mhnsw_stats(const mhnsw_index *h, int64_t *out, int n);
+int mhnsw_reset_stats(mhnsw_index *h);
+/* device time of the last search's main kernel (HIP events on its stream) */
+int mhnsw_last_kernel_ms(mhnsw_index *h, float *ms);
+
+/* ---- multi-GPU: merge per-shard top-k lists (device pointers) ----
+ * inputs [shards][B][k] (+ n_in [shards][B]); output best k by (dist, key). */
+int mhnsw_merge_topk_device(const int64_t *keys_in, const float *dist_in, const int32_t *n_in, int shards,
+                            int64_t B, int k, int64_t *out_keys, float *out_dist, int32_t *out_n, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

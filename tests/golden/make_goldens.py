@@ -1,0 +1,119 @@
+"""Writes the committed fixtures in tests/golden/.
+
+reference_goldens.json -- inputs/expected outputs transcribed from the
+    reference's own tests (data only; each entry cites its source file:line).
+    The Go toolchain is absent here, so these are the only reference-pinned
+    vectors; everything else is pinned against them through the oracle.
+oracle_fixtures.npz -- self-consistency pins produced by the CPU restatement
+    (oracle/) on seeded inputs: small graphs built in compat mode with the
+    SplitMix64 level stream, plus their compat / beam / exact search outputs.
+    Regenerate with:  python tests/golden/make_goldens.py
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+
+def reference_goldens():
+    return {
+        "distance": [
+            # distance_test.go:9-13 -- require.Equal(float32(5.196152), ...)
+            {"src": "distance_test.go:9-13", "fn": "euclidean", "a": [1, 2, 3], "b": [4, 5, 6],
+             "bits": "0x40a646e1", "tol": 0.0},
+            # distance_test.go:15-31 -- InDelta 1e-6
+            {"src": "distance_test.go:18-20", "fn": "cosine", "a": [1, 1, 1], "b": [0.8, 0.8, 0.8],
+             "want": 0.0, "tol": 1e-6},
+            {"src": "distance_test.go:23-25", "fn": "cosine", "a": [1, 0], "b": [0, 1], "want": 1.0, "tol": 1e-6},
+            {"src": "distance_test.go:28-30", "fn": "cosine", "a": [1, 0], "b": [1, 0], "want": 0.0, "tol": 1e-6},
+        ],
+        "max_level": [
+            {"src": "graph_test.go:18-20", "ml": 0.5, "n": 10, "want": 4},
+            {"src": "graph_test.go:22-24", "ml": 0.5, "n": 1000, "want": 11},
+        ],
+        # graph_test.go:27-74: hand graph, entry key 0; node under map key 4 has Key 5, Value {4}
+        "layer_node_search": {
+            "src": "graph_test.go:27-74",
+            "keys": [0, 1, 2, 3, 5, 5],
+            "values": [[0], [1], [2], [3], [4], [5]],
+            "deg": [3, -1, -1, 2, -1, -1],
+            "adj": {"0": [1, 2, 3], "3": [4, 5]},
+            "entry": 0, "k": 2, "ef": 4, "query": [4], "metric": "euclidean",
+            "want_keys": [5, 3],
+        },
+        # graph_test.go:253-275
+        "default_cosine": {
+            "src": "graph_test.go:253-275",
+            "M": 16, "Ml": 0.25, "EfSearch": 20,
+            "keys": [1, 2, 3], "values": [[1, 1], [0, 1], [1, -1]],
+            "query": [0.5, 0.5], "k": 1, "want_keys": [1],
+        },
+        # graph_test.go:86-133 (M=6, Ml=0.5, ef=20, Euclidean, 128 1-D points, Go math/rand seed 0)
+        "add_search_1d": {
+            "src": "graph_test.go:76-133",
+            "M": 6, "Ml": 0.5, "EfSearch": 20, "n": 128, "query": [64.5], "k": 4,
+            "want_keys_go_seed0": [64, 65, 62, 63],
+            "want_topography_go_seed0": [128, 67, 28, 12, 6, 2, 1, 1],
+            "note": "Go's math/rand seed-0 stream is not reproducible offline; the test asserts the "
+                    "property: 4 results, all within 60..68, containing 64 and 65",
+        },
+        # graph_test.go:415-459 error strings
+        "validation": [
+            {"src": "graph_test.go:421-425", "M": 0, "Ml": 0.25, "ef": 20, "metric": "cosine",
+             "contains": "M must be greater than 0"},
+            {"src": "graph_test.go:427-435", "M": 16, "Ml": 0.0, "ef": 20, "metric": "cosine",
+             "contains": "Ml must be between 0 and 1"},
+            {"src": "graph_test.go:432-434", "M": 16, "Ml": 1.5, "ef": 20, "metric": "cosine",
+             "contains": "Ml must be between 0 and 1"},
+            {"src": "graph_test.go:437-441", "M": 16, "Ml": 0.25, "ef": 0, "metric": "cosine",
+             "contains": "EfSearch must be greater than 0"},
+            {"src": "graph_test.go:443-447", "M": 16, "Ml": 0.25, "ef": 20, "metric": None,
+             "contains": "Distance function must be set"},
+        ],
+        "search_k": {"src": "graph_test.go:449-458", "k": 0, "contains": "k must be greater than 0"},
+    }
+
+
+def oracle_fixtures():
+    import oracle as O
+
+    out = {}
+    cases = [("c16_cos", 400, 16, O.COSINE, 8, 0.25, 20), ("c8_l2", 300, 8, O.EUCLIDEAN, 6, 0.5, 20),
+             ("c128_cos", 250, 128, O.COSINE, 16, 0.25, 20)]
+    for name, n, d, metric, M, ml, ef in cases:
+        rng = np.random.default_rng(sum(map(ord, name)))
+        X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+        Q = rng.uniform(-1, 1, (32, d)).astype(np.float32)
+        keys = rng.permutation(10 * n)[:n].astype(np.int64)
+        g = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=ml, EfSearch=ef, seed=1234)
+        levels = np.array([g.random_level() for _ in range(n)], np.int32)
+        g = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=ml, EfSearch=ef, seed=1234)
+        g.add(keys, X, levels)
+        out[f"{name}/X"] = X
+        out[f"{name}/Q"] = Q
+        out[f"{name}/keys"] = keys
+        out[f"{name}/levels"] = levels
+        out[f"{name}/cfg"] = np.array([metric, M, ef], np.int32)
+        out[f"{name}/ml"] = np.array([ml], np.float64)
+        for mname, mode in (("compat", O.MODE_COMPAT), ("beam", O.MODE_BEAM), ("exact", O.MODE_EXACT)):
+            k = 10
+            ok, od, on = g.search(Q, k, mode=mode, ef=ef if mode != O.MODE_BEAM else 32)
+            out[f"{name}/{mname}_keys"] = ok
+            out[f"{name}/{mname}_dist"] = od
+            out[f"{name}/{mname}_n"] = on
+        ex = g.export()
+        out[f"{name}/deg"] = ex["deg"]
+        out[f"{name}/adj"] = ex["adj"]
+    return out
+
+
+if __name__ == "__main__":
+    with open(os.path.join(HERE, "reference_goldens.json"), "w") as f:
+        json.dump(reference_goldens(), f, indent=1)
+    np.savez_compressed(os.path.join(HERE, "oracle_fixtures.npz"), **oracle_fixtures())
+    print("wrote", os.listdir(HERE))

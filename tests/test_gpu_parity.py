@@ -1,0 +1,303 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU restatement
+(oracle/) on identical inputs.  Integer/index results must be identical;
+distances must be bit-identical to the oracle's canonical-order restatement
+(OG_ORDER_DEV) and within 1e-5 (relative for L2) of the sequential-fp32
+restatement of vek32 (OG_ORDER_REF)."""
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TOL = 1e-5  # north_star: distances within 1e-5 fp32
+
+
+def _bits(x):
+    return struct.unpack("<I", struct.pack("<f", float(x)))[0]
+
+
+def _levels(O, metric, M, ml, ef, seed, n):
+    g = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=ml, EfSearch=ef, seed=seed)
+    return np.array([g.random_level() for _ in range(n)], np.int32)
+
+
+def _metric_fn(H, metric):
+    return H.CosineDistance if metric == 0 else H.EuclideanDistance
+
+
+def _same_graph(a, b):
+    assert np.array_equal(a["keys"], b["keys"])
+    assert np.array_equal(a["deg"], b["deg"]), "degree arrays differ"
+    L, N = a["deg"].shape
+    for l in range(L):
+        for i in range(N):
+            d = a["deg"][l, i]
+            if d > 0:
+                assert set(a["adj"][l, i, :d].tolist()) == set(b["adj"][l, i, :d].tolist()), (l, i)
+    assert np.array_equal(a["entry"], b["entry"])
+
+
+def _same_results(gk, gd, gn, rk, rd, rn, bitwise=True):
+    assert np.array_equal(gn, rn)
+    for b in range(len(gn)):
+        n = gn[b]
+        assert gk[b, :n].tolist() == rk[b, :n].tolist(), b
+        if bitwise:
+            assert np.array_equal(gd[b, :n].view(np.uint32), rd[b, :n].view(np.uint32)), b
+
+
+@pytest.fixture(scope="module")
+def ref():
+    with open(os.path.join(GOLD, "reference_goldens.json")) as f:
+        return json.load(f)
+
+
+# ---------------------------------------------------------------- distances
+def test_distance_kats(H, ref):
+    for c in ref["distance"]:
+        fn = H.CosineDistance if c["fn"] == "cosine" else H.EuclideanDistance
+        d = fn(c["a"], c["b"])
+        if "bits" in c:
+            assert _bits(d) == int(c["bits"], 16), c["src"]
+        else:
+            assert abs(d - c["want"]) <= c["tol"], c["src"]
+
+
+@pytest.mark.parametrize("dim", [1, 2, 3, 7, 16, 64, 100, 128, 255, 256, 500, 768, 1000, 1536, 2048])
+def test_distance_sweep_bitwise(H, O, dim):
+    rng = np.random.default_rng(dim)
+    X = rng.uniform(-1, 1, (300, dim)).astype(np.float32)
+    X[7] = 0.0  # zero vector: cosine -> NaN like the reference
+    q = rng.uniform(-1, 1, dim).astype(np.float32)
+    for metric, fn in ((O.COSINE, H.CosineDistance), (O.EUCLIDEAN, H.EuclideanDistance)):
+        got = fn.sweep(q, X)
+        dev = np.array([O.distance(metric, O.ORDER_DEV, x, q) for x in X], np.float32)
+        refd = np.array([O.distance(metric, O.ORDER_REF, x, q) for x in X], np.float32)
+        assert np.array_equal(got.view(np.uint32), dev.view(np.uint32)), (metric, dim)
+        ok = ~np.isnan(refd)
+        assert np.array_equal(np.isnan(got), np.isnan(refd))
+        scale = np.maximum(1.0, np.abs(refd[ok])) if metric == O.EUCLIDEAN else 1.0
+        assert np.all(np.abs(got[ok] - refd[ok]) <= TOL * scale)
+
+
+# ---------------------------------------------------------------- goldens
+def test_levels_match_oracle(H, O):
+    g = H.Graph(M=16, Ml=0.25, EfSearch=20, Rng=42)
+    want = _levels(O, O.COSINE, 16, 0.25, 20, 42, 500)
+    assert np.array_equal(g.preview_levels(500), want)
+
+
+def test_layer_node_search(H, ref):
+    c = ref["layer_node_search"]
+    g = H.Graph(M=6, Ml=0.5, EfSearch=c["ef"], Distance=H.EuclideanDistance)
+    n = len(c["keys"])
+    adj = -np.ones((1, n, 7), np.int32)
+    for i, lst in c["adj"].items():
+        adj[0, int(i), : len(lst)] = lst
+    g.import_graph(np.array(c["keys"]), np.array(c["values"], np.float32), np.array([c["deg"]], np.int32), adj,
+                   np.array([c["entry"]], np.int32))
+    k, _, nres = g.search_arrays(np.array([c["query"]], np.float32), c["k"], mode=H.MODE_COMPAT)
+    assert k[0, : nres[0]].tolist() == c["want_keys"]
+
+
+def test_default_cosine(H, ref):
+    c = ref["default_cosine"]
+    g = H.Graph(M=c["M"], Ml=c["Ml"], EfSearch=c["EfSearch"], Distance=H.CosineDistance, Rng=1)
+    g.Add(*[H.MakeNode(k, v) for k, v in zip(c["keys"], c["values"])])
+    res = g.Search(c["query"], c["k"])
+    assert [n.Key for n in res] == c["want_keys"]
+    assert np.array_equal(res[0].Value, np.array(c["values"][0], np.float32))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_add_search_1d(H, O, ref, seed):
+    c = ref["add_search_1d"]
+    n = c["n"]
+    lv = _levels(O, O.EUCLIDEAN, c["M"], c["Ml"], c["EfSearch"], seed, n)
+    o = O.Graph(metric=O.EUCLIDEAN, order=O.ORDER_DEV, M=c["M"], Ml=c["Ml"], EfSearch=c["EfSearch"])
+    o.add(np.arange(n), np.arange(n, dtype=np.float32).reshape(-1, 1), lv)
+    g = H.Graph(M=c["M"], Ml=c["Ml"], EfSearch=c["EfSearch"], Distance=H.EuclideanDistance)
+    g.BatchAdd([H.MakeNode(i, [float(i)]) for i in range(n)], levels=lv)
+    assert g.Topography() == o.topography()
+    _same_graph(g.export(), o.export())
+    res = [nd.Key for nd in g.Search(c["query"], c["k"])]
+    rk, _, rn = o.search(c["query"], c["k"])
+    assert res == rk[0, : rn[0]].tolist()
+    assert len(res) == 4 and {64, 65} <= set(res)
+
+
+# ---------------------------------------------------------------- compat build + search parity
+def _fixture_cases():
+    fx = np.load(os.path.join(GOLD, "oracle_fixtures.npz"))
+    return fx, sorted({k.split("/")[0] for k in fx.files})
+
+
+@pytest.mark.parametrize("name", ["c16_cos", "c8_l2", "c128_cos"])
+def test_fixture_build_and_search(H, name):
+    fx, _ = _fixture_cases()
+    metric, M, ef = fx[f"{name}/cfg"].tolist()
+    ml = float(fx[f"{name}/ml"][0])
+    g = H.Graph(M=M, Ml=ml, EfSearch=ef, Distance=_metric_fn(H, metric))
+    g.add_arrays(fx[f"{name}/keys"], fx[f"{name}/X"], levels=fx[f"{name}/levels"])
+    ex = g.export()
+    assert np.array_equal(ex["deg"], fx[f"{name}/deg"])
+    L, N = ex["deg"].shape
+    for l in range(L):
+        for i in range(N):
+            d = ex["deg"][l, i]
+            if d > 0:
+                assert set(ex["adj"][l, i, :d]) == set(fx[f"{name}/adj"][l, i, :d]), (l, i)
+    for mname, mode in (("compat", H.MODE_COMPAT), ("beam", H.MODE_BEAM), ("exact", H.MODE_EXACT)):
+        gk, gd, gn = g.search_arrays(fx[f"{name}/Q"], 10, mode=mode, ef=ef if mode != H.MODE_BEAM else 32)
+        _same_results(gk, gd, gn, fx[f"{name}/{mname}_keys"], fx[f"{name}/{mname}_dist"], fx[f"{name}/{mname}_n"])
+
+
+@pytest.mark.parametrize("n,d,metric,M,ml,ef", [
+    (1500, 100, 0, 16, 0.25, 20),
+    (1200, 768, 0, 16, 0.25, 20),
+    (1500, 33, 1, 10, 0.3, 24),
+    (800, 1536, 1, 12, 0.25, 16),
+    (600, 3, 1, 6, 0.5, 20),
+])
+def test_compat_build_parity(H, O, n, d, metric, M, ml, ef):
+    rng = np.random.default_rng(n + d)
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    if d > 4:
+        X[n // 3] = 0.0  # zero vector: NaN distances follow the reference's comparisons
+    Q = rng.uniform(-1, 1, (64, d)).astype(np.float32)
+    keys = rng.permutation(5 * n)[:n].astype(np.int64) - n
+    lv = _levels(O, metric, M, ml, ef, 77, n)
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=ml, EfSearch=ef)
+    o.add(keys, X, lv)
+    g = H.Graph(M=M, Ml=ml, EfSearch=ef, Distance=_metric_fn(H, metric))
+    g.add_arrays(keys, X, levels=lv)
+    _same_graph(g.export(), o.export())
+    for mode in (H.MODE_COMPAT, H.MODE_BEAM, H.MODE_EXACT):
+        for efq in ((ef, 50) if mode == H.MODE_COMPAT else (10, 64, 100, 200)):
+            gk, gd, gn = g.search_arrays(Q, 10, mode=mode, ef=efq)
+            rk, rd, rn = o.search(Q, 10, mode=mode, ef=efq)
+            _same_results(gk, gd, gn, rk, rd, rn)
+            if mode == H.MODE_EXACT:
+                break
+    # distances also within 1e-5 of the sequential fp32 restatement
+    r = O.Graph(metric=metric, order=O.ORDER_REF, M=M, Ml=ml, EfSearch=ef)
+    r.import_graph(**o.export())
+    rk, rd, rn = r.search(Q, 10, mode=O.MODE_EXACT)
+    gk, gd, gn = g.search_arrays(Q, 10, mode=H.MODE_EXACT)
+    fin = np.isfinite(rd[:, 0])
+    assert np.all(np.abs(gd[fin, 0] - rd[fin, 0]) <= TOL * np.maximum(1.0, np.abs(rd[fin, 0])))
+
+
+def test_entry_injection_and_incremental_adds(H, O):
+    rng = np.random.default_rng(3)
+    n, d = 900, 24
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    Q = rng.uniform(-1, 1, (40, d)).astype(np.float32)
+    lv = _levels(O, O.COSINE, 8, 0.25, 20, 5, n)
+    o = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=8, Ml=0.25, EfSearch=20)
+    g = H.Graph(M=8, Ml=0.25, EfSearch=20)
+    for a, b in ((0, 1), (1, 50), (50, 400), (400, n)):  # several Add calls grow the index
+        o.add(np.arange(a, b), X[a:b], lv[a:b])
+        g.add_arrays(np.arange(a, b), X[a:b], levels=lv[a:b])
+    _same_graph(g.export(), o.export())
+    top = len(o.topography()) - 1
+    ex = o.export()
+    members = [int(ex["keys"][i]) for i in range(n) if ex["deg"][top, i] != -2]
+    for ek in members[:3]:
+        gk, gd, gn = g.search_arrays(Q, 5, mode=H.MODE_COMPAT, entry_key=ek)
+        rk, rd, rn = o.search(Q, 5, mode=O.MODE_COMPAT, entry_key=ek)
+        _same_results(gk, gd, gn, rk, rd, rn)
+
+
+# ---------------------------------------------------------------- API behaviour
+def test_validation_and_errors(H):
+    g = H.Graph(M=0, Ml=0.25, EfSearch=20)
+    with pytest.raises(H.HnswError, match="M must be greater than 0, got 0"):
+        g.Add(H.MakeNode(1, [1, 2, 3]))
+    g = H.Graph(M=16, Ml=0.25, EfSearch=20)
+    with pytest.raises(H.HnswError, match="k must be greater than 0, got 0"):
+        g.Search([1, 2, 3], 0)
+    assert g.Search([1, 2, 3], 3) == []  # empty graph: nil, nil (graph.go:554-556)
+    g.Add(H.MakeNode(1, [1, 2, 3]))
+    with pytest.raises(H.HnswError, match=r"embedding dimension mismatch: 3 != 2"):
+        g.Add(H.MakeNode(2, [1, 2]))
+    with pytest.raises(H.HnswError, match=r"embedding dimension mismatch: 3 != 2"):
+        g.Search([1, 2], 1)
+    with pytest.raises(H.HnswError, match=r"embedding dimension mismatch for query 1: 3 != 2"):
+        g.BatchSearch([[1, 2, 3], [1, 2]], 1)
+    assert g.Len() == 1 and g.Dims() == 3
+    v, ok = g.Lookup(1)
+    assert ok and v.tolist() == [1, 2, 3]
+    assert g.Lookup(99) == (None, False)
+    with pytest.raises(H.HnswError, match="duplicate key"):
+        g.Add(H.MakeNode(1, [3, 2, 1]))
+
+
+def test_batch_search_matches_search(H):
+    rng = np.random.default_rng(8)
+    g = H.Graph(M=8, Ml=0.25, EfSearch=20, Rng=4)
+    X = rng.uniform(-1, 1, (300, 12)).astype(np.float32)
+    g.BatchAdd([H.MakeNode(i, X[i]) for i in range(300)])
+    Q = rng.uniform(-1, 1, (10, 12)).astype(np.float32)
+    bs = g.BatchSearch(list(Q), 4)
+    for q, r in zip(Q, bs):
+        assert [n.Key for n in g.Search(q, 4)] == [n.Key for n in r]
+
+
+def test_merge_topk_device(H):
+    torch = pytest.importorskip("torch")
+    S, B, k = 4, 257, 10
+    rng = np.random.default_rng(1)
+    dist = np.sort(rng.uniform(0, 1, (S, B, k)).astype(np.float32), axis=2)
+    keys = rng.permutation(S * B * k).reshape(S, B, k).astype(np.int64)
+    nn = rng.integers(0, k + 1, (S, B)).astype(np.int32)
+    dev = torch.device("cuda:0")
+    tk, td, tn = (torch.from_numpy(x).to(dev) for x in (keys, dist, nn))
+    ok = torch.empty((B, k), dtype=torch.int64, device=dev)
+    od = torch.empty((B, k), dtype=torch.float32, device=dev)
+    on = torch.empty((B,), dtype=torch.int32, device=dev)
+    H.merge_topk_device(tk.data_ptr(), td.data_ptr(), tn.data_ptr(), S, B, k, ok.data_ptr(), od.data_ptr(),
+                        on.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ok, od, on = ok.cpu().numpy(), od.cpu().numpy(), on.cpu().numpy()
+    for b in range(B):
+        cand = sorted((dist[s, b, j], keys[s, b, j]) for s in range(S) for j in range(nn[s, b]))[:k]
+        assert on[b] == len(cand)
+        assert ok[b, : on[b]].tolist() == [c[1] for c in cand]
+        assert od[b, : on[b]].tolist() == [c[0] for c in cand]
+
+
+# ---------------------------------------------------------------- batched build
+def _clustered(rng, n, d, nc=64, intrinsic=12, noise=0.05):
+    C = rng.normal(size=(nc, intrinsic)).astype(np.float32)
+    A = rng.normal(size=(intrinsic, d)).astype(np.float32) / np.sqrt(intrinsic)
+    z = C[rng.integers(0, nc, n)] + 0.35 * rng.normal(size=(n, intrinsic)).astype(np.float32)
+    x = z @ A + noise * rng.normal(size=(n, d)).astype(np.float32)
+    return x.astype(np.float32)
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_batch_build_recall_and_exact_parity(H, O, metric):
+    rng = np.random.default_rng(11 + metric)
+    n, d = 20000, 64
+    X = _clustered(rng, n, d)
+    Q = _clustered(rng, 200, d)
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=_metric_fn(H, metric), Rng=9, build_mode=H.BUILD_BATCH,
+                ef_construction=100)
+    g.add_arrays(np.arange(n), X)
+    st = g.stats()
+    assert st["dropped_proposals"] == 0
+    ek, ed, en = g.search_arrays(Q, 10, mode=H.MODE_EXACT)
+    bk, bd, bn = g.search_arrays(Q, 10, mode=H.MODE_BEAM, ef=64)
+    recall = np.mean([len(set(bk[b, : bn[b]]) & set(ek[b, : en[b]])) / 10 for b in range(len(Q))])
+    assert recall >= 0.95, recall
+    # same graph in the oracle: beam and exact identical
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=16, M0=32, Ml=0.25, EfSearch=64)
+    o.import_graph(**g.export())
+    rk, rd, rn = o.search(Q, 10, mode=O.MODE_EXACT)
+    _same_results(ek, ed, en, rk, rd, rn)
+    rk, rd, rn = o.search(Q, 10, mode=O.MODE_BEAM, ef=64)
+    _same_results(bk, bd, bn, rk, rd, rn)
