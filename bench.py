@@ -1,0 +1,298 @@
+#!/usr/bin/env python3
+"""Headline benchmark: queries/sec @ recall@10 on 1M x 768-d cosine
+(BASELINE.json configs[1]: single MI355X, batched-query HIP search, ef=64, k=10).
+
+A "step" = one batched layer-descent + layer-0 beam search of `--batch` query
+vectors already resident in HBM, through the C ABI (mhnsw_search_device).
+
+Multi-GPU (one process per GPU, torchrun):
+  --mode replica (default): every rank holds the full 1M-vector index and
+      serves its own slice of the query stream; no data-path collective
+      (per-GPU work fixed => "scaling": "weak").
+  --mode shard: node-ID range sharding -- rank r owns keys [r*n, (r+1)*n); every
+      query is searched on every shard, per-shard top-k are all-gathered over
+      RCCL (xGMI) and merged on the GPU (mhnsw_merge_topk_device).  The index
+      grows with the GPU count (BASELINE config 4: 10M over 8 GPUs).
+
+Also reported: recall@10 against the exact (MFMA brute-force) path, build
+throughput of the batched insert, the search kernel's roofline (HBM-bound;
+algorithmic bytes from in-kernel distance-evaluation / expansion counters), and
+the CPU restatement (oracle/, same algorithm, same graph) timed on a bounded
+sample on the host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import hnsw_amd as H  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--mode", choices=["replica", "shard"], default="replica")
+    p.add_argument("--n", type=int, default=1_000_000, help="vectors per index (per shard in shard mode)")
+    p.add_argument("--dim", type=int, default=768)
+    p.add_argument("--batch", type=int, default=16384, help="queries per step per GPU")
+    p.add_argument("--ef", type=int, default=64)
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--metric", choices=["cosine", "euclidean"], default="cosine")
+    p.add_argument("--M", type=int, default=16)
+    p.add_argument("--M0", type=int, default=32)
+    p.add_argument("--efc", type=int, default=128)
+    p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--intrinsic", type=int, default=16)
+    p.add_argument("--clusters", type=int, default=1000)
+    p.add_argument("--gt-queries", type=int, default=4096, help="queries scored against exact top-k")
+    p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline time box (0 disables)")
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_search.json"))
+    return p.parse_args()
+
+
+def gen_vectors(n, dim, seed, intrinsic, clusters, device, metric, offset=0):
+    """Synthetic embeddings with low intrinsic dimension: a Gaussian mixture of
+    `clusters` centres in R^intrinsic, mapped to R^dim by a fixed random linear
+    map, plus isotropic noise; L2-normalised for cosine.  Rows [offset, offset+n)
+    of the stream defined by `seed` (chunked so any slice is reproducible)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    C = torch.randn(clusters, intrinsic, generator=g, device=device)
+    A = torch.randn(intrinsic, dim, generator=g, device=device) / intrinsic ** 0.5
+    out = torch.empty(n, dim, device=device)
+    chunk = 1 << 16
+    first, last = offset // chunk, (offset + n - 1) // chunk
+    for c in range(first, last + 1):
+        gc = torch.Generator(device=device)
+        gc.manual_seed(seed * 1_000_003 + c + 1)
+        cid = torch.randint(0, clusters, (chunk,), generator=gc, device=device)
+        z = C[cid] + 0.5 * torch.randn(chunk, intrinsic, generator=gc, device=device)
+        x = z @ A + 0.05 * torch.randn(chunk, dim, generator=gc, device=device)
+        if metric == "cosine":
+            x = x / x.norm(dim=1, keepdim=True)
+        lo, hi = max(offset, c * chunk), min(offset + n, (c + 1) * chunk)
+        out[lo - offset:hi - offset] = x[lo - c * chunk:hi - c * chunk]
+    return out.contiguous()
+
+
+class Searcher:
+    def __init__(self, g, B, k, dim, device):
+        self.g, self.B, self.k, self.dim = g, B, k, dim
+        self.keys = torch.empty(B, k, dtype=torch.int64, device=device)
+        self.dist = torch.empty(B, k, dtype=torch.float32, device=device)
+        self.n = torch.empty(B, dtype=torch.int32, device=device)
+
+    def run(self, q, mode, ef):
+        s = torch.cuda.current_stream().cuda_stream
+        self.g.search_device(q.data_ptr(), q.shape[0], self.dim, self.k, self.keys.data_ptr(), self.dist.data_ptr(),
+                             self.n.data_ptr(), mode=mode, ef=ef, stream=s)
+        return self.keys, self.dist, self.n
+
+
+def shard_merge(keys, dists, n, world, k, device):
+    """all-gather per-shard top-k over RCCL, merge on the GPU."""
+    B = keys.shape[0]
+    ak = torch.empty(world, B, k, dtype=torch.int64, device=device)
+    ad = torch.empty(world, B, k, dtype=torch.float32, device=device)
+    an = torch.empty(world, B, dtype=torch.int32, device=device)
+    dist.all_gather_into_tensor(ak, keys.contiguous())
+    dist.all_gather_into_tensor(ad, dists.contiguous())
+    dist.all_gather_into_tensor(an, n.contiguous())
+    ok = torch.empty(B, k, dtype=torch.int64, device=device)
+    od = torch.empty(B, k, dtype=torch.float32, device=device)
+    on = torch.empty(B, dtype=torch.int32, device=device)
+    H.merge_topk_device(ak.data_ptr(), ad.data_ptr(), an.data_ptr(), world, B, k, ok.data_ptr(), od.data_ptr(),
+                        on.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    return ok, od, on
+
+
+def recall_at_k(res, n, truth, tn, k):
+    res, n, truth, tn = (x.cpu().numpy() for x in (res, n, truth, tn))
+    tot = 0.0
+    for b in range(res.shape[0]):
+        t = set(truth[b, : tn[b]].tolist())
+        tot += len(set(res[b, : n[b]].tolist()) & t) / max(1, min(k, len(t)))
+    return tot / res.shape[0]
+
+
+def cpu_baseline(g, queries_np, k, ef, metric, seconds):
+    """The CPU restatement (oracle/, test infrastructure) timed on this host on a
+    bounded sample: same graph, same beam algorithm; plus the reference's
+    compat Search() semantics.  Single thread, sequential queries
+    (= BatchSearch's loop, graph.go:1075)."""
+    import oracle as O  # checker / baseline only
+
+    ex = g.export()
+    o = O.Graph(metric=O.COSINE if metric == "cosine" else O.EUCLIDEAN, order=O.ORDER_REF, M=g.M,
+                M0=g.get_option("m0"), Ml=g.Ml, EfSearch=ef)
+    o.import_graph(**ex)
+    del ex
+    out = {}
+    for name, mode in (("beam", O.MODE_BEAM), ("compat", O.MODE_COMPAT)):
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds / 2 and done < len(queries_np):
+            o.search(queries_np[done:done + 32], k, mode=mode, ef=ef)
+            done += min(32, len(queries_np) - done)
+        out[name] = (done / (time.perf_counter() - t0), done)
+    return out
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    metric = H.CosineDistance if a.metric == "cosine" else H.EuclideanDistance
+
+    # ---- index --------------------------------------------------------------
+    shard = a.mode == "shard"
+    base_off = rank * a.n if shard else 0
+    X = gen_vectors(a.n, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=base_off)
+    g = H.Graph(M=a.M, Ml=0.25, EfSearch=a.ef, Distance=metric, Rng=a.seed + (rank if shard else 0),
+                build_mode=H.BUILD_BATCH, m0=a.M0, ef_construction=a.efc)
+    g.reserve(a.n, a.dim)
+    keys = np.arange(base_off, base_off + a.n, dtype=np.int64)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g.add_device(keys, X.data_ptr(), a.n, a.dim)
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t0
+    bstats = g.stats()
+
+    # ---- queries ------------------------------------------------------------
+    qseed = a.seed + 7_777
+    if shard:
+        Q = gen_vectors(a.batch, a.dim, qseed, a.intrinsic, a.clusters, device, a.metric)
+    else:
+        Q = gen_vectors(a.batch, a.dim, qseed, a.intrinsic, a.clusters, device, a.metric, offset=rank * a.batch)
+    S = Searcher(g, a.batch, a.k, a.dim, device)
+
+    def step():
+        kk, dd, nn = S.run(Q, H.MODE_BEAM, a.ef)
+        if shard and world > 1:
+            return shard_merge(kk, dd, nn, world, a.k, device)
+        return kk, dd, nn
+
+    # ---- recall vs exact ----------------------------------------------------
+    ngt = min(a.gt_queries, a.batch)
+    res_k, _, res_n = (x.clone() for x in step())
+    G = Searcher(g, ngt, a.k, a.dim, device)
+    tk, td, tn = G.run(Q[:ngt], H.MODE_EXACT, 0)
+    if shard and world > 1:
+        tk, td, tn = shard_merge(tk, td, tn, world, a.k, device)
+    torch.cuda.synchronize()
+    recall = recall_at_k(res_k[:ngt], res_n[:ngt], tk, tn, a.k)
+
+    # ---- timed steps --------------------------------------------------------
+    for _ in range(a.warmup):
+        step()
+    g.reset_stats()
+    kernel_ms = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+        kernel_ms.append(g.last_kernel_ms())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = g.stats()
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        rr = torch.tensor([recall], dtype=torch.float64, device=device)
+        dist.all_reduce(rr)
+        recall = rr.item() / world
+    elapsed = tt.item()
+
+    queries_done = a.batch * a.steps * (1 if shard else world)
+    qps = queries_done / elapsed
+
+    # roofline of the search kernel (per launch = one step on this GPU)
+    E = st["search_dist_evals"] / a.steps
+    Xp = st["search_expansions"] / a.steps
+    cap0 = a.M0 + 1
+    alg_bytes = E * 4 * a.dim + Xp * 4 * cap0 + a.batch * 4 * a.dim
+    kms = float(np.mean(kernel_ms))
+    achieved = alg_bytes / (kms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(a.pmc_json):
+        try:
+            pm = json.load(open(a.pmc_json))
+            if pm.get("n") == a.n and pm.get("dim") == a.dim and pm.get("batch") == a.batch and pm.get("ef") == a.ef:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": "queries/sec @ recall@10, 1M×768-d cosine; 1/2/4/8-GPU scaling",
+        "value": round(qps, 1),
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": (f"synthetic: {a.clusters}-centre Gaussian mixture in R^{a.intrinsic} mapped to R^{a.dim} by a "
+                 f"random linear map + N(0,0.05^2) noise, L2-normalised; seed {a.seed}; queries from the same "
+                 f"distribution (seed {qseed})"),
+        "config": {
+            "workload": f"{a.n // 1000}k x {a.dim}-d {a.metric}, batched beam search ef={a.ef} k={a.k}, "
+                        f"{a.batch} queries/step/GPU (BASELINE configs[1])",
+            "n_base": a.n * (world if shard else 1), "dim": a.dim, "batch_per_gpu": a.batch, "ef": a.ef,
+            "k": a.k, "M": a.M, "M0": a.M0, "ef_construction": a.efc,
+            "parallelism": f"{'shard' if shard else 'replica'}{world}",
+        },
+        "recall_at_10": round(recall, 4),
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "k_search_beam", "kernel_ms": round(kms, 4),
+            "alg_bytes_per_launch": int(alg_bytes),
+            "dist_evals_per_query": round(E / a.batch, 1), "expansions_per_query": round(Xp / a.batch, 1),
+        },
+        "build": {"inserts_per_s": round(a.n / build_s, 1), "seconds": round(build_s, 2),
+                  "dist_evals_per_insert": round(bstats["build_dist_evals"] / a.n, 1),
+                  "dropped_proposals": bstats["dropped_proposals"]},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and a.cpu_seconds > 0:
+        qn = Q[: min(a.batch, 4096)].cpu().numpy()
+        cb = cpu_baseline(g, qn, a.k, a.ef, a.metric, a.cpu_seconds)
+        out["cpu_baseline"] = {
+            "value": round(cb["beam"][0], 2), "unit": "queries/s", "cores": 1, "kind": "port",
+            "sample": f"{cb['beam'][1]} of the same queries, same 1M graph, oracle beam search (ORDER_REF "
+                      f"sequential fp32), single thread, ~{a.cpu_seconds / 2:.0f}s time box",
+            "compat_search_qps": round(cb["compat"][0], 2), "compat_sample": cb["compat"][1],
+            "host_cpus": os.cpu_count(),
+        }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

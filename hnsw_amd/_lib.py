@@ -66,10 +66,23 @@ class HnswError(RuntimeError):
         self.code = code
 
 
+def _share_hip_runtime_with_torch():
+    """One HIP runtime per process.  torch links its bundled libamdhip64.so by
+    file name, so if libmhnsw.so were loaded first (pulling /opt/rocm's copy,
+    same soname) torch would load a second runtime that cannot see the GPU.
+    Importing torch first makes our NEEDED libamdhip64.so.7 /
+    libhsa-runtime64.so.1 resolve to torch's already-loaded copies."""
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def load() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    _share_hip_runtime_with_torch()
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
     lib = C.CDLL(LIB_PATH)

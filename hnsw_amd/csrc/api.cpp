@@ -79,6 +79,8 @@ struct mhnsw_index {
     size_t touched_cap = 0;
     int32_t* touched_cnt = nullptr;
     int32_t* d_layer_entry = nullptr;
+    LayerDev* d_layers = nullptr;
+    LayerDev layers_host[MH_MAXL] = {};
     unsigned long long* d_stats = nullptr;
     int* d_err = nullptr;
     std::vector<Layer> layers;
@@ -267,22 +269,36 @@ int ensure_capacity(mhnsw_index* h, int64_t need) {
     return 0;
 }
 
+// mirror the per-layer pointers into the device table read by the kernels
+int sync_layer_table(mhnsw_index* h) {
+    LayerDev t[MH_MAXL];
+    memset(t, 0, sizeof(t));
+    for (int l = 0; l < (int)h->layers.size(); ++l) {
+        t[l].deg = h->layers[l].deg;
+        t[l].adj = h->layers[l].adj;
+        t[l].adjd = h->layers[l].adjd;
+        t[l].cap = h->layers[l].cap;
+    }
+    if (memcmp(t, h->layers_host, sizeof(t)) == 0) return 0;
+    memcpy(h->layers_host, t, sizeof(t));
+    HIPCHK(h, hipMemcpyAsync(h->d_layers, h->layers_host, sizeof(t), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
 GraphDev graph_view(const mhnsw_index* h) {
     GraphDev g;
     memset(&g, 0, sizeof(g));
     g.vecs = h->vecs;
     g.norms = h->norms;
     g.keys = h->keys;
-    for (int l = 0; l < (int)h->layers.size(); ++l) {
-        g.deg[l] = h->layers[l].deg;
-        g.adj[l] = h->layers[l].adj;
-        g.adjd[l] = h->layers[l].adjd;
-        g.cap[l] = h->layers[l].cap;
-    }
+    g.layers = h->d_layers;
     g.pitch = h->pitch;
     g.dim = h->dim;
     g.metric = h->metric;
     g.nlayers = (int)h->layers.size();
+    g.capn = (uint32_t)std::max<int64_t>(h->capn, 1);
+    g.err = h->d_err;
     return g;
 }
 
@@ -321,6 +337,7 @@ int run_build_compat(mhnsw_index* h, int64_t n0, int64_t n1) {
     if (h->M + 1 > 64) return fail(h, MHNSW_EUNSUPPORTED, "compat build supports M <= 63");
     int r;
     if ((r = sync_layer_entries(h))) return r;
+    if ((r = sync_layer_table(h))) return r;
     if ((r = zero_err(h))) return r;
     CompatBuildArgs a;
     a.g = graph_view(h);
@@ -341,6 +358,8 @@ int run_build_compat(mhnsw_index* h, int64_t n0, int64_t n1) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
     if (err & 1) return fail(h, MHNSW_EINTERNAL, "visited set overflow (raise vis_log2)");
     if (err & 2) return fail(h, MHNSW_EINTERNAL, "no nodes found in neighborhood search");
+    if (err & 4) return fail(h, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
+    if (err & 8) return fail(h, MHNSW_EINTERNAL, "replenish candidate heap overflow");
     return 0;
 }
 
@@ -349,6 +368,8 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
     HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(h->cur_entry + a0), (int)entry, (size_t)(a1 - a0), h->stream));
     int maxlvl = 0;
     for (int64_t i = a0; i < a1; ++i) maxlvl = std::max(maxlvl, h->hlevels[i]);
+    int r;
+    if ((r = sync_layer_table(h))) return r;
     const int efc = h->efc > 0 ? h->efc : h->ef;
     for (int l = top; l >= 0; --l) {
         const int mcap = l == 0 ? m0_of(h) : h->M;
@@ -379,6 +400,7 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
 
 int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1) {
     int r;
+    if ((r = zero_err(h))) return r;
     if (!h->inc_src) {
         if ((r = grow(h, h->inc_src, 0, h->capn * h->inc_cap, 0))) return r;
         if ((r = grow(h, h->inc_dist, 0, h->capn * h->inc_cap, 0))) return r;
@@ -424,6 +446,10 @@ int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1) {
         if ((r = run_batch_layers(h, i, j, top, entry))) return r;
         i = j;
     }
+    int err = 0;
+    HIPCHK(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (err & 4) return fail(h, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
     return 0;
 }
 
@@ -557,6 +583,7 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             (r = ensure_buf(h, h->cand, (size_t)qc * kk)))
             return r;
         LCHK(h, launch_norms(h->qpad.p, 0, B, h->pitch, h->lpr, h->vpl, h->qnorm.p, s));
+        if ((r = sync_layer_table(h))) return r;
         GraphDev g = graph_view(h);
         if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
         for (int64_t q0 = 0; q0 < B; q0 += qc) {
@@ -584,6 +611,7 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));
     } else {
         if ((r = sync_layer_entries(h))) return r;
+        if ((r = sync_layer_table(h))) return r;
         SearchArgs a;
         a.g = graph_view(h);
         a.q = h->qpad.p;
@@ -622,6 +650,7 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         int err = 0;
         HIPCHK(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(h, hipStreamSynchronize(s));
+        if (err & 4) return fail(h, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
         if (err) return fail(h, MHNSW_EINTERNAL, "visited set overflow (raise vis_log2)");
     }
     return 0;
@@ -656,7 +685,8 @@ int mhnsw_create(int metric, int M, double ml, int ef_search, uint64_t seed, mhn
     }
     if (hipMalloc(&h->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&h->d_err, sizeof(int)) != hipSuccess || hipMalloc(&h->touched_cnt, 16) != hipSuccess ||
-        hipMalloc(&h->d_layer_entry, MH_MAXL * 4) != hipSuccess || hipEventCreate(&h->ev0) != hipSuccess ||
+        hipMalloc(&h->d_layer_entry, MH_MAXL * 4) != hipSuccess ||
+        hipMalloc(&h->d_layers, MH_MAXL * sizeof(LayerDev)) != hipSuccess || hipEventCreate(&h->ev0) != hipSuccess ||
         hipEventCreate(&h->ev1) != hipSuccess || hipMemset(h->d_stats, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
         mhnsw_destroy(h);
         return fail(nullptr, MHNSW_EDEVICE, "device initialisation failed");
@@ -682,6 +712,7 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->touched);
     F(h->touched_cnt);
     F(h->d_layer_entry);
+    F(h->d_layers);
     F(h->d_stats);
     F(h->d_err);
     for (auto& L : h->layers) {
@@ -836,23 +867,12 @@ int mhnsw_lookup(mhnsw_index* h, int64_t key, float* out) {
 
 int mhnsw_distance_device(int metric, const float* d_q, const float* d_X, int64_t n, int dim, float* d_out,
                           void* stream) {
-    int lpr, vpl;
     if (metric != COSINE && metric != EUCLIDEAN) return fail(nullptr, MHNSW_EINVAL, "Distance function must be set");
-    if (!pick_cfg(dim, lpr, vpl)) return fail(nullptr, MHNSW_EUNSUPPORTED, "dimension %d not supported", dim);
+    if (dim <= 0) return fail(nullptr, MHNSW_EINVAL, "dimension must be positive");
     if (n <= 0) return 0;
-    const int pitch = pitch_of(lpr, vpl);
-    hipStream_t s = (hipStream_t)stream;
-    float *qp = nullptr, *xp = nullptr;
-    if (hipMallocAsync((void**)&qp, (size_t)pitch * 4, s) != hipSuccess ||
-        hipMallocAsync((void**)&xp, (size_t)n * pitch * 4, s) != hipSuccess)
-        return fail(nullptr, MHNSW_ENOMEM, "device allocation failed");
-    int r = 0;
-    if (launch_pad_rows(d_q, 1, dim, qp, pitch, s) || launch_pad_rows(d_X, n, dim, xp, pitch, s) ||
-        launch_sweep(qp, xp, n, pitch, lpr, vpl, metric, d_out, s))
-        r = fail(nullptr, MHNSW_EDEVICE, "sweep launch failed");
-    (void)hipFreeAsync(qp, s);
-    (void)hipFreeAsync(xp, s);
-    return r;
+    if (launch_sweep_raw(d_q, d_X, n, dim, metric, d_out, (hipStream_t)stream))
+        return fail(nullptr, MHNSW_EDEVICE, "sweep launch failed");
+    return 0;
 }
 
 int mhnsw_distance(int metric, const float* q, const float* X, int64_t n, int dim, float* out) {
@@ -981,6 +1001,9 @@ int mhnsw_stats(const mhnsw_index* h, int64_t* out, int n) {
     unsigned long long d[8];
     HIPCHK(hh, hipDeviceSynchronize());
     HIPCHK(hh, hipMemcpy(d, h->d_stats, sizeof(d), hipMemcpyDeviceToHost));
+    int err = 0;
+    HIPCHK(hh, hipMemcpy(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (err & 4) return fail(hh, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
     const int64_t v[7] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4],
                           (int64_t)d[5], (int64_t)d[6], h->stats_host[6]};
     for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];

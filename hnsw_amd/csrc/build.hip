@@ -30,14 +30,15 @@ struct BuildSmem {
     CompatSmem cs;
     float* hd;  // replenish heap
     uint32_t* hi;
+    int hcap;
 };
 
 template <class C, int G>
 __device__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v) {
     const int lane = lane_id();
-    const int capl = g.cap[l];
-    int32_t* row = g.adj[l] + (size_t)n * capl;
-    const int d = ld_i32<true>(g.deg[l] + n);
+    const int capl = g.layers[l].cap;
+    int32_t* row = g.layers[l].adj + (size_t)n * capl;
+    const int d = ld_i32<true>(g.layers[l].deg + n);
     if (d <= 0) return;
     const bool hit = lane < d && (uint32_t)ld_i32<true>(row + lane) == v;
     const unsigned long long m = __ballot(hit);
@@ -47,7 +48,7 @@ __device__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v) {
     build_sync();
     if (lane == 0) {
         st_i32(row + pos, last);
-        st_i32(g.deg[l] + n, d - 1);
+        st_i32(g.layers[l].deg + n, d - 1);
     }
     build_sync();
 }
@@ -55,16 +56,16 @@ __device__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v) {
 // append nw to n's neighbour set if absent; returns the new degree
 __device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw) {
     const int lane = lane_id();
-    const int capl = g.cap[l];
-    int32_t* row = g.adj[l] + (size_t)n * capl;
-    int d = ld_i32<true>(g.deg[l] + n);
+    const int capl = g.layers[l].cap;
+    int32_t* row = g.layers[l].adj + (size_t)n * capl;
+    int d = ld_i32<true>(g.layers[l].deg + n);
     if (d < 0) d = 0;  // graph.go:46-48 allocate the map
     const bool pres = lane < d && (uint32_t)ld_i32<true>(row + lane) == nw;
     const bool present = __ballot(pres) != 0;
     build_sync();
     if (lane == 0) {
         if (!present) st_i32(row + d, (int32_t)nw);
-        st_i32(g.deg[l] + n, present ? d : d + 1);
+        st_i32(g.layers[l].deg + n, present ? d : d + 1);
     }
     build_sync();
     return present ? d : d + 1;
@@ -74,8 +75,8 @@ __device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw) {
 template <class C, int G>
 __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err) {
     const int lane = lane_id();
-    const int capl = g.cap[l];
-    int dn = ld_i32<true>(g.deg[l] + n);
+    const int capl = g.layers[l].cap;
+    int dn = ld_i32<true>(g.layers[l].deg + n);
     if (dn < 0) dn = 0;
     if (dn >= m) return;
     const int vsize = 1 << S.cs.vlog2, vmask = vsize - 1;
@@ -85,7 +86,7 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
     uint32_t mine = 0xFFFFFFFFu;
     int64_t key = INT64_MAX;
     if (lane < dn) {
-        mine = (uint32_t)ld_i32<true>(g.adj[l] + (size_t)n * capl + lane);
+        mine = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane));
         key = g.keys[mine];
     }
     bitonic64(key, mine);
@@ -96,12 +97,12 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
     GHeap h{S.hd, S.hi, 0};
     for (int j = 0; j < dn; ++j) {  // graph.go:192-210
         const uint32_t nb = rl_u(mine, j);
-        const int dnb = ld_i32<true>(g.deg[l] + nb);
+        const int dnb = min(ld_i32<true>(g.layers[l].deg + nb), capl);
         if (dnb < 0) continue;
         uint32_t th = 0xFFFFFFFFu;
         int64_t tk = INT64_MAX;
         if (lane < dnb) {
-            th = (uint32_t)ld_i32<true>(g.adj[l] + (size_t)nb * capl + lane);
+            th = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)nb * capl + lane));
             tk = g.keys[th];
         }
         bitonic64(tk, th);
@@ -112,11 +113,14 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
         const uint32_t cid = compact(th, pr == 1, cnt);
         st.E += cnt;
         eval_list<C, G>(g, q, qn, cid, cnt, COSINE,  // graph.go:204 hard-coded cosine
-                        [&](float d, uint32_t u) { gh_push(h, d, u); });
+                        [&](float d, uint32_t u) {
+                            if (h.n < S.hcap) gh_push(h, d, u);
+                            else err |= 8;
+                        });
     }
     // graph.go:213-218 (len < m before every add: addNeighbor cannot evict)
     while (h.n > 0) {
-        int cur = ld_i32<true>(g.deg[l] + n);
+        int cur = ld_i32<true>(g.layers[l].deg + n);
         if (cur < 0) cur = 0;
         if (cur >= m) break;
         float bd;
@@ -131,13 +135,13 @@ template <class C, int G>
 __device__ void add_neighbor(const GraphDev& g, int l, uint32_t n, uint32_t nw, int m, BuildSmem& S, WaveStats& st,
                              int& err) {
     const int lane = lane_id();
-    const int capl = g.cap[l];
+    const int capl = g.layers[l].cap;
     const int d = list_append(g, l, n, nw);
     if (d <= m) return;
     uint32_t nb = 0xFFFFFFFFu;
     int64_t key = INT64_MAX;
     if (lane < d) {
-        nb = (uint32_t)ld_i32<true>(g.adj[l] + (size_t)n * capl + lane);
+        nb = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane));
         key = g.keys[nb];
     }
     bitonic64(key, nb);  // Go map order -> ascending key
@@ -155,7 +159,7 @@ __device__ void add_neighbor(const GraphDev& g, int l, uint32_t n, uint32_t nw, 
     });
     if (worst == EMPTY_ID) return;
     list_remove<C, G>(g, l, n, worst);  // graph.go:74
-    if (ld_i32<true>(g.deg[l] + worst) >= 0) list_remove<C, G>(g, l, worst, n);  // graph.go:76-78
+    if (ld_i32<true>(g.layers[l].deg + worst) >= 0) list_remove<C, G>(g, l, worst, n);  // graph.go:76-78
     replenish<C, G>(g, l, worst, m, S, st, err);  // graph.go:79
 }
 
@@ -180,6 +184,7 @@ __global__ __launch_bounds__(64) void k_build_compat(CompatBuildArgs a) {
     S.hd = reinterpret_cast<float*>(p);
     p += hcap;
     S.hi = p;
+    S.hcap = hcap;
     WaveStats st;
     int err = 0;
     int top = -1;
@@ -196,7 +201,7 @@ __global__ __launch_bounds__(64) void k_build_compat(CompatBuildArgs a) {
             const int32_t ent = a.layer_entry[l];
             if (ent == (int32_t)id) {  // graph.go:485-488: empty layer, no search
                 build_sync();
-                if (lane == 0) st_i32(a.g.deg[l] + id, -1);
+                if (lane == 0) st_i32(a.g.layers[l].deg + id, -1);
                 build_sync();
                 continue;
             }
@@ -210,7 +215,7 @@ __global__ __launch_bounds__(64) void k_build_compat(CompatBuildArgs a) {
             if (level >= l) {       // graph.go:510-521
                 const uint32_t nbh = lane < cnt ? S.cs.ri[lane] : 0u;
                 build_sync();
-                if (lane == 0) st_i32(a.g.deg[l] + id, -1);
+                if (lane == 0) st_i32(a.g.layers[l].deg + id, -1);
                 build_sync();
                 for (int j = 0; j < cnt; ++j) {
                     const uint32_t c = rl_u(nbh, j);
@@ -297,10 +302,10 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
                 ++nsel;
             }
         }
-        const int capl = a.g.cap[l];
+        const int capl = a.g.layers[l].cap;
         if (lane < nsel) {
-            a.g.adj[l][(size_t)u * capl + lane] = (int32_t)sel;
-            a.g.adjd[l][(size_t)u * capl + lane] = seld;
+            a.g.layers[l].adj[(size_t)u * capl + lane] = (int32_t)sel;
+            a.g.layers[l].adjd[(size_t)u * capl + lane] = seld;
             const int slot = atomicAdd(&a.inc_cnt[sel], 1);
             if (slot < a.inc_cap) {
                 a.inc_src[(size_t)sel * a.inc_cap + slot] = u;
@@ -313,7 +318,7 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
                 a.touched[t] = sel;
             }
         }
-        if (lane == 0) a.g.deg[l][u] = nsel;
+        if (lane == 0) a.g.layers[l].deg[u] = nsel;
     }
     if (lane == 0) {
         atomicAdd(&a.stats[0], st.E);
@@ -330,8 +335,8 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
     if ((int)blockIdx.x >= n_t) return;
     const uint32_t v = a.touched[blockIdx.x];
     const int l = a.layer;
-    const int capl = a.g.cap[l];
-    int d = a.g.deg[l][v];
+    const int capl = a.g.layers[l].cap;
+    int d = a.g.layers[l].deg[v];
     if (d < 0) d = 0;
     int nin = a.inc_cnt[v];
     if (nin > a.inc_cap) nin = a.inc_cap;
@@ -340,8 +345,8 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
         float dd = __int_as_float(0x7f800000);
         uint32_t ii = EMPTY_ID;
         if (e < d) {
-            ii = (uint32_t)a.g.adj[l][(size_t)v * capl + e];
-            dd = a.g.adjd[l][(size_t)v * capl + e];
+            ii = (uint32_t)a.g.layers[l].adj[(size_t)v * capl + e];
+            dd = a.g.layers[l].adjd[(size_t)v * capl + e];
         } else if (e < tot) {
             ii = a.inc_src[(size_t)v * a.inc_cap + (e - d)];
             dd = a.inc_dist[(size_t)v * a.inc_cap + (e - d)];
@@ -366,12 +371,12 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
     for (int h = 0; h < 2; ++h) {
         const int e = lane + 64 * h;
         if (e < tot && rank[h] < keep) {
-            a.g.adj[l][(size_t)v * capl + rank[h]] = (int32_t)mi[h];
-            a.g.adjd[l][(size_t)v * capl + rank[h]] = md[h];
+            a.g.layers[l].adj[(size_t)v * capl + rank[h]] = (int32_t)mi[h];
+            a.g.layers[l].adjd[(size_t)v * capl + rank[h]] = md[h];
         }
     }
     if (lane == 0) {
-        a.g.deg[l][v] = keep;
+        a.g.layers[l].deg[v] = keep;
         a.inc_cnt[v] = 0;
     }
 }
@@ -396,8 +401,10 @@ static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
     X(64, 8, 2)
 
 int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, hipStream_t s) {
+    // the sequential build keeps three query rows live (search / addNeighbor /
+    // replenish): two rows in flight per group keeps it spill-free
 #define X_(L, V, G) \
-    if (lpr == L && vpl == V) return launch_build_compat_t<Cfg<L, V>, G>(a, s);
+    if (lpr == L && vpl == V) return launch_build_compat_t<Cfg<L, V>, (G < 2 ? G : 2)>(a, s);
     MH_FOR_EACH_CFG(X_)
 #undef X_
     return -3;

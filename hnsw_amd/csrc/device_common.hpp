@@ -29,19 +29,36 @@ constexpr uint32_t VIS_EMPTY = 0xFFFFFFFFu;
 
 enum Metric { COSINE = 0, EUCLIDEAN = 1 };
 
+// one layer of the graph in HBM (fixed-stride adjacency rows)
+struct LayerDev {
+    int32_t* deg;  // [cap_nodes]: -2 absent, -1 nil neighbour map, >=0 degree
+    int32_t* adj;  // [cap_nodes * cap] internal ids
+    float* adjd;   // [cap_nodes * cap] edge distances (batch build)
+    int cap;
+    int pad_;
+};
+
 struct GraphDev {
-    const float* vecs;   // [cap_nodes * pitch] row-major, zero padded
-    const float* norms;  // [cap_nodes] canonical |x|
-    const int64_t* keys; // [cap_nodes]
-    int32_t* deg[MH_MAXL];  // per layer [cap_nodes]: -2 absent, -1 nil map, >=0 degree
-    int32_t* adj[MH_MAXL];  // per layer [cap_nodes * cap[l]] internal ids
-    float* adjd[MH_MAXL];   // per layer [cap_nodes * cap[l]] edge distances (batch build)
-    int cap[MH_MAXL];
+    const float* vecs;        // [cap_nodes * pitch] row-major, zero padded
+    const float* norms;       // [cap_nodes] canonical |x|
+    const int64_t* keys;      // [cap_nodes]
+    const LayerDev* layers;   // [nlayers] device table (read-only in kernels)
     int pitch;
     int dim;
     int metric;
     int nlayers;
+    uint32_t capn;  // rows allocated: every gathered id is checked against it
+    int* err;       // bit 4: out-of-range id seen (load clamped, no fault)
 };
+
+// bounds guard for gathered ids: records the violation and clamps to row 0
+__device__ __forceinline__ uint32_t guard_id(const GraphDev& g, uint32_t id) {
+    if (id >= g.capn) {
+        atomicOr(g.err, 4);
+        return 0u;
+    }
+    return id;
+}
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
@@ -123,6 +140,12 @@ __device__ __forceinline__ float query_norm(const QReg<C>& q) {
     return sqrtf(seg_allreduce<C::LPR>(acc));
 }
 
+// branch-free select (keeps register arrays out of scratch: a `c ? p[i] : p[j]`
+// on an array is otherwise rewritten into a dynamically indexed stack load)
+__device__ __forceinline__ float bsel(uint32_t mask, float a, float b) {
+    return __uint_as_float((__float_as_uint(a) & mask) | (__float_as_uint(b) & ~mask));
+}
+
 // Transposed reduce-scatter of G per-lane partials over an LPR-lane segment.
 // On return lane l holds the full sum of row g(l) = (l % LPR) >> (LOG_LPR - log2 G).
 template <int G, int LPR>
@@ -135,11 +158,12 @@ __device__ __forceinline__ float reduce_rows(float (&p)[G]) {
         const int cnt = G >> s;
         if (cnt > 1) {
             const int half = cnt >> 1;
-            const bool up = (lane & o) != 0;
+            const uint32_t up = (lane & o) ? 0xFFFFFFFFu : 0u;
 #pragma unroll
             for (int i = 0; i < half; ++i) {
-                float send = up ? p[i] : p[i + half];
-                float keep = up ? p[i + half] : p[i];
+                const float lo = p[i], hi = p[i + half];
+                const float send = bsel(up, lo, hi);
+                const float keep = bsel(up, hi, lo);
                 p[i] = keep + __shfl_xor(send, o, 64);
             }
         } else {

@@ -44,7 +44,7 @@ __device__ __forceinline__ void eval_list(const GraphDev& g, const QReg<C>& q, f
                 ids[gg] = rl_u(cid, (base + gg) & 63);
             else
                 ids[gg] = shfl_u(cid, t & 63);
-            if (!valid[gg]) ids[gg] = 0;
+            ids[gg] = valid[gg] ? guard_id(g, ids[gg]) : 0u;
         }
         float s;
         if (metric == EUCLIDEAN)
@@ -54,7 +54,7 @@ __device__ __forceinline__ void eval_list(const GraphDev& g, const QReg<C>& q, f
         const int town = base + RM::owned_row(lane);
         const uint32_t idown = shfl_u(cid, town & 63);
         float xn = 1.f;
-        if (metric == COSINE && town < cnt) xn = g.norms[idown];
+        if (metric == COSINE && town < cnt) xn = g.norms[guard_id(g, idown)];
         const float dist = finalize(metric, s, xn, qn);
 #pragma unroll
         for (int t = 0; t < RM::T; ++t) {
@@ -82,7 +82,7 @@ struct WaveStats {
 // beam: sorted list of <= ef entries; stop when every entry is expanded
 // ---------------------------------------------------------------------------
 template <class C, int R, int G, bool COH = false>
-__device__ void beam_layer(const GraphDev& g, int layer, uint32_t entry, int ef, const QReg<C>& q, float qn,
+__device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_t entry, int ef, const QReg<C>& q, float qn,
                            BList<R>& L, uint32_t* vis, int vlog2, WaveStats& st) {
     const int lane = lane_id();
     const int vsize = 1 << vlog2, vmask = vsize - 1;
@@ -94,20 +94,23 @@ __device__ void beam_layer(const GraphDev& g, int layer, uint32_t entry, int ef,
     int vcount = 1;
     eval_list<C, G>(g, q, qn, entry, 1, g.metric, [&](float d, uint32_t u) { bl_insert(L, ef, d, u); });
     st.E += 1;
-    const int32_t* degp = g.deg[layer];
-    const int32_t* adjp = g.adj[layer];
-    const int capl = g.cap[layer];
+    const int32_t* degp = g.layers[layer].deg;
+    const int32_t* adjp = g.layers[layer].adj;
+    const int capl = g.layers[layer].cap;
     for (;;) {
         const uint32_t cur = bl_next(L);
         if (cur == EMPTY_ID) break;
         st.X += 1;
-        const int deg = ld_i32<COH>(degp + cur);
+        const int deg = min(ld_i32<COH>(degp + guard_id(g, cur)), capl);
         if (deg <= 0) continue;
         const bool have = lane < deg;
         uint32_t nb = 0;
         if (have) nb = (uint32_t)ld_i32<COH>(adjp + (size_t)cur * capl + lane);
         int pr = 0;
-        if (have && nb != 0xFFFFFFFFu) pr = vis_probe(vis, vmask, nb);
+        if (have && nb != 0xFFFFFFFFu) {
+            nb = guard_id(g, nb);
+            pr = vis_probe(vis, vmask, nb);
+        }
         vcount += __popcll(__ballot(pr == 1));
         int cnt;
         const uint32_t cid = compact(nb, pr != 0, cnt);
@@ -137,7 +140,7 @@ struct CompatSmem {
 };
 
 template <class C, int G, bool COH = false>
-__device__ int compat_layer(const GraphDev& g, int layer, uint32_t entry, int k, int ef, const QReg<C>& q, float qn,
+__device__ __forceinline__ int compat_layer(const GraphDev& g, int layer, uint32_t entry, int k, int ef, const QReg<C>& q, float qn,
                             CompatSmem& S, WaveStats& st, int& err) {
     const int lane = lane_id();
     if (entry == EMPTY_ID) return 0;
@@ -151,22 +154,22 @@ __device__ int compat_layer(const GraphDev& g, int layer, uint32_t entry, int k,
     if (lane == 0) vis_probe(S.vis, vmask, entry);  // graph.go:123
     gh_push(cand, d0, entry);                        // graph.go:109-114
     gh_push(res, cand.d[0], cand.id[0]);             // graph.go:122
-    const int32_t* degp = g.deg[layer];
-    const int32_t* adjp = g.adj[layer];
-    const int capl = g.cap[layer];
+    const int32_t* degp = g.layers[layer].deg;
+    const int32_t* adjp = g.layers[layer].adj;
+    const int capl = g.layers[layer].cap;
     while (cand.n > 0) {
         float cdist;
         uint32_t cur;
         gh_pop(cand, cdist, cur);  // graph.go:127
         bool improved = false;
-        const int deg = ld_i32<COH>(degp + cur);
+        const int deg = min(ld_i32<COH>(degp + guard_id(g, cur)), capl);
         if (deg < 0) continue;  // graph.go:131-133 (nil neighbor map)
         st.X += 1;
         const bool have = lane < deg;
         uint32_t nb = 0xFFFFFFFFu;
         int64_t key = INT64_MAX;
         if (have) {
-            nb = (uint32_t)ld_i32<COH>(adjp + (size_t)cur * capl + lane);
+            nb = guard_id(g, (uint32_t)ld_i32<COH>(adjp + (size_t)cur * capl + lane));
             key = g.keys[nb];
         }
         bitonic64(key, nb);  // graph.go:137-138 ascending key order

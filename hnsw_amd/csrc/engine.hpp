@@ -46,6 +46,7 @@ int launch_pad_rows(const float* src, int64_t n, int dim, float* dst, int pitch,
 int launch_norms(const float* X, int64_t n0, int64_t n1, int pitch, int lpr, int vpl, float* out, hipStream_t s);
 int launch_sweep(const float* q, const float* X, int64_t n, int pitch, int lpr, int vpl, int metric, float* out,
                  hipStream_t s);
+int launch_sweep_raw(const float* q, const float* X, int64_t n, int dim, int metric, float* out, hipStream_t s);
 int launch_search_beam(const SearchArgs& a, int lpr, int vpl, hipStream_t s);
 int launch_search_compat(const SearchArgs& a, int lpr, int vpl, hipStream_t s);
 

@@ -105,6 +105,46 @@ __global__ __launch_bounds__(256) void k_sweep(const float* __restrict__ qp, con
     if (rown < n && (lane & (GROUP - 1)) == 0) out[rown] = d;
 }
 
+// Allocation-free sweep over raw rows (dim-contiguous, any alignment): one
+// wave per row, lane l owns elements e with (e/4) mod 64 == l (canonical order).
+__global__ __launch_bounds__(256) void k_sweep_raw(const float* __restrict__ q, const float* __restrict__ X,
+                                                   int64_t n, int dim, int metric, float* __restrict__ out) {
+    const int lane = lane_id();
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const float* x = X + (size_t)row * dim;
+    float acc = 0.f, xx = 0.f, qq = 0.f;
+    for (int base = 4 * lane; base < dim; base += 256) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = base + j;
+            if (e < dim) {
+                const float a = x[e], b = q[e];
+                if (metric == EUCLIDEAN) {
+                    const float t = a - b;
+                    acc = fmaf(t, t, acc);
+                } else {
+                    acc = fmaf(a, b, acc);
+                    xx = fmaf(a, a, xx);
+                    qq = fmaf(b, b, qq);
+                }
+            }
+        }
+    }
+    acc = seg_allreduce<64>(acc);
+    if (metric == COSINE) {
+        xx = seg_allreduce<64>(xx);
+        qq = seg_allreduce<64>(qq);
+    }
+    if (lane == 0) out[row] = finalize(metric, acc, sqrtf(xx), sqrtf(qq));
+}
+
+int launch_sweep_raw(const float* q, const float* X, int64_t n, int dim, int metric, float* out, hipStream_t s) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_sweep_raw, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, q, X, n, dim, metric, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 template <class C>
 static int launch_norms_t(const float* X, int64_t n0, int64_t n1, int pitch, float* out, hipStream_t s) {
     const int64_t rows = n1 - n0;

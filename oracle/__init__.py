@@ -60,6 +60,7 @@ def lib():
         L.og_layer_entry.restype = C.c_int32
         L.og_layer_entry.argtypes = [C.c_void_p, C.c_int]
         L.og_random_level.argtypes = [C.c_void_p]
+        L.og_preview_levels.argtypes = [C.c_void_p, C.c_int64, i32p]
         L.og_add.argtypes = [C.c_void_p, i64p, f32p, C.c_int64, C.c_int, i32p]
         L.og_search.argtypes = [C.c_void_p, f32p, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int,
                                 i64p, i64p, f32p, i32p]
@@ -161,6 +162,11 @@ class Graph:
 
     def random_level(self):
         return lib().og_random_level(self._h)
+
+    def preview_levels(self, n):
+        out = np.zeros(n, np.int32)
+        lib().og_preview_levels(self._h, n, _p(out, C.c_int32))
+        return out
 
     def add(self, keys, vecs, levels=None):
         keys = np.ascontiguousarray(keys, dtype=np.int64)

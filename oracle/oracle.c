@@ -712,6 +712,28 @@ int og_random_level(og_graph *g) {
     return max;
 }
 
+/* levels the next n Adds would draw (graph.go:388-417 with the layer-0 size
+ * growing by one per insert); does not consume the RNG */
+int og_preview_levels(og_graph *g, int64_t n, int32_t *out) {
+    uint64_t s = g->rng;
+    int le = g->layers_exist;
+    int64_t cnt = og_len(g);
+    for (int64_t i = 0; i < n; ++i) {
+        int max = 1;
+        if (le) max = og_max_level(g->ml, cnt + i);
+        int lv = max;
+        for (int level = 0; level < max; ++level) {
+            if (og_rng_next(&s) > g->ml) {
+                lv = level;
+                break;
+            }
+        }
+        out[i] = lv;
+        le = 1;
+    }
+    return OG_OK;
+}
+
 /* graph.go:437-531 Graph.Add (sequential, compat) */
 int og_add(og_graph *g, const int64_t *keys, const float *vecs, int64_t n, int dim, const int32_t *levels) {
     int rc = og_validate(g);

@@ -82,6 +82,8 @@ int64_t og_layer_count(og_graph *g, int layer);
 int32_t og_layer_entry(og_graph *g, int layer);
 /* draw the level the next Add would use (consumes RNG) */
 int og_random_level(og_graph *g);
+/* levels the next n Adds would draw (layer-0 size growing per insert; RNG untouched) */
+int og_preview_levels(og_graph *g, int64_t n, int32_t *out);
 
 /* Graph.Add (compat, sequential). levels may be NULL (drawn from the RNG). */
 int og_add(og_graph *g, const int64_t *keys, const float *vecs, int64_t n, int dim,

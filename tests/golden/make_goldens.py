@@ -91,7 +91,7 @@ def oracle_fixtures():
         Q = rng.uniform(-1, 1, (32, d)).astype(np.float32)
         keys = rng.permutation(10 * n)[:n].astype(np.int64)
         g = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=ml, EfSearch=ef, seed=1234)
-        levels = np.array([g.random_level() for _ in range(n)], np.int32)
+        levels = g.preview_levels(n)
         g = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=ml, EfSearch=ef, seed=1234)
         g.add(keys, X, levels)
         out[f"{name}/X"] = X

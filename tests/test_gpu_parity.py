@@ -21,11 +21,18 @@ def _bits(x):
 
 def _levels(O, metric, M, ml, ef, seed, n):
     g = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=ml, EfSearch=ef, seed=seed)
-    return np.array([g.random_level() for _ in range(n)], np.int32)
+    return g.preview_levels(n)
 
 
 def _metric_fn(H, metric):
     return H.CosineDistance if metric == 0 else H.EuclideanDistance
+
+
+def _bit_equal(a, b):
+    """bitwise equality, any NaN equal to any NaN (NaN sign/payload is not meaningful)"""
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    na, nb = np.isnan(a), np.isnan(b)
+    return np.array_equal(na, nb) and np.array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
 
 
 def _same_graph(a, b):
@@ -46,7 +53,7 @@ def _same_results(gk, gd, gn, rk, rd, rn, bitwise=True):
         n = gn[b]
         assert gk[b, :n].tolist() == rk[b, :n].tolist(), b
         if bitwise:
-            assert np.array_equal(gd[b, :n].view(np.uint32), rd[b, :n].view(np.uint32)), b
+            assert _bit_equal(gd[b, :n], rd[b, :n]), b
 
 
 @pytest.fixture(scope="module")
@@ -76,7 +83,7 @@ def test_distance_sweep_bitwise(H, O, dim):
         got = fn.sweep(q, X)
         dev = np.array([O.distance(metric, O.ORDER_DEV, x, q) for x in X], np.float32)
         refd = np.array([O.distance(metric, O.ORDER_REF, x, q) for x in X], np.float32)
-        assert np.array_equal(got.view(np.uint32), dev.view(np.uint32)), (metric, dim)
+        assert _bit_equal(got, dev), (metric, dim)
         ok = ~np.isnan(refd)
         assert np.array_equal(np.isnan(got), np.isnan(refd))
         scale = np.maximum(1.0, np.abs(refd[ok])) if metric == O.EUCLIDEAN else 1.0
