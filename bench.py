@@ -51,10 +51,10 @@ def parse():
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--metric", choices=["cosine", "euclidean"], default="cosine")
     p.add_argument("--M", type=int, default=16)
-    p.add_argument("--M0", type=int, default=32)
-    p.add_argument("--efc", type=int, default=128)
+    p.add_argument("--M0", type=int, default=48)
+    p.add_argument("--efc", type=int, default=200)
     p.add_argument("--seed", type=int, default=1234)
-    p.add_argument("--intrinsic", type=int, default=16)
+    p.add_argument("--intrinsic", type=int, default=12)
     p.add_argument("--clusters", type=int, default=1000)
     p.add_argument("--gt-queries", type=int, default=4096, help="queries scored against exact top-k")
     p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline time box (0 disables)")
@@ -165,7 +165,7 @@ def main():
     base_off = rank * a.n if shard else 0
     X = gen_vectors(a.n, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=base_off)
     g = H.Graph(M=a.M, Ml=0.25, EfSearch=a.ef, Distance=metric, Rng=a.seed + (rank if shard else 0),
-                build_mode=H.BUILD_BATCH, m0=a.M0, ef_construction=a.efc)
+                build_mode=H.BUILD_BATCH, m0=a.M0, ef_construction=a.efc, heuristic=2)
     g.reserve(a.n, a.dim)
     keys = np.arange(base_off, base_off + a.n, dtype=np.int64)
     torch.cuda.synchronize()

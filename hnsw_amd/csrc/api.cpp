@@ -393,7 +393,7 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         a.vis_log2 = h->vis_log2;
         HIPCHK(h, hipMemsetAsync(h->touched_cnt, 0, 4, h->stream));
         LCHK(h, launch_build_batch_search(a, h->lpr, h->vpl, h->stream));
-        if (maxlvl >= l) LCHK(h, launch_build_batch_commit(a, (a1 - a0) * mcap, h->stream));
+        if (maxlvl >= l) LCHK(h, launch_build_batch_commit(a, h->lpr, h->vpl, (a1 - a0) * mcap, h->stream));
     }
     return 0;
 }
@@ -772,7 +772,8 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "ef_construction") {
         h->efc = (int)v;
     } else if (n == "heuristic") {
-        h->heuristic = (int)(v != 0);
+        if (v < 0 || v > 2) return fail(h, MHNSW_EINVAL, "heuristic must be 0, 1 or 2");
+        h->heuristic = (int)v;
     } else if (n == "batch_min") {
         h->batch_min = (int)std::max<int64_t>(1, v);
     } else if (n == "batch_max") {
@@ -833,6 +834,7 @@ int mhnsw_add(mhnsw_index* h, const int64_t* keys, const float* vecs, int64_t n,
 int mhnsw_add_device(mhnsw_index* h, const int64_t* keys, const float* d_vecs, int64_t n, int dim,
                      const int32_t* levels) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
+    HIPCHK(h, hipDeviceSynchronize());  // order after whatever produced d_vecs
     return add_impl(h, keys, d_vecs, true, n, dim, levels);
 }
 
@@ -846,8 +848,9 @@ int mhnsw_search(mhnsw_index* h, const float* queries, int64_t B, int dim, int k
 int mhnsw_search_device(mhnsw_index* h, const float* d_queries, int64_t B, int dim, int k, int mode, int ef,
                         int64_t* d_keys, float* d_dist, int32_t* d_n, void* stream) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
-    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
-    return search_impl(h, d_queries, true, B, dim, k, mode, ef, nullptr, d_keys, d_dist, d_n, s, true);
+    // NULL is the HIP null stream (torch's default stream handle is 0)
+    return search_impl(h, d_queries, true, B, dim, k, mode, ef, nullptr, d_keys, d_dist, d_n, (hipStream_t)stream,
+                       true);
 }
 
 int64_t mhnsw_len(const mhnsw_index* h) { return h->layers.empty() ? 0 : h->layers[0].count; }

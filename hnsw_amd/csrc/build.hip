@@ -326,16 +326,26 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
     }
 }
 
-// one wave per touched node: keep the best cap of (existing U proposals) by (dist, id)
+// One wave per touched node v: merge v's row with the proposals it received.
+// (existing U proposals) is ranked by (dist to v, id); when it fits the row it
+// is written in rank order, otherwise the best `cap` are kept -- or, with
+// heuristic >= 2, HNSW's diversity rule (Alg. 4) is applied on overflow: a
+// candidate is dropped when it is closer to an already kept neighbour than to v.
+template <class C, int G>
 __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
     __shared__ float sd[128];
     __shared__ uint32_t si[128];
+    __shared__ float rd[128];
+    __shared__ uint32_t ri[128];
     const int lane = lane_id();
     const int n_t = *a.touched_cnt;
     if ((int)blockIdx.x >= n_t) return;
     const uint32_t v = a.touched[blockIdx.x];
     const int l = a.layer;
     const int capl = a.g.layers[l].cap;
+    const int keep_cap = min(capl, a.mcap);
+    int32_t* row = a.g.layers[l].adj + (size_t)v * capl;
+    float* rowd = a.g.layers[l].adjd + (size_t)v * capl;
     int d = a.g.layers[l].deg[v];
     if (d < 0) d = 0;
     int nin = a.inc_cnt[v];
@@ -345,8 +355,8 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
         float dd = __int_as_float(0x7f800000);
         uint32_t ii = EMPTY_ID;
         if (e < d) {
-            ii = (uint32_t)a.g.layers[l].adj[(size_t)v * capl + e];
-            dd = a.g.layers[l].adjd[(size_t)v * capl + e];
+            ii = (uint32_t)row[e];
+            dd = rowd[e];
         } else if (e < tot) {
             ii = a.inc_src[(size_t)v * a.inc_cap + (e - d)];
             dd = a.inc_dist[(size_t)v * a.inc_cap + (e - d)];
@@ -355,28 +365,59 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
         si[e] = ii;
     }
     __syncthreads();
-    int rank[2] = {0, 0};
-    float md[2];
-    uint32_t mi[2];
-    for (int h = 0; h < 2; ++h) {
-        md[h] = sd[lane + 64 * h];
-        mi[h] = si[lane + 64 * h];
-    }
-    for (int e = 0; e < tot; ++e) {
-        const float od = sd[e];
-        const uint32_t oi = si[e];
-        for (int h = 0; h < 2; ++h) rank[h] += lt_di(od, oi, md[h], mi[h]) ? 1 : 0;
-    }
-    const int keep = tot < capl ? tot : capl;
+    // rank = number of entries ordered before this one by (dist, id)
     for (int h = 0; h < 2; ++h) {
         const int e = lane + 64 * h;
-        if (e < tot && rank[h] < keep) {
-            a.g.layers[l].adj[(size_t)v * capl + rank[h]] = (int32_t)mi[h];
-            a.g.layers[l].adjd[(size_t)v * capl + rank[h]] = md[h];
+        const float md = sd[e];
+        const uint32_t mi = si[e];
+        int rank = 0;
+        for (int f = 0; f < tot; ++f) rank += lt_di(sd[f], si[f], md, mi) ? 1 : 0;
+        if (e < tot) {
+            rd[rank] = md;
+            ri[rank] = mi;
         }
     }
+    __syncthreads();
+    int nkeep = 0;
+    if (tot <= keep_cap || a.heuristic < 2) {
+        nkeep = min(tot, keep_cap);
+        for (int e = lane; e < nkeep; e += 64) {
+            row[e] = (int32_t)ri[e];
+            rowd[e] = rd[e];
+        }
+    } else {
+        uint32_t kept = 0;   // lane j holds the j-th kept id
+        float keptd = 0.f;
+        WaveStats st;
+        for (int i = 0; i < tot && nkeep < keep_cap; ++i) {
+            const uint32_t c = ri[i];
+            const float dcv = rd[i];
+            bool good = true;
+            if (nkeep > 0) {
+                QReg<C> qc;
+                load_query(qc, a.g.vecs + (size_t)guard_id(a.g, c) * a.g.pitch);
+                const float cn = a.g.norms[guard_id(a.g, c)];
+                st.E += nkeep;
+                eval_list<C, G>(a.g, qc, cn, kept, nkeep, a.g.metric, [&](float dcs, uint32_t) {
+                    if (dcs < dcv) good = false;
+                });
+            }
+            if (good) {
+                if (lane == nkeep) {
+                    kept = c;
+                    keptd = dcv;
+                }
+                ++nkeep;
+            }
+        }
+        if (lane < nkeep) {
+            row[lane] = (int32_t)kept;
+            rowd[lane] = keptd;
+        }
+        if (lane == 0) atomicAdd(&a.stats[0], st.E);
+    }
     if (lane == 0) {
-        a.g.layers[l].deg[v] = keep;
+        a.g.layers[l].deg[v] = nkeep;
         a.inc_cnt[v] = 0;
     }
 }
@@ -423,10 +464,17 @@ int launch_build_batch_search(const BatchBuildArgs& a, int lpr, int vpl, hipStre
     return -3;
 }
 
-int launch_build_batch_commit(const BatchBuildArgs& a, int64_t max_touched, hipStream_t s) {
+int launch_build_batch_commit(const BatchBuildArgs& a, int lpr, int vpl, int64_t max_touched, hipStream_t s) {
     if (max_touched <= 0) return 0;
-    hipLaunchKernelGGL(k_batch_commit, dim3((unsigned)max_touched), dim3(64), 0, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+#define X_(L, V, G)                                                                                   \
+    if (lpr == L && vpl == V) {                                                                       \
+        hipLaunchKernelGGL((k_batch_commit<Cfg<L, V>, (G < 4 ? G : 4)>), dim3((unsigned)max_touched), \
+                           dim3(64), 0, s, a);                                                        \
+        return hipGetLastError() == hipSuccess ? 0 : -1;                                              \
+    }
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return -3;
 }
 
 }  // namespace mh

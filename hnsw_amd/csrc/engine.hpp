@@ -71,7 +71,7 @@ struct BatchBuildArgs {
     uint32_t* cur_entry;          // [cap_nodes] per-node descent entry (in/out)
     int ef;                       // efConstruction
     int mcap;                     // neighbors to select on this layer
-    int heuristic;
+    int heuristic;                // 0 closest-M, 1 HNSW heuristic on the new row, 2 also on overflowing rows
     int32_t* inc_cnt;             // [cap_nodes] incoming request counters (zero between batches)
     uint32_t* inc_src;            // [cap_nodes * inc_cap]
     float* inc_dist;              // [cap_nodes * inc_cap]
@@ -82,7 +82,7 @@ struct BatchBuildArgs {
     int vis_log2;
 };
 int launch_build_batch_search(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s);
-int launch_build_batch_commit(const BatchBuildArgs& a, int64_t n_touched, hipStream_t s);
+int launch_build_batch_commit(const BatchBuildArgs& a, int lpr, int vpl, int64_t n_touched, hipStream_t s);
 
 // ---- exact / merge ----
 struct ExactArgs {

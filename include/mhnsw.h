@@ -13,7 +13,8 @@
  *    row-major, `dim` contiguous floats per row.
  *  - Host-pointer entry points copy their inputs before returning (the cgo
  *    rule forbids C from retaining Go pointers).  *_device entry points take
- *    device pointers and enqueue on the given HIP stream (NULL = library stream).
+ *    device pointers and enqueue asynchronously on the given HIP stream
+ *    (NULL = the HIP null stream, as in the HIP/CUDA runtime convention).
  *  - Return value: MHNSW_OK (0) or a negative error class; the message, with
  *    the reference's wording where one exists, is mhnsw_last_error(h).
  *  - Concurrency mirrors graph.go:328 (sync.RWMutex): searches may run
