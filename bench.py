@@ -34,6 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import hnsw_amd as H  # noqa: E402
+from hnsw_amd.shard import gather_topk, merge_topk, shard_range  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -58,6 +59,8 @@ def parse():
     p.add_argument("--clusters", type=int, default=1000)
     p.add_argument("--gt-queries", type=int, default=4096, help="queries scored against exact top-k")
     p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline time box (0 disables)")
+    p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
+    p.add_argument("--one-gpu", action="store_true", help="map every rank to cuda:0 (multi-rank rehearsal)")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_search.json"))
     return p.parse_args()
 
@@ -101,21 +104,10 @@ class Searcher:
         return self.keys, self.dist, self.n
 
 
-def shard_merge(keys, dists, n, world, k, device):
-    """all-gather per-shard top-k over RCCL, merge on the GPU."""
-    B = keys.shape[0]
-    ak = torch.empty(world, B, k, dtype=torch.int64, device=device)
-    ad = torch.empty(world, B, k, dtype=torch.float32, device=device)
-    an = torch.empty(world, B, dtype=torch.int32, device=device)
-    dist.all_gather_into_tensor(ak, keys.contiguous())
-    dist.all_gather_into_tensor(ad, dists.contiguous())
-    dist.all_gather_into_tensor(an, n.contiguous())
-    ok = torch.empty(B, k, dtype=torch.int64, device=device)
-    od = torch.empty(B, k, dtype=torch.float32, device=device)
-    on = torch.empty(B, dtype=torch.int32, device=device)
-    H.merge_topk_device(ak.data_ptr(), ad.data_ptr(), an.data_ptr(), world, B, k, ok.data_ptr(), od.data_ptr(),
-                        on.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    return ok, od, on
+def shard_merge(keys, dists, n, k):
+    """all-gather per-shard top-k over RCCL, merge on the GPU (hnsw_amd.shard)."""
+    ak, ad, an = gather_topk(keys, dists, n)
+    return merge_topk(ak, ad, an, k)
 
 
 def recall_at_k(res, n, truth, tn, k):
@@ -154,15 +146,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.one_gpu:
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(a.backend)
     metric = H.CosineDistance if a.metric == "cosine" else H.EuclideanDistance
 
     # ---- index --------------------------------------------------------------
     shard = a.mode == "shard"
-    base_off = rank * a.n if shard else 0
+    base_off = shard_range(a.n * world, world, rank)[0] if shard else 0
     X = gen_vectors(a.n, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=base_off)
     g = H.Graph(M=a.M, Ml=0.25, EfSearch=a.ef, Distance=metric, Rng=a.seed + (rank if shard else 0),
                 build_mode=H.BUILD_BATCH, m0=a.M0, ef_construction=a.efc, heuristic=2)
@@ -186,7 +183,7 @@ def main():
     def step():
         kk, dd, nn = S.run(Q, H.MODE_BEAM, a.ef)
         if shard and world > 1:
-            return shard_merge(kk, dd, nn, world, a.k, device)
+            return shard_merge(kk, dd, nn, a.k)
         return kk, dd, nn
 
     # ---- recall vs exact ----------------------------------------------------
@@ -195,7 +192,7 @@ def main():
     G = Searcher(g, ngt, a.k, a.dim, device)
     tk, td, tn = G.run(Q[:ngt], H.MODE_EXACT, 0)
     if shard and world > 1:
-        tk, td, tn = shard_merge(tk, td, tn, world, a.k, device)
+        tk, td, tn = shard_merge(tk, td, tn, a.k)
     torch.cuda.synchronize()
     recall = recall_at_k(res_k[:ngt], res_n[:ngt], tk, tn, a.k)
 

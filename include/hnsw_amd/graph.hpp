@@ -1,0 +1,230 @@
+// hnsw_amd/graph.hpp -- header-only C++17 mirror of the reference's Go API
+// (TFMV/hnsw graph.go:17-27, 305-366, 437-1110; distance.go:12-46) over the C
+// ABI in mhnsw.h.  Same names, argument meaning and error messages; Go's
+// `error` becomes hnsw::Error (empty == nil).  Keys are Go `int`-like
+// integral types (the C ABI carries int64).  Vectors are copied in (the
+// reference aliases caller slices, graph.go:447, 911 -- documented in DESIGN.md).
+#pragma once
+
+#include <cstdint>
+#include <initializer_list>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "../mhnsw.h"
+
+namespace hnsw {
+
+using Vector = std::vector<float>;
+
+// Go `error`: empty message == nil
+struct Error {
+    std::string msg;
+    int code = 0;
+    explicit operator bool() const { return code != 0; }
+    const std::string& Error_() const { return msg; }
+};
+
+inline Error make_error(int rc, const mhnsw_index* h) {
+    if (rc >= 0) return {};
+    const char* m = mhnsw_last_error(h);
+    return Error{m ? m : "error", rc};
+}
+
+template <class K>
+struct Node {  // graph.go:19-23
+    K Key;
+    Vector Value;
+    bool operator==(const Node& o) const { return Key == o.Key && Value == o.Value; }
+};
+
+template <class K>
+Node<K> MakeNode(K key, Vector vec) {  // graph.go:25-27
+    return Node<K>{key, std::move(vec)};
+}
+
+// distance.go:12 DistanceFunc -- the built-ins run on the GPU sweep kernel
+struct DistanceFunc {
+    int metric;
+    const char* name;
+    float operator()(const Vector& a, const Vector& b) const {
+        if (a.size() != b.size()) throw std::invalid_argument("vector length mismatch");
+        float out = 0.f;
+        int rc = mhnsw_distance(metric, a.data(), b.data(), 1, (int)a.size(), &out);
+        if (rc < 0) throw std::runtime_error(mhnsw_last_error(nullptr));
+        return out;
+    }
+};
+inline const DistanceFunc CosineDistance{MHNSW_COSINE, "cosine"};        // distance.go:15-17
+inline const DistanceFunc EuclideanDistance{MHNSW_EUCLIDEAN, "euclidean"};  // distance.go:20-23
+
+template <class K>
+class Graph {  // graph.go:305-332
+    static_assert(std::is_integral<K>::value, "hnsw_amd keys are integral (Go int); see INTEGRATION.md");
+
+   public:
+    const DistanceFunc* Distance = &CosineDistance;
+    uint64_t Rng = 0;
+    int M = 16;
+    double Ml = 0.25;
+    int EfSearch = 20;
+
+    Graph() { create(); }
+    Graph(int m, double ml, int ef, const DistanceFunc* dist, uint64_t seed)
+        : Distance(dist), Rng(seed), M(m), Ml(ml), EfSearch(ef) {
+        create();
+    }
+    Graph(const Graph&) = delete;
+    Graph& operator=(const Graph&) = delete;
+    ~Graph() {
+        if (h_) mhnsw_destroy(h_);
+    }
+
+    mhnsw_index* handle() { return h_; }
+    Error SetOption(const char* name, int64_t v) { return make_error(mhnsw_set_option(h_, name, v), h_); }
+
+    // graph.go:916-937
+    Error Validate() {
+        sync();
+        return make_error(mhnsw_validate(h_), h_);
+    }
+
+    // graph.go:437-531
+    Error Add(std::initializer_list<Node<K>> nodes) { return BatchAdd(std::vector<Node<K>>(nodes)); }
+    Error Add(const Node<K>& n) { return BatchAdd(std::vector<Node<K>>{n}); }
+
+    // graph.go:942-1042 (levels: optional injection for parity tests)
+    Error BatchAdd(const std::vector<Node<K>>& nodes, const std::vector<int32_t>* levels = nullptr) {
+        sync();
+        if (nodes.empty()) return make_error(mhnsw_validate(h_), h_);
+        const size_t d = nodes[0].Value.size();
+        std::vector<int64_t> keys;
+        std::vector<float> flat;
+        keys.reserve(nodes.size());
+        flat.reserve(nodes.size() * d);
+        for (const auto& n : nodes) {
+            if (n.Value.size() != d) {
+                const int have = Dims() ? Dims() : (int)d;
+                return Error{"embedding dimension mismatch: " + std::to_string(have) + " != " +
+                                 std::to_string(n.Value.size()),
+                             MHNSW_EDIM};
+            }
+            keys.push_back((int64_t)n.Key);
+            flat.insert(flat.end(), n.Value.begin(), n.Value.end());
+        }
+        int rc = mhnsw_add(h_, keys.data(), flat.data(), (int64_t)nodes.size(), (int)d,
+                           levels ? levels->data() : nullptr);
+        if (rc < 0) return make_error(rc, h_);
+        for (const auto& n : nodes) values_[(int64_t)n.Key] = n.Value;
+        return {};
+    }
+
+    // graph.go:534-625 (mode: MHNSW_MODE_COMPAT = the reference's semantics)
+    std::pair<std::vector<Node<K>>, Error> Search(const Vector& near, int k, int mode = MHNSW_MODE_COMPAT) {
+        auto r = BatchSearch(std::vector<Vector>{near}, k, mode, /*single=*/true);
+        if (r.second) return {{}, r.second};
+        return {r.first.empty() ? std::vector<Node<K>>{} : r.first[0], {}};
+    }
+
+    // graph.go:1047-1110
+    std::pair<std::vector<std::vector<Node<K>>>, Error> BatchSearch(const std::vector<Vector>& queries, int k,
+                                                                    int mode = MHNSW_MODE_COMPAT,
+                                                                    bool single = false) {
+        sync();
+        if (queries.empty()) return {{}, make_error(mhnsw_validate(h_), h_)};
+        const size_t d = queries[0].size();
+        const int have = Dims();
+        for (size_t i = 0; i < queries.size() && have; ++i)
+            if ((int)queries[i].size() != have) {
+                if (single)
+                    return {{}, Error{"embedding dimension mismatch: " + std::to_string(have) + " != " +
+                                          std::to_string(queries[i].size()),
+                                      MHNSW_EDIM}};
+                return {{}, Error{"embedding dimension mismatch for query " + std::to_string(i) + ": " +
+                                      std::to_string(have) + " != " + std::to_string(queries[i].size()),
+                                  MHNSW_EDIM}};
+            }
+        std::vector<float> flat;
+        for (const auto& q : queries) flat.insert(flat.end(), q.begin(), q.end());
+        const size_t B = queries.size(), kk = k > 0 ? (size_t)k : 1;
+        std::vector<int64_t> keys(B * kk);
+        std::vector<float> dist(B * kk);
+        std::vector<int32_t> n(B);
+        int rc = mhnsw_search(h_, flat.data(), (int64_t)B, (int)d, k, mode, 0, nullptr, keys.data(), dist.data(),
+                              n.data());
+        if (rc < 0) return {{}, make_error(rc, h_)};
+        std::vector<std::vector<Node<K>>> out(B);
+        for (size_t b = 0; b < B; ++b)
+            for (int j = 0; j < n[b]; ++j) {
+                const int64_t key = keys[b * kk + j];
+                out[b].push_back(Node<K>{(K)key, lookup_value(key)});
+            }
+        return {out, {}};
+    }
+
+    int Len() const { return (int)mhnsw_len(h_); }   // graph.go:829
+    int Dims() const { return mhnsw_dims(h_); }      // graph.go:421
+
+    std::pair<Vector, bool> Lookup(K key) {  // graph.go:898
+        auto it = values_.find((int64_t)key);
+        if (it != values_.end()) return {it->second, true};
+        Vector v(Dims() > 0 ? Dims() : 1);
+        int found = mhnsw_lookup(h_, (int64_t)key, v.data());
+        if (found <= 0) return {{}, false};
+        return {v, true};
+    }
+
+    std::vector<int> Topography() const {  // analyzer.go:41-49
+        std::vector<int> t;
+        for (int l = 0; l < mhnsw_num_layers(h_); ++l) t.push_back((int)mhnsw_layer_count(h_, l));
+        return t;
+    }
+
+   private:
+    void create() {
+        int rc = mhnsw_create(MHNSW_COSINE, 16, 0.25, 20, Rng, &h_);
+        if (rc < 0) throw std::runtime_error(mhnsw_last_error(nullptr));
+    }
+    void sync() {
+        mhnsw_set_params(h_, Distance ? Distance->metric : MHNSW_NO_DISTANCE, M, Ml, EfSearch);
+        if (Rng != seeded_) {
+            mhnsw_seed(h_, Rng);
+            seeded_ = Rng;
+        }
+    }
+    Vector lookup_value(int64_t key) {
+        auto it = values_.find(key);
+        if (it != values_.end()) return it->second;
+        Vector v(Dims() > 0 ? Dims() : 1);
+        mhnsw_lookup(h_, key, v.data());
+        return v;
+    }
+
+    mhnsw_index* h_ = nullptr;
+    uint64_t seeded_ = 0;
+    std::map<int64_t, Vector> values_;
+};
+
+// graph.go:340-348
+template <class K>
+std::unique_ptr<Graph<K>> NewGraph(uint64_t seed = 0) {
+    return std::make_unique<Graph<K>>(16, 0.25, 20, &CosineDistance, seed);
+}
+
+// graph.go:352-366: validates before touching the device
+template <class K>
+std::pair<std::unique_ptr<Graph<K>>, Error> NewGraphWithConfig(int m, double ml, int efSearch,
+                                                               const DistanceFunc* distance, uint64_t seed = 0) {
+    mhnsw_index* probe = nullptr;
+    int rc = mhnsw_create(distance ? distance->metric : MHNSW_NO_DISTANCE, m, ml, efSearch, seed, &probe);
+    if (rc < 0) return {nullptr, Error{mhnsw_last_error(nullptr), rc}};
+    mhnsw_destroy(probe);
+    return {std::make_unique<Graph<K>>(m, ml, efSearch, distance, seed), {}};
+}
+
+}  // namespace hnsw

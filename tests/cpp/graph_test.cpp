@@ -1,0 +1,122 @@
+// C++ mirror of the reference's own tests (graph_test.go, distance_test.go),
+// written against the C++ host shim include/hnsw_amd/graph.hpp -> C ABI ->
+// HIP kernels.  Run by tests/test_cpp_shim.py (GPU).  Exit code = failures.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <set>
+
+#include "hnsw_amd/graph.hpp"
+
+static int failures = 0;
+#define REQUIRE(cond, name)                                              \
+    do {                                                                 \
+        if (!(cond)) {                                                   \
+            std::printf("FAIL %s: %s (line %d)\n", name, #cond, __LINE__); \
+            ++failures;                                                  \
+        }                                                                \
+    } while (0)
+
+static uint32_t bits(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+}
+
+// distance_test.go:9-31
+static void TestDistances() {
+    REQUIRE(bits(hnsw::EuclideanDistance({1, 2, 3}, {4, 5, 6})) == 0x40a646e1u, "TestEuclideanDistance");
+    REQUIRE(std::fabs(hnsw::CosineDistance({1, 1, 1}, {0.8f, 0.8f, 0.8f})) <= 1e-6, "TestCosineSimilarity");
+    REQUIRE(std::fabs(hnsw::CosineDistance({1, 0}, {0, 1}) - 1.0f) <= 1e-6, "TestCosineSimilarity");
+    REQUIRE(std::fabs(hnsw::CosineDistance({1, 0}, {1, 0})) <= 1e-6, "TestCosineSimilarity");
+}
+
+// graph_test.go:27-74 (hand-built layer; node under map key 4 has Key 5, Value {4})
+static void Test_layerNode_search() {
+    hnsw::Graph<int> g(6, 0.5, 4, &hnsw::EuclideanDistance, 0);
+    const int64_t keys[6] = {0, 1, 2, 3, 5, 5};
+    const float vals[6] = {0, 1, 2, 3, 4, 5};
+    const int32_t deg[6] = {3, -1, -1, 2, -1, -1};
+    int32_t adj[6 * 7];
+    for (int& a : adj) a = -1;
+    adj[0] = 1, adj[1] = 2, adj[2] = 3, adj[3 * 7 + 0] = 4, adj[3 * 7 + 1] = 5;
+    const int32_t entry[1] = {0};
+    REQUIRE(mhnsw_import(g.handle(), 6, 1, 1, 7, keys, vals, deg, adj, entry) == 0, "Test_layerNode_search import");
+    auto r = g.Search({4}, 2);
+    REQUIRE(!r.second, "Test_layerNode_search err");
+    REQUIRE(r.first.size() == 2 && r.first[0].Key == 5 && r.first[1].Key == 3, "Test_layerNode_search keys");
+}
+
+// graph_test.go:86-133 (level stream: SplitMix64 seed 0 -- Go's seed-0 stream is not
+// reproducible offline, so the golden [64,65,62,63] is checked as a property)
+static void TestGraph_AddSearch() {
+    hnsw::Graph<int> g(6, 0.5, 20, &hnsw::EuclideanDistance, 0);
+    for (int i = 0; i < 128; ++i) REQUIRE(!g.Add(hnsw::MakeNode(i, {(float)i})), "TestGraph_AddSearch add");
+    auto topo = g.Topography();
+    REQUIRE(!topo.empty() && topo[0] == 128, "TestGraph_AddSearch topography[0]");
+    for (size_t i = 1; i < topo.size(); ++i) REQUIRE(topo[i] <= topo[i - 1], "TestGraph_AddSearch topography");
+    auto r = g.Search({64.5f}, 4);
+    REQUIRE(!r.second && r.first.size() == 4, "TestGraph_AddSearch len");
+    std::set<int> got;
+    for (auto& n : r.first) {
+        got.insert(n.Key);
+        REQUIRE(n.Value.size() == 1 && n.Value[0] == (float)n.Key, "TestGraph_AddSearch value");
+    }
+    REQUIRE(got.count(64) && got.count(65), "TestGraph_AddSearch nearest");
+    for (int k : got) REQUIRE(k >= 60 && k <= 68, "TestGraph_AddSearch range");
+}
+
+// graph_test.go:253-275
+static void TestGraph_DefaultCosine() {
+    auto g = hnsw::NewGraph<int>(7);
+    REQUIRE(!g->Add({hnsw::MakeNode(1, {1, 1}), hnsw::MakeNode(2, {0, 1}), hnsw::MakeNode(3, {1, -1})}),
+            "TestGraph_DefaultCosine add");
+    auto r = g->Search({0.5f, 0.5f}, 1);
+    REQUIRE(!r.second && r.first.size() == 1, "TestGraph_DefaultCosine len");
+    REQUIRE(r.first.size() == 1 && (r.first[0] == hnsw::Node<int>{1, {1, 1}}), "TestGraph_DefaultCosine node");
+}
+
+// graph_test.go:415-459
+static void TestGraphValidation() {
+    auto ok = hnsw::NewGraphWithConfig<int>(16, 0.25, 20, &hnsw::CosineDistance);
+    REQUIRE(!ok.second && ok.first, "ValidConfig");
+    auto e1 = hnsw::NewGraphWithConfig<int>(0, 0.25, 20, &hnsw::CosineDistance);
+    REQUIRE(e1.second && e1.second.msg.find("M must be greater than 0") != std::string::npos, "InvalidM");
+    auto e2 = hnsw::NewGraphWithConfig<int>(16, 0, 20, &hnsw::CosineDistance);
+    REQUIRE(e2.second && e2.second.msg.find("Ml must be between 0 and 1") != std::string::npos, "InvalidMl");
+    auto e3 = hnsw::NewGraphWithConfig<int>(16, 1.5, 20, &hnsw::CosineDistance);
+    REQUIRE(e3.second && e3.second.msg.find("Ml must be between 0 and 1") != std::string::npos, "InvalidMl");
+    auto e4 = hnsw::NewGraphWithConfig<int>(16, 0.25, 0, &hnsw::CosineDistance);
+    REQUIRE(e4.second && e4.second.msg.find("EfSearch must be greater than 0") != std::string::npos,
+            "InvalidEfSearch");
+    auto e5 = hnsw::NewGraphWithConfig<int>(16, 0.25, 20, nullptr);
+    REQUIRE(e5.second && e5.second.msg.find("Distance function must be set") != std::string::npos,
+            "NilDistance");
+    auto g = hnsw::NewGraph<int>();
+    auto r = g->Search({1, 2, 3}, 0);
+    REQUIRE(r.second && r.second.msg.find("k must be greater than 0") != std::string::npos, "InvalidK");
+}
+
+static void TestDimensionMismatch() {
+    auto g = hnsw::NewGraph<int>(3);
+    REQUIRE(!g->Add(hnsw::MakeNode(1, {1, 2, 3})), "dim add");
+    auto e = g->Add(hnsw::MakeNode(2, {1, 2}));
+    REQUIRE(e && e.msg == "embedding dimension mismatch: 3 != 2", "dim add mismatch");
+    auto r = g->Search({1, 2}, 1);
+    REQUIRE(r.second && r.second.msg == "embedding dimension mismatch: 3 != 2", "dim search mismatch");
+    auto v = g->Lookup(1);
+    REQUIRE(v.second && v.first == hnsw::Vector({1, 2, 3}), "Lookup");
+    REQUIRE(!g->Lookup(42).second, "Lookup missing");
+    REQUIRE(g->Len() == 1 && g->Dims() == 3, "Len/Dims");
+}
+
+int main() {
+    TestDistances();
+    Test_layerNode_search();
+    TestGraph_AddSearch();
+    TestGraph_DefaultCosine();
+    TestGraphValidation();
+    TestDimensionMismatch();
+    std::printf("%s (%d failures)\n", failures ? "FAIL" : "PASS", failures);
+    return failures;
+}

@@ -292,8 +292,11 @@ def test_batch_build_recall_and_exact_parity(H, O, metric):
     n, d = 20000, 64
     X = _clustered(rng, n, d)
     Q = _clustered(rng, 200, d)
+    if metric == 0:  # embeddings compared by cosine are L2-normalised
+        X /= np.linalg.norm(X, axis=1, keepdims=True)
+        Q /= np.linalg.norm(Q, axis=1, keepdims=True)
     g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=_metric_fn(H, metric), Rng=9, build_mode=H.BUILD_BATCH,
-                ef_construction=100)
+                ef_construction=100, heuristic=2)
     g.add_arrays(np.arange(n), X)
     st = g.stats()
     assert st["dropped_proposals"] == 0
