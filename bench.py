@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--mode", choices=["replica", "shard"], default="replica")
-    p.add_argument("--n", type=int, default=1_000_000, help="vectors per index (per shard in shard mode)")
+    p.add_argument("--nbase", type=int, default=1_000_000, help="vectors per index (per shard in shard mode)")
     p.add_argument("--dim", type=int, default=768)
     p.add_argument("--batch", type=int, default=16384, help="queries per step per GPU")
     p.add_argument("--ef", type=int, default=64)
@@ -159,15 +159,15 @@ def main():
 
     # ---- index --------------------------------------------------------------
     shard = a.mode == "shard"
-    base_off = shard_range(a.n * world, world, rank)[0] if shard else 0
-    X = gen_vectors(a.n, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=base_off)
+    base_off = shard_range(a.nbase * world, world, rank)[0] if shard else 0
+    X = gen_vectors(a.nbase, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=base_off)
     g = H.Graph(M=a.M, Ml=0.25, EfSearch=a.ef, Distance=metric, Rng=a.seed + (rank if shard else 0),
                 build_mode=H.BUILD_BATCH, m0=a.M0, ef_construction=a.efc, heuristic=2)
-    g.reserve(a.n, a.dim)
-    keys = np.arange(base_off, base_off + a.n, dtype=np.int64)
+    g.reserve(a.nbase, a.dim)
+    keys = np.arange(base_off, base_off + a.nbase, dtype=np.int64)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    g.add_device(keys, X.data_ptr(), a.n, a.dim)
+    g.add_device(keys, X.data_ptr(), a.nbase, a.dim)
     torch.cuda.synchronize()
     build_s = time.perf_counter() - t0
     bstats = g.stats()
@@ -235,7 +235,7 @@ def main():
     if os.path.exists(a.pmc_json):
         try:
             pm = json.load(open(a.pmc_json))
-            if pm.get("n") == a.n and pm.get("dim") == a.dim and pm.get("batch") == a.batch and pm.get("ef") == a.ef:
+            if pm.get("n") == a.nbase and pm.get("dim") == a.dim and pm.get("batch") == a.batch and pm.get("ef") == a.ef:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -256,9 +256,9 @@ def main():
                  f"random linear map + N(0,0.05^2) noise, L2-normalised; seed {a.seed}; queries from the same "
                  f"distribution (seed {qseed})"),
         "config": {
-            "workload": f"{a.n // 1000}k x {a.dim}-d {a.metric}, batched beam search ef={a.ef} k={a.k}, "
+            "workload": f"{a.nbase // 1000}k x {a.dim}-d {a.metric}, batched beam search ef={a.ef} k={a.k}, "
                         f"{a.batch} queries/step/GPU (BASELINE configs[1])",
-            "n_base": a.n * (world if shard else 1), "dim": a.dim, "batch_per_gpu": a.batch, "ef": a.ef,
+            "n_base": a.nbase * (world if shard else 1), "dim": a.dim, "batch_per_gpu": a.batch, "ef": a.ef,
             "k": a.k, "M": a.M, "M0": a.M0, "ef_construction": a.efc,
             "parallelism": f"{'shard' if shard else 'replica'}{world}",
         },
@@ -270,8 +270,8 @@ def main():
             "alg_bytes_per_launch": int(alg_bytes),
             "dist_evals_per_query": round(E / a.batch, 1), "expansions_per_query": round(Xp / a.batch, 1),
         },
-        "build": {"inserts_per_s": round(a.n / build_s, 1), "seconds": round(build_s, 2),
-                  "dist_evals_per_insert": round(bstats["build_dist_evals"] / a.n, 1),
+        "build": {"inserts_per_s": round(a.nbase / build_s, 1), "seconds": round(build_s, 2),
+                  "dist_evals_per_insert": round(bstats["build_dist_evals"] / a.nbase, 1),
                   "dropped_proposals": bstats["dropped_proposals"]},
         "cpu_baseline": None,
     }

@@ -56,6 +56,7 @@ struct mhnsw_index {
     int m0 = 0;  // 0 => 2*M in batch mode, M in compat mode
     int efc = 0; // 0 => EfSearch
     int heuristic = 1;
+    int keep_pruned = 0;
     int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
     int vis_log2 = 12;
     int exact_kk = 0;
@@ -383,6 +384,7 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         a.ef = std::max(efc, mcap);
         a.mcap = mcap;
         a.heuristic = h->heuristic;
+        a.keep_pruned = h->keep_pruned;
         a.inc_cnt = h->inc_cnt;
         a.inc_src = h->inc_src;
         a.inc_dist = h->inc_dist;
@@ -629,7 +631,7 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         a.err = h->d_err;
         a.vis_log2 = h->vis_log2;
         if (mode == MHNSW_MODE_BEAM) {
-            if (std::max(ef, k) > 256) return fail(h, MHNSW_EUNSUPPORTED, "beam mode supports max(ef,k) <= 256");
+            if (std::max(ef, k) > 512) return fail(h, MHNSW_EUNSUPPORTED, "beam mode supports max(ef,k) <= 512");
             if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
             LCHK(h, launch_search_beam(a, h->lpr, h->vpl, s));
             if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));
@@ -774,6 +776,8 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "heuristic") {
         if (v < 0 || v > 2) return fail(h, MHNSW_EINVAL, "heuristic must be 0, 1 or 2");
         h->heuristic = (int)v;
+    } else if (n == "keep_pruned") {
+        h->keep_pruned = (int)(v != 0);
     } else if (n == "batch_min") {
         h->batch_min = (int)std::max<int64_t>(1, v);
     } else if (n == "batch_max") {
@@ -797,6 +801,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "m0") *v = m0_of(h);
     else if (n == "ef_construction") *v = h->efc > 0 ? h->efc : h->ef;
     else if (n == "heuristic") *v = h->heuristic;
+    else if (n == "keep_pruned") *v = h->keep_pruned;
     else if (n == "batch_min") *v = h->batch_min;
     else if (n == "batch_max") *v = h->batch_max;
     else if (n == "batch_ratio_pct") *v = h->batch_ratio_pct;

@@ -302,6 +302,21 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
                 ++nsel;
             }
         }
+        if (a.keep_pruned && nsel < a.mcap) {  // Malkov Alg. 4 keepPrunedConnections
+            for (int i = 0; i < nl && nsel < a.mcap; ++i) {
+                float dc;
+                uint32_t c;
+                bl_at(L, i, dc, c);
+                if (c == EMPTY_ID) break;
+                c &= ID_MASK;
+                if (__ballot(lane < nsel && sel == c)) continue;
+                if (lane == nsel) {
+                    sel = c;
+                    seld = dc;
+                }
+                ++nsel;
+            }
+        }
         const int capl = a.g.layers[l].cap;
         if (lane < nsel) {
             a.g.layers[l].adj[(size_t)u * capl + lane] = (int32_t)sel;
@@ -457,6 +472,7 @@ int launch_build_batch_search(const BatchBuildArgs& a, int lpr, int vpl, hipStre
         if (a.ef <= 64) return launch_batch_search_t<Cfg<L, V>, 1, G>(a, s); \
         if (a.ef <= 128) return launch_batch_search_t<Cfg<L, V>, 2, G>(a, s); \
         if (a.ef <= 256) return launch_batch_search_t<Cfg<L, V>, 4, G>(a, s); \
+        if (a.ef <= 512) return launch_batch_search_t<Cfg<L, V>, 8, G>(a, s); \
         return -4;                                                           \
     }
     MH_FOR_EACH_CFG(X_)

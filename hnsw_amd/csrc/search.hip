@@ -312,6 +312,7 @@ int launch_search_beam(const SearchArgs& a, int lpr, int vpl, hipStream_t s) {
         if (efl <= 64) return launch_beam_t<Cfg<L, V>, 1, G>(a, s);              \
         if (efl <= 128) return launch_beam_t<Cfg<L, V>, 2, G>(a, s);             \
         if (efl <= 256) return launch_beam_t<Cfg<L, V>, 4, G>(a, s);             \
+        if (efl <= 512) return launch_beam_t<Cfg<L, V>, 8, G>(a, s);             \
         return -4;                                                               \
     }
     MH_FOR_EACH_CFG(X_)

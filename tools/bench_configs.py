@@ -1,0 +1,103 @@
+"""Secondary BASELINE configs (not the headline line; results go to profiles/):
+  config 3: 1M x 768 Euclidean build throughput (batched insert; compat insert
+            throughput on a bounded prefix), plus the resulting recall@10.
+  config 5: 1M x 1536 cosine, batch 1024, exact MFMA path: queries/s and
+            k_scores TFLOP/s.
+  compat  : the reference's Search() semantics on the GPU vs the oracle on the
+            host, same graph.
+Usage: python tools/bench_configs.py [3] [5] [compat]"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import hnsw_amd as H  # noqa: E402
+from bench import Searcher, gen_vectors, recall_at_k  # noqa: E402
+
+dev = torch.device("cuda")
+which = sys.argv[1:] or ["3", "5", "compat"]
+
+
+def timed(fn, reps=1):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps, r
+
+
+if "3" in which:
+    n = 1_000_000
+    X = gen_vectors(n, 768, 77, 12, 1000, dev, "euclidean")
+    Q = gen_vectors(4096, 768, 78, 12, 1000, dev, "euclidean")
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.EuclideanDistance, Rng=5, build_mode=H.BUILD_BATCH,
+                m0=48, ef_construction=200, heuristic=2)
+    g.reserve(n, 768)
+    bt, _ = timed(lambda: g.add_device(np.arange(n), X.data_ptr(), n, 768))
+    st = g.stats()
+    tk, td, tn = (x.clone() for x in Searcher(g, 4096, 10, 768, dev).run(Q, H.MODE_EXACT, 0))
+    k_, d_, n_ = Searcher(g, 4096, 10, 768, dev).run(Q, H.MODE_BEAM, 64)
+    rec = recall_at_k(k_, n_, tk, tn, 10)
+    g.close()
+    # compat (graph.go:437-531 semantics, strictly sequential) on a bounded prefix
+    nc = 20000
+    gc = H.Graph(M=16, Ml=0.25, EfSearch=20, Distance=H.EuclideanDistance, Rng=5)
+    gc.reserve(nc, 768)
+    ct, _ = timed(lambda: gc.add_device(np.arange(nc), X.data_ptr(), nc, 768))
+    gc.close()
+    print(json.dumps({"config": "configs[2] 1M x 768 Euclidean insert", "batched_inserts_per_s": round(n / bt, 1),
+                      "batched_seconds": round(bt, 2), "dist_evals_per_insert": round(st["build_dist_evals"] / n, 1),
+                      "recall_at_10_ef64": round(rec, 4), "M": 16, "M0": 48, "ef_construction": 200,
+                      "compat_inserts_per_s": round(nc / ct, 1), "compat_prefix": nc,
+                      "note": "compat = reference Add() semantics, one wave walks inserts in order"}), flush=True)
+    del X
+
+if "5" in which:
+    n, d, B = 1_000_000, 1536, 1024
+    X = gen_vectors(n, d, 55, 12, 1000, dev, "cosine")
+    Q = gen_vectors(B, d, 56, 12, 1000, dev, "cosine")
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_BATCH, m0=32,
+                ef_construction=64)
+    g.reserve(n, d)
+    g.add_device(np.arange(n), X.data_ptr(), n, d)
+    S = Searcher(g, B, 10, d, dev)
+    S.run(Q, H.MODE_EXACT, 0)
+    dt, _ = timed(lambda: S.run(Q, H.MODE_EXACT, 0), reps=5)
+    kms = g.last_kernel_ms()
+    flops = 2.0 * B * n * d
+    print(json.dumps({"config": "configs[4] 1M x 1536 cosine exact, batch 1024", "queries_per_s": round(B / dt, 1),
+                      "ms_per_batch": round(dt * 1e3, 3), "exact_path_ms_events": round(kms, 3),
+                      "gemm_tflops_end_to_end": round(flops / dt / 1e12, 1), "mfma_f32_peak_tflops": 157.3,
+                      "recall": 1.0}), flush=True)
+    g.close()
+    del X
+
+if "compat" in which:
+    import oracle as O  # CPU baseline only
+
+    n = 200_000
+    X = gen_vectors(n, 768, 1234, 12, 1000, dev, "cosine")
+    Q = gen_vectors(4096, 768, 9011, 12, 1000, dev, "cosine")
+    g = H.Graph(M=16, Ml=0.25, EfSearch=20, Distance=H.CosineDistance, Rng=3, build_mode=H.BUILD_BATCH, m0=16,
+                ef_construction=64)
+    g.add_device(np.arange(n), X.data_ptr(), n, 768)
+    S = Searcher(g, 4096, 10, 768, dev)
+    S.run(Q, H.MODE_COMPAT, 20)
+    dt, res = timed(lambda: S.run(Q, H.MODE_COMPAT, 20), reps=3)
+    gk = res[0].cpu().numpy()
+    o = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=16, M0=16, Ml=0.25, EfSearch=20)
+    o.import_graph(**g.export())
+    qn = Q.cpu().numpy()
+    t0 = time.perf_counter()
+    ok, od, on = o.search(qn[:512], 10, mode=O.MODE_COMPAT, ef=20)
+    ct = time.perf_counter() - t0
+    same = bool(np.array_equal(ok, gk[:512]))
+    print(json.dumps({"config": "compat Search() semantics, 200k x 768 cosine, M=16 ef=20 k=10",
+                      "gpu_queries_per_s": round(4096 / dt, 1), "cpu_oracle_queries_per_s_1thread": round(512 / ct, 1),
+                      "identical_results_first_512": same}), flush=True)

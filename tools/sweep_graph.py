@@ -1,0 +1,48 @@
+"""GPU sweep: graph build settings -> recall@10 and batched-search QPS on the
+bench workload (1M x 768 cosine).  python tools/sweep_graph.py [n]"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import hnsw_amd as H  # noqa: E402
+from bench import Searcher, gen_vectors, recall_at_k  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+dev = torch.device("cuda")
+X = gen_vectors(n, 768, 1234, 12, 1000, dev, "cosine")
+Q = gen_vectors(16384, 768, 1234 + 7777, 12, 1000, dev, "cosine")
+configs = [
+    dict(M=16, m0=48, ef_construction=400, heuristic=2),
+    dict(M=16, m0=63, ef_construction=400, heuristic=2),
+    dict(M=16, m0=32, ef_construction=400, heuristic=2),
+    dict(M=16, m0=48, ef_construction=400, heuristic=2, keep_pruned=1),
+    dict(M=24, m0=48, ef_construction=200, heuristic=2),
+]
+for cfg in configs:
+    cfg = dict(cfg)
+    M = cfg.pop("M")
+    g = H.Graph(M=M, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=1234, build_mode=H.BUILD_BATCH, **cfg)
+    g.reserve(n, 768)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    g.add_device(np.arange(n), X.data_ptr(), n, 768)
+    torch.cuda.synchronize()
+    bt = time.time() - t0
+    G = Searcher(g, 4096, 10, 768, dev)
+    tk, td, tn = (x.clone() for x in G.run(Q[:4096], H.MODE_EXACT, 0))
+    S = Searcher(g, 16384, 10, 768, dev)
+    for ef in (48, 64, 96):
+        S.run(Q, H.MODE_BEAM, ef)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        for _ in range(5):
+            k_, d_, n_ = S.run(Q, H.MODE_BEAM, ef)
+        torch.cuda.synchronize()
+        dt = (time.time() - t0) / 5
+        r = recall_at_k(k_[:4096], n_[:4096], tk, tn, 10)
+        print(f"M={M} {cfg} build={bt:.1f}s ef={ef} recall@10={r:.4f} qps={16384 / dt / 1e6:.3f}M", flush=True)
+    g.close()
