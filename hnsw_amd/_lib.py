@@ -21,6 +21,7 @@ OK, EINVAL, EDIM, EK, ENOMEM, EDEVICE, EUNSUPPORTED, EINTERNAL = 0, -1, -2, -3, 
 #: every symbol include/mhnsw.h declares: name -> (restype, argtypes)
 _P = C.POINTER
 _f32p, _i32p, _i64p, _vp = _P(C.c_float), _P(C.c_int32), _P(C.c_int64), C.c_void_p
+_u8p = _P(C.c_uint8)
 SIGNATURES = {
     "mhnsw_create": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_int, C.c_uint64, _P(_vp)]),
     "mhnsw_destroy": (None, [_vp]),
@@ -43,11 +44,14 @@ SIGNATURES = {
     "mhnsw_lookup": (C.c_int, [_vp, C.c_int64, _f32p]),
     "mhnsw_num_layers": (C.c_int, [_vp]),
     "mhnsw_layer_count": (C.c_int64, [_vp, C.c_int]),
+    "mhnsw_connectivity": (C.c_int, [_vp, _P(C.c_double), C.c_int]),
+    "mhnsw_delete": (C.c_int, [_vp, _i64p, C.c_int64, _u8p]),
     "mhnsw_distance": (C.c_int, [C.c_int, _f32p, _f32p, C.c_int64, C.c_int, _f32p]),
     "mhnsw_distance_device": (C.c_int, [C.c_int, _vp, _vp, C.c_int64, C.c_int, _vp, _vp]),
     "mhnsw_export_sizes": (C.c_int, [_vp, _i64p, _P(C.c_int), _P(C.c_int), _P(C.c_int)]),
-    "mhnsw_export": (C.c_int, [_vp, _i64p, _f32p, _i32p, _i32p, C.c_int, _i32p]),
-    "mhnsw_import": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, C.c_int, _i64p, _f32p, _i32p, _i32p, _i32p]),
+    "mhnsw_export": (C.c_int, [_vp, _i64p, _f32p, _i32p, _i32p, C.c_int, _i32p, _u8p]),
+    "mhnsw_import": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, C.c_int, _i64p, _f32p, _i32p, _i32p, _i32p,
+                               _u8p]),
     "mhnsw_preview_levels": (C.c_int, [_vp, C.c_int64, _i32p]),
     "mhnsw_stats": (C.c_int, [_vp, _i64p, C.c_int]),
     "mhnsw_reset_stats": (C.c_int, [_vp]),

@@ -71,6 +71,8 @@ struct mhnsw_index {
     float* norms = nullptr;
     int64_t* keys = nullptr;
     int32_t* levels = nullptr;
+    uint8_t* dead = nullptr;  // [capn] deleted rows (graph.go:843-864)
+    bool any_dead = false;
     uint32_t* cur_entry = nullptr;
     int32_t* inc_cnt = nullptr;
     uint32_t* inc_src = nullptr;
@@ -94,8 +96,10 @@ struct mhnsw_index {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool have_timing = false;
     // host mirrors
-    std::unordered_map<int64_t, int32_t> key2id;
+    std::unordered_map<int64_t, int32_t> key2id;  // live keys only
     std::vector<int32_t> hlevels;
+    std::vector<uint32_t> hmask;  // bit l: row is in layer l (compat may promote into emptied layers)
+    std::vector<uint8_t> hdead;
     int64_t stats_host[8] = {0};
     std::string err;
     mutable std::shared_mutex mu;
@@ -255,6 +259,7 @@ int ensure_capacity(mhnsw_index* h, int64_t need) {
     if ((r = grow(h, h->norms, oc, nc, 0))) return r;
     if ((r = grow(h, h->keys, oc, nc, 0))) return r;
     if ((r = grow(h, h->levels, oc, nc, 0))) return r;
+    if ((r = grow(h, h->dead, oc, nc, 0))) return r;
     if ((r = grow(h, h->cur_entry, 0, nc, 0))) return r;
     if ((r = grow(h, h->inc_cnt, 0, nc, 0))) return r;
     if (h->build_mode == MHNSW_BUILD_BATCH || h->inc_src) {
@@ -300,7 +305,34 @@ GraphDev graph_view(const mhnsw_index* h) {
     g.nlayers = (int)h->layers.size();
     g.capn = (uint32_t)std::max<int64_t>(h->capn, 1);
     g.err = h->d_err;
+    g.dead = h->any_dead ? h->dead : nullptr;
     return g;
+}
+
+int64_t live_count(const mhnsw_index* h) { return h->layers.empty() ? 0 : h->layers[0].count; }
+
+// highest layer holding a live node (Search skips emptied top layers, graph.go:572-582)
+int top_live_layer(const mhnsw_index* h) {
+    int top = (int)h->layers.size() - 1;
+    while (top > 0 && h->layers[top].count == 0) --top;
+    return top;
+}
+
+bool in_layer(const mhnsw_index* h, int64_t id, int l) { return (h->hmask[id] >> l) & 1u; }
+
+// lowest-id live member: the deterministic stand-in for entry() (graph.go:250-258)
+void fix_entries(mhnsw_index* h) {
+    for (int l = 0; l < (int)h->layers.size(); ++l) {
+        Layer& L = h->layers[l];
+        if (L.entry >= 0 && in_layer(h, L.entry, l) && !h->hdead[L.entry]) continue;
+        L.entry = -1;
+        if (L.count == 0) continue;
+        for (int64_t i = 0; i < h->n; ++i)
+            if (in_layer(h, i, l) && !h->hdead[i]) {
+                L.entry = (int32_t)i;
+                break;
+            }
+    }
 }
 
 int set_shape(mhnsw_index* h, int dim) {
@@ -321,7 +353,8 @@ int set_deg(mhnsw_index* h, int l, int64_t id, int32_t v) {
 
 int sync_layer_entries(mhnsw_index* h) {
     int32_t e[MH_MAXL];
-    for (int l = 0; l < MH_MAXL; ++l) e[l] = l < (int)h->layers.size() ? h->layers[l].entry : -1;
+    for (int l = 0; l < MH_MAXL; ++l)
+        e[l] = l < (int)h->layers.size() && h->layers[l].count > 0 ? h->layers[l].entry : -1;
     HIPCHK(h, hipMemcpyAsync(h->d_layer_entry, e, sizeof(e), hipMemcpyHostToDevice, h->stream));
     return 0;
 }
@@ -334,7 +367,7 @@ int zero_err(mhnsw_index* h) {
 // ---------------------------------------------------------------------------
 // build drivers
 // ---------------------------------------------------------------------------
-int run_build_compat(mhnsw_index* h, int64_t n0, int64_t n1) {
+int run_build_compat(mhnsw_index* h, int64_t n0, int64_t n1, int top0) {
     if (h->M + 1 > 64) return fail(h, MHNSW_EUNSUPPORTED, "compat build supports M <= 63");
     int r;
     if ((r = sync_layer_entries(h))) return r;
@@ -346,6 +379,7 @@ int run_build_compat(mhnsw_index* h, int64_t n0, int64_t n1) {
     a.n1 = n1;
     a.levels = h->levels;
     a.layer_entry = h->d_layer_entry;
+    a.top0 = top0;
     a.M = h->M;
     a.ef = h->ef;
     a.stats = h->d_stats + 4;
@@ -400,7 +434,8 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
     return 0;
 }
 
-int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1) {
+// top / entry: the live top layer and its entry before this batch (-1: empty graph)
+int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1, int top, uint32_t entry) {
     int r;
     if ((r = zero_err(h))) return r;
     if (!h->inc_src) {
@@ -413,14 +448,6 @@ int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1) {
         if (hipMalloc(&h->touched, tneed * 4) != hipSuccess) return fail(h, MHNSW_ENOMEM, "device allocation failed");
         h->touched_cap = tneed;
     }
-    // top layer / entry before this call, from the levels of nodes < n0
-    int top = -1;
-    uint32_t entry = EMPTY_ID;
-    for (int64_t i = 0; i < n0; ++i)
-        if (h->hlevels[i] > top) {
-            top = h->hlevels[i];
-            entry = (uint32_t)i;
-        }
     int64_t i = n0;
     while (i < n1) {
         const int lv = h->hlevels[i];
@@ -478,7 +505,8 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     if (m0_of(h) + 1 > 64 || h->M + 1 > 64) return fail(h, MHNSW_EUNSUPPORTED, "degree caps above 63 unsupported");
     if ((r = ensure_caps(h))) return r;
     const int64_t n0 = h->n, n1 = h->n + n;
-    // levels (graph.go:457): count before each insert grows by one
+    const int64_t live0 = live_count(h);
+    // levels (graph.go:457): the layer-0 size (live nodes) grows by one per insert
     std::vector<int32_t> lv(n);
     bool le = h->layers_exist;
     for (int64_t i = 0; i < n; ++i) {
@@ -486,12 +514,19 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
             lv[i] = levels[i];
             if (lv[i] < 0) return fail(h, MHNSW_EINVAL, "invalid level: %d", lv[i]);
         } else {
-            lv[i] = random_level(h->ml, le, n0 + i, &h->rng);
+            lv[i] = random_level(h->ml, le, live0 + i, &h->rng);
         }
         if (lv[i] >= MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "level %d >= %d", lv[i], MH_MAXL);
         le = true;
     }
     if ((r = ensure_capacity(h, n1))) return r;
+    const int top0 = (int)h->layers.size() - 1;  // len(g.layers) - 1 before this batch
+    int top_live = -1;
+    uint32_t entry_live = EMPTY_ID;
+    if (h->layers_exist && live0 > 0) {
+        top_live = top_live_layer(h);
+        entry_live = (uint32_t)h->layers[top_live].entry;
+    }
     int maxl = 0;
     for (auto v : lv) maxl = std::max(maxl, v);
     if ((r = ensure_layer(h, maxl))) return r;
@@ -506,22 +541,33 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     }
     LCHK(h, launch_pad_rows(src, n, dim, h->vecs + (size_t)n0 * h->pitch, h->pitch, h->stream));
     LCHK(h, launch_norms(h->vecs, n0, n1, h->pitch, h->lpr, h->vpl, h->norms, h->stream));
-    // host bookkeeping
+    // host bookkeeping: layer membership, counts, entries
+    const bool compat = h->build_mode == MHNSW_BUILD_COMPAT;
+    h->hmask.resize(n1, 0u);
+    h->hdead.resize(n1, 0);
+    int nl = top0 + 1;
     for (int64_t i = 0; i < n; ++i) {
         const int32_t id = (int32_t)(n0 + i);
         h->key2id[keys[i]] = id;
         h->hlevels.push_back(lv[i]);
-        for (int l = 0; l <= lv[i]; ++l) {
-            if (h->layers[l].count == 0) h->layers[l].entry = id;
-            h->layers[l].count++;
+        nl = std::max(nl, lv[i] + 1);  // graph.go:462-464
+        uint32_t mask = 0;
+        for (int l = nl - 1; l >= 0; --l) {
+            Layer& L = h->layers[l];
+            // graph.go:485-488: an empty layer takes the node whatever its level
+            if (!(l <= lv[i] || (compat && L.count == 0))) continue;
+            if (L.count == 0) L.entry = id;
+            L.count++;
+            mask |= 1u << l;
         }
+        h->hmask[id] = mask;
     }
     h->layers_exist = true;
     h->n = n1;
-    if (h->build_mode == MHNSW_BUILD_COMPAT)
-        r = run_build_compat(h, n0, n1);
+    if (compat)
+        r = run_build_compat(h, n0, n1, top0);
     else
-        r = run_build_batch(h, n0, n1);
+        r = run_build_batch(h, n0, n1, top_live, entry_live);
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return r;
 }
@@ -537,7 +583,7 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
     }
     if (mode < 0 || mode > 2) return fail(h, MHNSW_EINVAL, "unknown search mode %d", mode);
     if (B <= 0) return 0;
-    if (!h->layers_exist || h->n == 0) {  // graph.go:554-556: nil, nil
+    if (!h->layers_exist || live_count(h) == 0) {  // graph.go:554-556: nil, nil
         if (on_device)
             HIPCHK(h, hipMemsetAsync(on, 0, B * 4, s));
         else
@@ -545,12 +591,11 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         return 0;
     }
     if (ef <= 0) ef = h->ef;
-    int top = (int)h->layers.size() - 1;
-    while (top > 0 && h->layers[top].count == 0) --top;
+    const int top = top_live_layer(h);
     uint32_t entry = (uint32_t)h->layers[top].entry;
     if (entry_key) {
         auto it = h->key2id.find(*entry_key);
-        if (it == h->key2id.end() || h->hlevels[it->second] < top)
+        if (it == h->key2id.end() || !in_layer(h, it->second, top))
             return fail(h, MHNSW_EINVAL, "entry key %lld not in top layer", (long long)*entry_key);
         entry = (uint32_t)it->second;
     }
@@ -593,7 +638,7 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             ExactArgs a;
             a.X = h->vecs;
             a.xnorm = h->norms;
-            a.deg0 = h->layers[0].deg;
+            a.dead = h->any_dead ? h->dead : nullptr;
             a.N = h->n;
             a.Q = h->qpad.p + (size_t)q0 * h->pitch;
             a.qnorm = h->qnorm.p + q0;
@@ -707,6 +752,7 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->norms);
     F(h->keys);
     F(h->levels);
+    F(h->dead);
     F(h->cur_entry);
     F(h->inc_cnt);
     F(h->inc_src);
@@ -914,17 +960,19 @@ int mhnsw_export_sizes(mhnsw_index* h, int64_t* N, int* dim, int* L, int* cap) {
     return 0;
 }
 
-int mhnsw_export(mhnsw_index* h, int64_t* keys, float* vecs, int32_t* deg, int32_t* adj, int cap, int32_t* entry) {
+int mhnsw_export(mhnsw_index* h, int64_t* keys, float* vecs, int32_t* deg, int32_t* adj, int cap, int32_t* entry,
+                 uint8_t* dead) {
     std::shared_lock<std::shared_mutex> lk(h->mu);
     const int64_t N = h->n;
     if (N == 0) return 0;
+    if (dead) memcpy(dead, h->hdead.data(), (size_t)N);
     HIPCHK(h, hipMemcpy(keys, h->keys, N * 8, hipMemcpyDeviceToHost));
     HIPCHK(h, hipMemcpy2D(vecs, (size_t)h->dim * 4, h->vecs, (size_t)h->pitch * 4, (size_t)h->dim * 4, N,
                           hipMemcpyDeviceToHost));
     std::vector<int32_t> row;
     for (int l = 0; l < (int)h->layers.size(); ++l) {
         const Layer& L = h->layers[l];
-        entry[l] = L.entry;
+        entry[l] = L.count > 0 ? L.entry : -1;
         HIPCHK(h, hipMemcpy(deg + (size_t)l * N, L.deg, N * 4, hipMemcpyDeviceToHost));
         row.resize((size_t)N * L.cap);
         HIPCHK(h, hipMemcpy(row.data(), L.adj, (size_t)N * L.cap * 4, hipMemcpyDeviceToHost));
@@ -939,7 +987,7 @@ int mhnsw_export(mhnsw_index* h, int64_t* keys, float* vecs, int32_t* deg, int32
 }
 
 int mhnsw_import(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t* keys, const float* vecs,
-                 const int32_t* deg, const int32_t* adj, const int32_t* entry) {
+                 const int32_t* deg, const int32_t* adj, const int32_t* entry, const uint8_t* dead) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
     if (h->n > 0) return fail(h, MHNSW_EINVAL, "import requires an empty index");
     if (L > MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "more than %d layers", MH_MAXL);
@@ -968,6 +1016,14 @@ int mhnsw_import(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64
     HIPCHK(h, hipStreamSynchronize(h->stream));
     std::vector<int32_t> row;
     h->hlevels.assign(N, 0);
+    h->hmask.assign(N, 0u);
+    h->hdead.assign(N, 0);
+    h->any_dead = false;
+    for (int64_t i = 0; i < N && dead; ++i) {
+        h->hdead[i] = dead[i] ? 1 : 0;
+        h->any_dead |= dead[i] != 0;
+    }
+    HIPCHK(h, hipMemcpy(h->dead, h->hdead.data(), (size_t)N, hipMemcpyHostToDevice));
     for (int l = 0; l < L; ++l) {
         Layer& Ly = h->layers[l];
         HIPCHK(h, hipMemcpy(Ly.deg, deg + (size_t)l * N, N * 4, hipMemcpyHostToDevice));
@@ -976,8 +1032,9 @@ int mhnsw_import(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64
         for (int64_t i = 0; i < N; ++i) {
             const int d = deg[(size_t)l * N + i];
             if (d != -2) {
-                Ly.count++;
+                h->hmask[i] |= 1u << l;
                 h->hlevels[i] = std::max(h->hlevels[i], l);
+                if (!h->hdead[i]) Ly.count++;
             }
             for (int j = 0; j < d && j < cap; ++j) row[(size_t)i * Ly.cap + j] = adj[((size_t)l * N + i) * cap + j];
         }
@@ -987,10 +1044,86 @@ int mhnsw_import(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64
     HIPCHK(h, hipMemcpy(h->levels, h->hlevels.data(), N * 4, hipMemcpyHostToDevice));
     h->key2id.clear();
     for (int64_t i = 0; i < N; ++i)
-        if (!h->key2id.count(keys[i])) h->key2id[keys[i]] = (int32_t)i;
+        if (!h->hdead[i] && !h->key2id.count(keys[i])) h->key2id[keys[i]] = (int32_t)i;
     h->n = N;
     h->layers_exist = L > 0;
     return 0;
+}
+
+// graph.go:843-895 Delete / BatchDelete
+int mhnsw_delete(mhnsw_index* h, const int64_t* keys, int64_t n, uint8_t* out) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    if (n > 0 && (!keys || !out)) return fail(h, MHNSW_EINVAL, "keys and out must be non-NULL");
+    for (int64_t i = 0; i < n; ++i) out[i] = 0;
+    if (n <= 0 || h->layers.empty()) return 0;
+    std::vector<uint32_t> ids;
+    for (int64_t i = 0; i < n; ++i) {
+        auto it = h->key2id.find(keys[i]);
+        if (it == h->key2id.end()) continue;  // not found (or deleted earlier in this batch)
+        const int32_t id = it->second;
+        h->key2id.erase(it);
+        h->hdead[id] = 1;
+        for (int l = 0; l < (int)h->layers.size(); ++l)
+            if (in_layer(h, id, l)) h->layers[l].count--;
+        out[i] = 1;
+        ids.push_back((uint32_t)id);
+    }
+    if (ids.empty()) return 0;
+    h->any_dead = true;
+    int r;
+    HIPCHK(h, hipMemcpyAsync(h->dead, h->hdead.data(), (size_t)h->n, hipMemcpyHostToDevice, h->stream));
+    if ((r = zero_err(h)) || (r = sync_layer_table(h))) return r;
+    DeleteArgs a;
+    memset(&a, 0, sizeof(a));
+    a.g = graph_view(h);
+    a.stats = h->d_stats + 4;
+    a.err = h->d_err;
+    a.vis_log2 = h->vis_log2;
+    if (h->build_mode == MHNSW_BUILD_COMPAT) {
+        if ((r = ensure_buf(h, h->cand, ids.size()))) return r;
+        HIPCHK(h, hipMemcpyAsync(h->cand.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, h->stream));
+        a.ids = h->cand.p;
+        a.nids = (int64_t)ids.size();
+        a.M = h->M;
+        const int lr = launch_delete_compat(a, h->lpr, h->vpl, h->stream);
+        if (lr == -2) return fail(h, MHNSW_EUNSUPPORTED, "compat delete LDS budget exceeded (M=%d)", h->M);
+        LCHK(h, lr);
+    } else {
+        a.n = h->n;
+        a.heuristic = h->heuristic;
+        a.keep_pruned = h->keep_pruned;
+        for (int l = 0; l < (int)h->layers.size(); ++l) {
+            a.layer = l;
+            a.mcap = l == 0 ? m0_of(h) : h->M;
+            LCHK(h, launch_delete_repair(a, h->lpr, h->vpl, h->stream));
+        }
+    }
+    fix_entries(h);
+    int err = 0;
+    HIPCHK(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (err & 1) return fail(h, MHNSW_EINTERNAL, "visited set overflow (raise vis_log2)");
+    if (err & 4) return fail(h, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
+    if (err & 8) return fail(h, MHNSW_EINTERNAL, "replenish candidate heap overflow");
+    return 0;
+}
+
+// analyzer.go:20-38 Connectivity: mean len(neighbors) per non-empty layer
+int mhnsw_connectivity(mhnsw_index* h, double* out, int max_layers) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    std::vector<int32_t> deg((size_t)std::max<int64_t>(h->n, 1));
+    int w = 0;
+    for (int l = 0; l < (int)h->layers.size(); ++l) {
+        const Layer& L = h->layers[l];
+        if (L.count == 0) continue;
+        HIPCHK(h, hipMemcpy(deg.data(), L.deg, (size_t)h->n * 4, hipMemcpyDeviceToHost));
+        double sum = 0;
+        for (int64_t i = 0; i < h->n; ++i)
+            if (in_layer(h, i, l) && !h->hdead[i]) sum += std::max(deg[i], 0);
+        if (w < max_layers && out) out[w] = sum / (double)L.count;
+        ++w;
+    }
+    return w;
 }
 
 int mhnsw_preview_levels(mhnsw_index* h, int64_t n, int32_t* out) {
@@ -998,7 +1131,7 @@ int mhnsw_preview_levels(mhnsw_index* h, int64_t n, int32_t* out) {
     uint64_t s = h->rng;
     bool le = h->layers_exist;
     for (int64_t i = 0; i < n; ++i) {
-        out[i] = random_level(h->ml, le, h->n + i, &s);
+        out[i] = random_level(h->ml, le, live_count(h) + i, &s);
         le = true;
     }
     return 0;

@@ -187,8 +187,7 @@ __global__ __launch_bounds__(64) void k_build_compat(CompatBuildArgs a) {
     S.hcap = hcap;
     WaveStats st;
     int err = 0;
-    int top = -1;
-    for (int64_t i = 0; i < a.n0; ++i) top = max(top, a.levels[i]);
+    int top = a.top0;
     for (int64_t i = a.n0; i < a.n1; ++i) {
         const uint32_t id = (uint32_t)i;
         const int level = a.levels[i];
@@ -205,7 +204,15 @@ __global__ __launch_bounds__(64) void k_build_compat(CompatBuildArgs a) {
                 build_sync();
                 continue;
             }
-            const uint32_t sp = elevator != EMPTY_ID ? elevator : (uint32_t)ent;  // graph.go:492-498
+            // graph.go:492-498: layer.nodes[*elevator] is nil once that node was deleted
+            uint32_t sp = ent < 0 ? EMPTY_ID : (uint32_t)ent;
+            if (elevator != EMPTY_ID)
+                sp = (ld_i32<true>(a.g.layers[l].deg + elevator) != -2 && !is_dead(a.g, elevator)) ? elevator
+                                                                                                   : EMPTY_ID;
+            if (sp == EMPTY_ID) {  // search(nil) -> "no nodes found in neighborhood search"
+                err |= 2;
+                break;
+            }
             const int cnt = compat_layer<C, G, true>(a.g, l, sp, a.M, a.ef, q, qn, S.cs, st, err);  // :500
             if (cnt == 0) {
                 err |= 2;
@@ -284,6 +291,7 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
             bl_at(L, i, dc, c);
             if (c == EMPTY_ID) break;
             c &= ID_MASK;
+            if (is_dead(a.g, c)) continue;
             bool good = true;
             if (a.heuristic && nsel > 0) {  // HNSW Alg. 4: drop c if closer to a kept neighbour than to u
                 QReg<C> qc;
@@ -309,6 +317,7 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
                 bl_at(L, i, dc, c);
                 if (c == EMPTY_ID) break;
                 c &= ID_MASK;
+                if (is_dead(a.g, c)) continue;
                 if (__ballot(lane < nsel && sel == c)) continue;
                 if (lane == nsel) {
                     sel = c;
@@ -437,6 +446,192 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// delete (graph.go:843-895)
+// ---------------------------------------------------------------------------
+// graph.go:221-235 isolate: neighbours in ascending key order (the map-order
+// stand-in) drop their backlink and are replenished; the deleted node's own
+// row stays (the reference keeps the layerNode behind one-directional edges).
+template <class C, int G>
+__device__ void isolate(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err) {
+    const int lane = lane_id();
+    const int capl = g.layers[l].cap;
+    const int dn = min(ld_i32<true>(g.layers[l].deg + n), capl);
+    if (dn < 0) return;  // nil neighbour map
+    uint32_t mine = 0xFFFFFFFFu;
+    int64_t key = INT64_MAX;
+    if (lane < dn) {
+        mine = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane));
+        key = g.keys[mine];
+    }
+    bitonic64(key, mine);
+    for (int j = 0; j < dn; ++j) {
+        const uint32_t x = rl_u(mine, j);
+        if (ld_i32<true>(g.layers[l].deg + x) < 0) continue;  // neighbor.neighbors == nil
+        list_remove<C, G>(g, l, x, n);                         // graph.go:231
+        replenish<C, G>(g, l, x, m, S, st, err);               // graph.go:232
+    }
+}
+
+// Delete / BatchDelete with the reference's semantics: one wave walks the keys
+// in order and every layer holding the node (graph.go:852-861).
+template <class C, int G>
+__global__ __launch_bounds__(64) void k_delete_compat(DeleteArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int lane = lane_id();
+    BuildSmem S;
+    S.cs.vis = smem;
+    S.cs.vlog2 = a.vis_log2;
+    uint32_t* p = smem + (1 << a.vis_log2);
+    const int hcap = a.M * (a.M + 1) + 2;
+    S.hd = reinterpret_cast<float*>(p);
+    p += hcap;
+    S.hi = p;
+    S.hcap = hcap;
+    WaveStats st;
+    int err = 0;
+    for (int64_t i = 0; i < a.nids; ++i) {
+        const uint32_t id = a.ids[i];
+        for (int l = 0; l < a.g.nlayers; ++l) {
+            if (ld_i32<true>(a.g.layers[l].deg + id) == -2) continue;
+            isolate<C, G>(a.g, l, id, a.M, S, st, err);
+        }
+    }
+    if (lane == 0) {
+        atomicAdd(&a.stats[0], st.E);
+        if (err) atomicOr(a.err, err);
+    }
+}
+
+// Batched-graph repair, one wave per row of layer a.layer: a live row that
+// points at a deleted node is rebuilt from its live neighbours plus the rows
+// of its deleted neighbours (gather order, first REPAIR_POOL kept), ranked by
+// (distance, id) and selected like k_batch_search (diversity heuristic,
+// optional keep-pruned fill).  Deleted rows are only read and live rows are
+// only written by their owner, so rows are independent.  Restated in
+// oracle/oracle.c repair_layer.
+template <class C, int G>
+__global__ __launch_bounds__(64) void k_delete_repair(DeleteArgs a) {
+    __shared__ uint32_t pid[REPAIR_POOL];
+    __shared__ float pd[REPAIR_POOL];
+    __shared__ uint32_t sid[REPAIR_POOL];
+    __shared__ float sdd[REPAIR_POOL];
+    const int64_t v64 = blockIdx.x;
+    if (v64 >= a.n) return;
+    const uint32_t v = (uint32_t)v64;
+    const int lane = lane_id();
+    const int l = a.layer;
+    if (a.g.dead[v]) return;
+    const int capl = a.g.layers[l].cap;
+    const int d = min(a.g.layers[l].deg[v], capl);
+    if (d <= 0) return;
+    int32_t* row = a.g.layers[l].adj + (size_t)v * capl;
+    float* rowd = a.g.layers[l].adjd + (size_t)v * capl;
+    const uint32_t nb = lane < d ? guard_id(a.g, (uint32_t)row[lane]) : 0u;
+    const bool nd = lane < d && a.g.dead[nb];
+    const unsigned long long mdead = __ballot(nd);
+    if (!mdead) return;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const unsigned long long mlive = __ballot(lane < d && !nd);
+    if (lane < d && !nd) pid[__popcll(mlive & below)] = nb;
+    int np = __popcll(mlive);
+    for (unsigned long long m = mdead; m; m &= m - 1) {
+        const int j = __ffsll((long long)m) - 1;
+        const uint32_t x = rl_u(nb, j);
+        const int dx = min(a.g.layers[l].deg[x], capl);
+        if (dx <= 0) continue;
+        const uint32_t y = lane < dx ? guard_id(a.g, (uint32_t)a.g.layers[l].adj[(size_t)x * capl + lane]) : 0u;
+        const bool ok = lane < dx && y != v && !a.g.dead[y];
+        const unsigned long long my = __ballot(ok);
+        const int pos = np + __popcll(my & below);
+        if (ok && pos < REPAIR_POOL) pid[pos] = y;
+        np = min(np + __popcll(my), REPAIR_POOL);
+    }
+    __syncthreads();
+    QReg<C> q;
+    load_query(q, a.g.vecs + (size_t)v * a.g.pitch);
+    const float qn = a.g.norms[v];
+    const float inf = __int_as_float(0x7f800000);
+    WaveStats st;
+    for (int base = 0; base < np; base += 64) {
+        const int cnt = min(64, np - base);
+        const uint32_t cid = lane < cnt ? pid[base + lane] : 0u;
+        int t = base;
+        st.E += cnt;
+        eval_list<C, G>(a.g, q, qn, cid, cnt, a.g.metric, [&](float dd, uint32_t) {
+            if (lane == 0) pd[t] = dd != dd ? inf : dd;  // NaN (zero vectors) ranks last
+            ++t;
+        });
+    }
+    __syncthreads();
+    for (int e = lane; e < np; e += 64) {  // rank by (dist, id); duplicates keep gather order
+        const float md = pd[e];
+        const uint32_t mi = pid[e];
+        int rank = 0;
+        for (int f = 0; f < np; ++f) {
+            const float fd = pd[f];
+            const uint32_t fi = pid[f];
+            rank += (lt_di(fd, fi, md, mi) || (fd == md && fi == mi && f < e)) ? 1 : 0;
+        }
+        sdd[rank] = md;
+        sid[rank] = mi;
+    }
+    __syncthreads();
+    uint32_t kept = 0;  // lane j holds the j-th kept id
+    float keptd = 0.f;
+    int nkeep = 0;
+    for (int i = 0; i < np && nkeep < a.mcap; ++i) {
+        const uint32_t c = sid[i];
+        if (i > 0 && c == sid[i - 1]) continue;
+        const float dcv = sdd[i];
+        bool good = true;
+        if (a.heuristic && nkeep > 0) {
+            QReg<C> qc;
+            load_query(qc, a.g.vecs + (size_t)c * a.g.pitch);
+            const float cn = a.g.norms[c];
+            st.E += nkeep;
+            eval_list<C, G>(a.g, qc, cn, kept, nkeep, a.g.metric, [&](float dcs, uint32_t) {
+                if (dcs < dcv) good = false;
+            });
+        }
+        if (good) {
+            if (lane == nkeep) {
+                kept = c;
+                keptd = dcv;
+            }
+            ++nkeep;
+        }
+    }
+    if (a.keep_pruned) {
+        for (int i = 0; i < np && nkeep < a.mcap; ++i) {
+            const uint32_t c = sid[i];
+            if (i > 0 && c == sid[i - 1]) continue;
+            if (__ballot(lane < nkeep && kept == c)) continue;
+            if (lane == nkeep) {
+                kept = c;
+                keptd = sdd[i];
+            }
+            ++nkeep;
+        }
+    }
+    if (lane < nkeep) {
+        row[lane] = (int32_t)kept;
+        rowd[lane] = keptd;
+    }
+    if (lane == 0) {
+        a.g.layers[l].deg[v] = nkeep;
+        atomicAdd(&a.stats[0], st.E);
+    }
+}
+
+template <class C, int G>
+static int launch_delete_compat_t(const DeleteArgs& a, hipStream_t s) {
+    const size_t words = ((size_t)1 << a.vis_log2) + 2 * (size_t)(a.M * (a.M + 1) + 2);
+    if (words * 4 > 160 * 1024) return -2;
+    hipLaunchKernelGGL((k_delete_compat<C, G>), dim3(1), dim3(64), words * 4, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 template <class C, int R, int G>
 static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 << a.vis_log2;
@@ -487,6 +682,28 @@ int launch_build_batch_commit(const BatchBuildArgs& a, int lpr, int vpl, int64_t
         hipLaunchKernelGGL((k_batch_commit<Cfg<L, V>, (G < 4 ? G : 4)>), dim3((unsigned)max_touched), \
                            dim3(64), 0, s, a);                                                        \
         return hipGetLastError() == hipSuccess ? 0 : -1;                                              \
+    }
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return -3;
+}
+
+int launch_delete_compat(const DeleteArgs& a, int lpr, int vpl, hipStream_t s) {
+    if (a.nids <= 0) return 0;
+#define X_(L, V, G) \
+    if (lpr == L && vpl == V) return launch_delete_compat_t<Cfg<L, V>, (G < 2 ? G : 2)>(a, s);
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return -3;
+}
+
+int launch_delete_repair(const DeleteArgs& a, int lpr, int vpl, hipStream_t s) {
+    if (a.n <= 0) return 0;
+#define X_(L, V, G)                                                                                      \
+    if (lpr == L && vpl == V) {                                                                          \
+        hipLaunchKernelGGL((k_delete_repair<Cfg<L, V>, (G < 4 ? G : 4)>), dim3((unsigned)a.n), dim3(64), 0, s, \
+                           a);                                                                           \
+        return hipGetLastError() == hipSuccess ? 0 : -1;                                                 \
     }
     MH_FOR_EACH_CFG(X_)
 #undef X_

@@ -49,7 +49,15 @@ struct GraphDev {
     int nlayers;
     uint32_t capn;  // rows allocated: every gathered id is checked against it
     int* err;       // bit 4: out-of-range id seen (load clamped, no fault)
+    const uint8_t* dead;  // [cap_nodes] 1 = deleted (nullptr until the first Delete)
 };
+
+__device__ __forceinline__ bool is_dead(const GraphDev& g, uint32_t id) { return g.dead && g.dead[id]; }
+
+// `layer.nodes[key] != nil` (graph.go:576-578): present in layer l and not deleted
+__device__ __forceinline__ bool is_member(const GraphDev& g, int l, uint32_t id) {
+    return id < g.capn && g.layers[l].deg[id] != -2 && !is_dead(g, id);
+}
 
 // bounds guard for gathered ids: records the violation and clamps to row 0
 __device__ __forceinline__ uint32_t guard_id(const GraphDev& g, uint32_t id) {

@@ -56,12 +56,31 @@ struct CompatBuildArgs {
     int64_t n0, n1;               // insert internal ids [n0, n1) in order
     const int32_t* levels;        // [cap_nodes] level of each node
     const int32_t* layer_entry;   // [MH_MAXL] first node id of each layer (-1 none)
+    int top0;                     // len(g.layers) - 1 before this batch (-1: no layers)
     int M, ef;
     unsigned long long* stats;    // [0]=dist evals [1]=expansions
     int* err;
     int vis_log2;
 };
 int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, hipStream_t s);
+
+// ---- delete (graph.go:843-895) ----
+struct DeleteArgs {
+    GraphDev g;
+    const uint32_t* ids;          // compat: internal ids in BatchDelete order
+    int64_t nids;
+    int64_t n;                    // repair: rows [0, n)
+    int layer;                    // repair: layer being repaired
+    int M;                        // compat: the reference's cap (M on every layer)
+    int mcap;                     // repair: row cap of this layer
+    int heuristic, keep_pruned;   // repair: selection rule (as the batched insert)
+    unsigned long long* stats;    // [0]=dist evals
+    int* err;
+    int vis_log2;
+};
+constexpr int REPAIR_POOL = 256;  // candidate pool per repaired row (oracle: OG_REPAIR_POOL)
+int launch_delete_compat(const DeleteArgs& a, int lpr, int vpl, hipStream_t s);
+int launch_delete_repair(const DeleteArgs& a, int lpr, int vpl, hipStream_t s);
 
 struct BatchBuildArgs {
     GraphDev g;
@@ -89,7 +108,7 @@ int launch_build_batch_commit(const BatchBuildArgs& a, int lpr, int vpl, int64_t
 struct ExactArgs {
     const float* X;       // [N * pitch]
     const float* xnorm;   // [N]
-    const int32_t* deg0;  // [N] layer-0 membership (-2 absent)
+    const uint8_t* dead;  // [N] 1 = deleted row (nullable)
     int64_t N;
     const float* Q;       // [B * pitch]
     const float* qnorm;   // [B] canonical |q|

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void k_scores(ExactArgs a) {
     for (int j = 0; j < 2; ++j) {
         const int64_t xr = n0 + wn * 64 + j * 32 + li;
         if (xr >= a.N) continue;
-        const bool xok = a.deg0[xr] != -2;
+        const bool xok = !(a.dead && a.dead[xr]);
         const float xn = a.xnorm[xr];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {

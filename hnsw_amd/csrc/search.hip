@@ -183,6 +183,11 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
     {
         BList<1> L1;
         for (int l = a.top; l >= 1; --l) {  // greedy descent, ef = 1
+            if (a.g.layers[l].deg[ep] == -2) {  // not in this layer: restart at its entry
+                const int32_t e = a.layer_entry[l];
+                if (e < 0) continue;
+                ep = (uint32_t)e;
+            }
             beam_layer<C, 1, G>(a.g, l, ep, 1, q, qn, L1, smem, a.vis_log2, st);
             float d;
             uint32_t id;
@@ -192,19 +197,30 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
     }
     BList<R> L;
     const int efl = a.ef > a.k ? a.ef : a.k;
+    if (a.g.layers[0].deg[ep] == -2) ep = (uint32_t)a.layer_entry[0];
     beam_layer<C, R, G>(a.g, 0, ep, efl, q, qn, L, smem, a.vis_log2, st);
+    // compact the sorted list into the first k live entries (deleted rows
+    // route the search but are never returned)
     int nvalid = 0;
+    const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int idx = r * 64 + lane;
-        const bool ok = idx < a.k && L.i[r] != EMPTY_ID;
-        nvalid += __popcll(__ballot(ok));
-        if (idx < a.k) {
-            const uint32_t id = L.i[r] & ID_MASK;
-            a.out_keys[b * a.k + idx] = ok ? a.g.keys[id] : (int64_t)-1;
-            a.out_dist[b * a.k + idx] = ok ? L.d[r] : __int_as_float(0x7f800000);
-            if (a.out_ids) a.out_ids[b * a.k + idx] = ok ? (int32_t)id : -1;
+        const uint32_t id = L.i[r] & ID_MASK;
+        const bool ok = L.i[r] != EMPTY_ID && !is_dead(a.g, id);
+        const unsigned long long m = __ballot(ok);
+        const int pos = nvalid + __popcll(m & below);
+        if (ok && pos < a.k) {
+            a.out_keys[b * a.k + pos] = a.g.keys[id];
+            a.out_dist[b * a.k + pos] = L.d[r];
+            if (a.out_ids) a.out_ids[b * a.k + pos] = (int32_t)id;
         }
+        nvalid += __popcll(m);
+    }
+    nvalid = min(nvalid, a.k);
+    for (int i = nvalid + lane; i < a.k; i += 64) {
+        a.out_keys[b * a.k + i] = (int64_t)-1;
+        a.out_dist[b * a.k + i] = __int_as_float(0x7f800000);
+        if (a.out_ids) a.out_ids[b * a.k + i] = -1;
     }
     if (lane == 0) {
         a.out_n[b] = nvalid;
@@ -236,8 +252,13 @@ __global__ __launch_bounds__(64) void k_search_compat(SearchArgs a) {
     uint32_t elevator = EMPTY_ID;
     int nres = 0;
     for (int l = a.top; l >= 0; --l) {  // graph.go:571-622
-        uint32_t p = elevator != EMPTY_ID ? elevator
-                                          : (l == a.top ? a.entry : (uint32_t)a.layer_entry[l]);
+        // searchPoint: layers[l].nodes[*elevator] (nil once deleted) or entry() (nil when empty)
+        uint32_t p;
+        if (elevator != EMPTY_ID)
+            p = is_member(a.g, l, elevator) ? elevator : EMPTY_ID;
+        else
+            p = l == a.top ? a.entry : (a.layer_entry[l] < 0 ? EMPTY_ID : (uint32_t)a.layer_entry[l]);
+        if (p == EMPTY_ID) continue;  // search(nil) returns nothing (graph.go:101-103)
         if (l > 0) {
             const int c = compat_layer<C, G>(a.g, l, p, 1, a.ef, q, qn, S, st, err);
             if (c == 0) continue;

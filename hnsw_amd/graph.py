@@ -264,6 +264,27 @@ class Graph:
         lib = load()
         return [int(lib.mhnsw_layer_count(self._h, l)) for l in range(lib.mhnsw_num_layers(self._h))]
 
+    def Connectivity(self) -> List[float]:  # analyzer.go:20-38
+        out = np.zeros(64, np.float64)
+        n = self._check(load().mhnsw_connectivity(self._h, _ptr(out, C.c_double), 64))
+        return out[:n].tolist()
+
+    # -- Delete / BatchDelete (graph.go:843-895) -------------------------------
+    def Delete(self, key: int) -> bool:
+        return self.BatchDelete([key])[0]
+
+    def BatchDelete(self, keys) -> List[bool]:
+        keys = np.ascontiguousarray(np.asarray(list(keys) if not isinstance(keys, np.ndarray) else keys).reshape(-1),
+                                    np.int64)
+        out = np.zeros(max(len(keys), 1), np.uint8)
+        self._sync()
+        self._check(load().mhnsw_delete(self._h, _ptr(keys, C.c_int64), len(keys), _ptr(out, C.c_uint8)))
+        res = [bool(x) for x in out[:len(keys)]]
+        for key, ok in zip(keys.tolist(), res):
+            if ok:
+                self._values.pop(int(key), None)
+        return res
+
     # -- levels / stats / exchange ------------------------------------------------
     def preview_levels(self, n: int) -> np.ndarray:
         out = np.zeros(n, np.int32)
@@ -296,21 +317,23 @@ class Graph:
         deg = np.zeros((L, N), np.int32)
         adj = np.zeros((L, N, cap), np.int32)
         entry = np.zeros(max(L, 1), np.int32)
+        dead = np.zeros(max(N, 1), np.uint8)
         self._check(lib.mhnsw_export(self._h, _ptr(keys, C.c_int64), _ptr(vecs, C.c_float), _ptr(deg, C.c_int32),
-                                     _ptr(adj, C.c_int32), cap, _ptr(entry, C.c_int32)))
-        return dict(keys=keys, vecs=vecs, deg=deg, adj=adj, entry=entry[:L])
+                                     _ptr(adj, C.c_int32), cap, _ptr(entry, C.c_int32), _ptr(dead, C.c_uint8)))
+        return dict(keys=keys, vecs=vecs, deg=deg, adj=adj, entry=entry[:L], dead=dead[:N])
 
-    def import_graph(self, keys, vecs, deg, adj, entry):
+    def import_graph(self, keys, vecs, deg, adj, entry, dead=None):
         keys = np.ascontiguousarray(keys, np.int64)
         vecs = _f32(vecs)
         deg = np.ascontiguousarray(deg, np.int32)
         adj = np.ascontiguousarray(adj, np.int32)
         entry = np.ascontiguousarray(entry, np.int32)
+        dd = None if dead is None else np.ascontiguousarray(dead, np.uint8)
         L, N = deg.shape
         self._sync()
         self._check(load().mhnsw_import(self._h, N, vecs.shape[1], L, adj.shape[2], _ptr(keys, C.c_int64),
                                         _ptr(vecs, C.c_float), _ptr(deg, C.c_int32), _ptr(adj, C.c_int32),
-                                        _ptr(entry, C.c_int32)))
+                                        _ptr(entry, C.c_int32), None if dd is None else _ptr(dd, C.c_uint8)))
 
 
 def NewGraph() -> Graph:  # graph.go:340-348

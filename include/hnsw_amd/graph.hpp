@@ -185,6 +185,32 @@ class Graph {  // graph.go:305-332
         return t;
     }
 
+    std::vector<double> Connectivity() {  // analyzer.go:20-38
+        std::vector<double> c(64);
+        int n = mhnsw_connectivity(h_, c.data(), (int)c.size());
+        c.resize(n > 0 ? (size_t)n : 0);
+        return c;
+    }
+
+    // graph.go:843-864
+    bool Delete(K key) { return BatchDelete(std::vector<K>{key})[0]; }
+
+    // graph.go:868-895
+    std::vector<bool> BatchDelete(const std::vector<K>& keys) {
+        std::vector<bool> res(keys.size(), false);
+        if (keys.empty()) return res;
+        sync();
+        std::vector<int64_t> k64(keys.begin(), keys.end());
+        std::vector<uint8_t> out(keys.size());
+        if (mhnsw_delete(h_, k64.data(), (int64_t)k64.size(), out.data()) < 0)
+            throw std::runtime_error(mhnsw_last_error(h_));
+        for (size_t i = 0; i < keys.size(); ++i) {
+            res[i] = out[i] != 0;
+            if (res[i]) values_.erase(k64[i]);
+        }
+        return res;
+    }
+
    private:
     void create() {
         int rc = mhnsw_create(MHNSW_COSINE, 16, 0.25, 20, Rng, &h_);

@@ -101,6 +101,17 @@ int mhnsw_dims(const mhnsw_index *h);
 int mhnsw_lookup(mhnsw_index *h, int64_t key, float *out_vec); /* 1 found, 0 absent, <0 error */
 int mhnsw_num_layers(const mhnsw_index *h);
 int64_t mhnsw_layer_count(const mhnsw_index *h, int layer);
+/* Analyzer.Connectivity (analyzer.go:20-38): mean neighbour count of each
+ * non-empty layer; returns how many layers it has (writes min(that, max_layers)) */
+int mhnsw_connectivity(mhnsw_index *h, double *out, int max_layers);
+
+/* ---- Graph.Delete / Graph.BatchDelete (graph.go:843-895) ----
+ * out[i] = 1 when keys[i] was present.  COMPAT build mode runs the reference's
+ * isolate + replenish per key (graph.go:172-235: the deleted row keeps its
+ * edges and stays reachable through one-directional links, as in Go); BATCH
+ * build mode repairs every row that points at a deleted node in parallel.
+ * Deleted rows are never returned by BEAM or EXACT searches. */
+int mhnsw_delete(mhnsw_index *h, const int64_t *keys, int64_t n, uint8_t *out);
 
 /* ---- DistanceFunc (distance.go:12-23): batched sweep of one query over n rows ---- */
 int mhnsw_distance(int metric, const float *q, const float *X, int64_t n, int dim, float *out);
@@ -109,11 +120,13 @@ int mhnsw_distance_device(int metric, const float *d_q, const float *d_X, int64_
 
 /* ---- graph exchange (CSR view of encode.go's layer/neighbour structure) ----
  * keys[N], vecs[N*dim], deg[L*N] (-2 absent, -1 nil map, >=0 degree),
- * adj[L*N*cap] internal ids (row-major, -1 padded), entry[L]. */
+ * adj[L*N*cap] internal ids (row-major, -1 padded), entry[L] (-1: empty
+ * layer), dead[N] (1 = deleted row; nullable). */
 int mhnsw_export_sizes(mhnsw_index *h, int64_t *N, int *dim, int *L, int *cap);
-int mhnsw_export(mhnsw_index *h, int64_t *keys, float *vecs, int32_t *deg, int32_t *adj, int cap, int32_t *entry);
+int mhnsw_export(mhnsw_index *h, int64_t *keys, float *vecs, int32_t *deg, int32_t *adj, int cap, int32_t *entry,
+                 uint8_t *dead);
 int mhnsw_import(mhnsw_index *h, int64_t N, int dim, int L, int cap, const int64_t *keys, const float *vecs,
-                 const int32_t *deg, const int32_t *adj, const int32_t *entry);
+                 const int32_t *deg, const int32_t *adj, const int32_t *entry, const uint8_t *dead);
 
 /* levels randomLevel() would draw for the next n Adds (does not consume the RNG) */
 int mhnsw_preview_levels(mhnsw_index *h, int64_t n, int32_t *out);

@@ -69,9 +69,11 @@ def lib():
         L.og_layer_search_compat.argtypes = [C.c_void_p, C.c_int, C.c_int32, C.c_int, C.c_int, f32p,
                                              i32p, f32p]
         L.og_export_sizes.argtypes = [C.c_void_p, i64p, P(C.c_int), P(C.c_int), P(C.c_int)]
-        L.og_export.argtypes = [C.c_void_p, i64p, f32p, i32p, i32p, C.c_int, i32p]
+        u8p = P(C.c_uint8)
+        L.og_export.argtypes = [C.c_void_p, i64p, f32p, i32p, i32p, C.c_int, i32p, u8p]
+        L.og_delete.argtypes = [C.c_void_p, i64p, C.c_int64, C.c_int, C.c_int, C.c_int, u8p]
         L.og_import.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, i64p, f32p, i32p,
-                                i32p, i32p]
+                                i32p, i32p, u8p]
         L.og_stats.argtypes = [C.c_void_p, i64p]
         L.og_reset_stats.argtypes = [C.c_void_p]
         _lib = L
@@ -134,8 +136,12 @@ class Graph:
         self.metric = metric
 
     def __del__(self):
-        if getattr(self, "_h", None):
-            lib().og_destroy(self._h)
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:  # module globals may be gone at interpreter exit
+            try:
+                _lib.og_destroy(h)
+            except Exception:
+                pass
             self._h = None
 
     def _check(self, rc):
@@ -211,21 +217,33 @@ class Graph:
         deg = np.zeros((L, N), np.int32)
         adj = np.zeros((L, N, cap), np.int32)
         entry = np.zeros(max(L, 1), np.int32)
+        dead = np.zeros(max(N, 1), np.uint8)
         self._check(lib().og_export(self._h, _p(keys, C.c_int64), _p(vecs, C.c_float), _p(deg, C.c_int32),
-                                    _p(adj, C.c_int32), cap, _p(entry, C.c_int32)))
-        return dict(keys=keys, vecs=vecs, deg=deg, adj=adj, entry=entry[:L])
+                                    _p(adj, C.c_int32), cap, _p(entry, C.c_int32), _p(dead, C.c_uint8)))
+        return dict(keys=keys, vecs=vecs, deg=deg, adj=adj, entry=entry[:L], dead=dead[:N])
 
-    def import_graph(self, keys, vecs, deg, adj, entry):
+    def delete(self, keys, mode=0, heuristic=1, keep_pruned=0):
+        """Graph.BatchDelete (graph.go:868-895); mode 0 = the reference's
+        isolate/replenish, 1 = the engine's batched-graph repair."""
+        keys = np.ascontiguousarray(np.atleast_1d(keys), np.int64)
+        out = np.zeros(max(len(keys), 1), np.uint8)
+        self._check(lib().og_delete(self._h, _p(keys, C.c_int64), len(keys), mode, heuristic, keep_pruned,
+                                    _p(out, C.c_uint8)))
+        return [bool(x) for x in out[:len(keys)]]
+
+    def import_graph(self, keys, vecs, deg, adj, entry, dead=None):
         keys = np.ascontiguousarray(keys, np.int64)
         vecs = f32(vecs)
         deg = np.ascontiguousarray(deg, np.int32)
         adj = np.ascontiguousarray(adj, np.int32)
         entry = np.ascontiguousarray(entry, np.int32)
+        dd = None if dead is None else np.ascontiguousarray(dead, np.uint8)
         L, N = deg.shape
         cap = adj.shape[2]
         self._check(lib().og_import(self._h, N, vecs.shape[1] if vecs.ndim == 2 else 1, L, cap,
                                     _p(keys, C.c_int64), _p(vecs, C.c_float), _p(deg, C.c_int32),
-                                    _p(adj, C.c_int32), _p(entry, C.c_int32)))
+                                    _p(adj, C.c_int32), _p(entry, C.c_int32),
+                                    None if dd is None else _p(dd, C.c_uint8)))
 
     def stats(self):
         o = np.zeros(4, np.int64)

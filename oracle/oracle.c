@@ -255,6 +255,7 @@ struct og_graph {
     int64_t *keys;
     float *vecs;
     float *norms;
+    uint8_t *dead; /* [cap_nodes] 1 = deleted (graph.go:843-864); rows stay for dangling edges */
     int nlayers;
     og_layer *layers;
     /* key -> id hash (open addressing, linear probe) */
@@ -281,12 +282,26 @@ static uint64_t hmix(int64_t k) {
     return z ^ (z >> 29);
 }
 
+/* slot values: -1 empty, -2 tombstone (deleted key), >= 0 id */
 static int32_t hget(og_graph *g, int64_t key) {
     if (!g->hcap) return -1;
     uint64_t m = (uint64_t)g->hcap - 1, h = hmix(key) & m;
     for (;;) {
-        if (g->hvals[h] < 0) return -1;
-        if (g->hkeys[h] == key) return g->hvals[h];
+        if (g->hvals[h] == -1) return -1;
+        if (g->hvals[h] >= 0 && g->hkeys[h] == key) return g->hvals[h];
+        h = (h + 1) & m;
+    }
+}
+
+static void hdel(og_graph *g, int64_t key) {
+    if (!g->hcap) return;
+    uint64_t m = (uint64_t)g->hcap - 1, h = hmix(key) & m;
+    for (;;) {
+        if (g->hvals[h] == -1) return;
+        if (g->hvals[h] >= 0 && g->hkeys[h] == key) {
+            g->hvals[h] = -2;
+            return;
+        }
         h = (h + 1) & m;
     }
 }
@@ -348,6 +363,7 @@ void og_destroy(og_graph *g) {
     free(g->keys);
     free(g->vecs);
     free(g->norms);
+    free(g->dead);
     free(g->hkeys);
     free(g->hvals);
     free(g->scr.visited);
@@ -398,6 +414,10 @@ static int ensure_nodes(og_graph *g, int64_t need) {
     float *nn = (float *)realloc(g->norms, sizeof(float) * (size_t)nc);
     if (!nn) return -1;
     g->norms = nn;
+    uint8_t *dd = (uint8_t *)realloc(g->dead, (size_t)nc);
+    if (!dd) return -1;
+    for (int64_t i = g->cap_nodes; i < nc; ++i) dd[i] = 0;
+    g->dead = dd;
     uint32_t *vis = (uint32_t *)realloc(g->scr.visited, sizeof(uint32_t) * (size_t)nc);
     if (!vis) return -1;
     for (int64_t i = g->cap_nodes; i < nc; ++i) vis[i] = 0;
@@ -456,6 +476,19 @@ static inline uint32_t next_stamp(og_scratch *s, int64_t n) {
 }
 
 static inline const float *vec_of(const og_graph *g, int32_t id) { return g->vecs + (size_t)id * (size_t)g->dim; }
+
+/* `layer.nodes[key]` is non-nil: present in the layer and not deleted */
+static inline int member(const og_graph *g, int l, int32_t id) {
+    return id >= 0 && l >= 0 && l < g->nlayers && g->layers[l].deg[id] != -2 && !g->dead[id];
+}
+
+/* highest layer with a live node (empty top layers are skipped by Search:
+ * entry() == nil -> search() == nil -> continue, graph.go:572-582) */
+static int top_live_layer(const og_graph *g) {
+    int top = g->nlayers - 1;
+    while (top > 0 && g->layers[top].count == 0) --top;
+    return top;
+}
 
 /* distance(node, target) as used by search (graph.go:112, 146) */
 static inline float dist_q(const og_graph *g, int32_t id, const float *q, float qn) {
@@ -770,7 +803,9 @@ int og_add(og_graph *g, const int64_t *keys, const float *vecs, int64_t n, int d
                 L->entry = id;
                 continue;
             }
-            int32_t sp = elevator >= 0 ? elevator : L->entry; /* graph.go:492-498 */
+            /* graph.go:492-498: layer.nodes[*elevator] is nil once the elevator
+             * node was deleted -> search(nil) -> error below */
+            int32_t sp = elevator >= 0 ? (member(g, l, elevator) ? elevator : -1) : L->entry;
             int cnt = compat_layer_search(g, &g->scr, l, sp, g->M, g->ef, vec, qn, nbh, nbd, &g->stats[2],
                                           &g->stats[3]); /* graph.go:500 */
             if (cnt == 0) {
@@ -794,6 +829,133 @@ int og_add(og_graph *g, const int64_t *keys, const float *vecs, int64_t n, int d
     return OG_OK;
 }
 
+/* ---- graph.go:843-895 Delete / BatchDelete ----------------------------- */
+
+/* graph.go:221-235 isolate: for each neighbour (ascending key = the map-order
+ * stand-in) drop the backlink and replenish the neighbour.  The deleted
+ * node's own map is left intact (the reference keeps the layerNode alive
+ * behind one-directional edges), and replenish may even re-link it. */
+static void isolate(og_graph *g, int l, int32_t n, int m) {
+    og_layer *L = &g->layers[l];
+    if (L->deg[n] < 0) return; /* nil neighbor map */
+    int32_t *nb = (int32_t *)malloc(sizeof(int32_t) * (size_t)g->acap);
+    int d = sorted_neighbors(g, L, n, nb);
+    for (int j = 0; j < d; ++j) {
+        int32_t x = nb[j];
+        if (L->deg[x] < 0) continue; /* neighbor.neighbors == nil */
+        list_remove(L, g->acap, x, n);
+        replenish(g, l, x, m);
+    }
+    free(nb);
+}
+
+typedef struct {
+    float d;
+    int32_t id;
+} rp_t;
+static int rp_cmp(const void *a, const void *b) {
+    const rp_t *x = (const rp_t *)a, *y = (const rp_t *)b;
+    if (blt(x->d, x->id, y->d, y->id)) return -1;
+    if (blt(y->d, y->id, x->d, x->id)) return 1;
+    return 0;
+}
+
+/* Batched-graph repair (engine semantics, k_delete_repair): every live row of
+ * layer l that points at a deleted node is rebuilt from its live neighbours
+ * plus the neighbours of its deleted neighbours (gather order: row order,
+ * capped at OG_REPAIR_POOL), ranked by (distance, id) and selected like the
+ * batched insert (HNSW diversity heuristic, optional keep-pruned fill).  Rows
+ * of deleted nodes are read, never written, so rows are independent. */
+#define OG_REPAIR_POOL 256
+static void repair_layer(og_graph *g, int l, int mcap, int heuristic, int keep_pruned) {
+    og_layer *L = &g->layers[l];
+    rp_t *pool = (rp_t *)malloc(sizeof(rp_t) * OG_REPAIR_POOL);
+    int32_t *sel = (int32_t *)malloc(sizeof(int32_t) * (size_t)g->acap);
+    for (int64_t v = 0; v < g->n; ++v) {
+        int d = L->deg[v];
+        if (g->dead[v] || d <= 0) continue;
+        const int32_t *row = L->adj + (size_t)v * g->acap;
+        int hit = 0;
+        for (int j = 0; j < d; ++j) hit |= g->dead[row[j]];
+        if (!hit) continue;
+        int np = 0;
+        for (int j = 0; j < d && np < OG_REPAIR_POOL; ++j)
+            if (!g->dead[row[j]]) pool[np++].id = row[j];
+        for (int j = 0; j < d; ++j) {
+            int32_t x = row[j];
+            if (!g->dead[x] || L->deg[x] <= 0) continue;
+            const int32_t *xr = L->adj + (size_t)x * g->acap;
+            for (int t = 0; t < L->deg[x] && np < OG_REPAIR_POOL; ++t)
+                if (xr[t] != (int32_t)v && !g->dead[xr[t]]) pool[np++].id = xr[t];
+        }
+        for (int i = 0; i < np; ++i) {
+            float dd = dist_nodes(g, pool[i].id, (int32_t)v, g->metric);
+            pool[i].d = dd != dd ? INFINITY : dd; /* NaN (zero vectors) ranks last */
+            g->stats[2]++;
+        }
+        qsort(pool, (size_t)np, sizeof(rp_t), rp_cmp);
+        int ns = 0;
+        for (int i = 0; i < np && ns < mcap; ++i) {
+            if (i > 0 && pool[i].id == pool[i - 1].id) continue;
+            int good = 1;
+            if (heuristic && ns > 0)
+                for (int s2 = 0; s2 < ns; ++s2) {
+                    g->stats[2]++;
+                    if (dist_nodes(g, sel[s2], pool[i].id, g->metric) < pool[i].d) good = 0;
+                }
+            if (good) sel[ns++] = pool[i].id;
+        }
+        if (keep_pruned)
+            for (int i = 0; i < np && ns < mcap; ++i) {
+                if (i > 0 && pool[i].id == pool[i - 1].id) continue;
+                int have = 0;
+                for (int s2 = 0; s2 < ns; ++s2) have |= sel[s2] == pool[i].id;
+                if (!have) sel[ns++] = pool[i].id;
+            }
+        int32_t *w = L->adj + (size_t)v * g->acap;
+        for (int i = 0; i < ns; ++i) w[i] = sel[i];
+        L->deg[v] = ns;
+    }
+    free(pool);
+    free(sel);
+}
+
+/* lowest-id live member, the deterministic stand-in for entry() (graph.go:250-258) */
+static void fix_entries(og_graph *g) {
+    for (int l = 0; l < g->nlayers; ++l) {
+        og_layer *L = &g->layers[l];
+        if (member(g, l, L->entry)) continue;
+        L->entry = -1;
+        for (int64_t i = 0; i < g->n; ++i)
+            if (member(g, l, (int32_t)i)) {
+                L->entry = (int32_t)i;
+                break;
+            }
+    }
+}
+
+int og_delete(og_graph *g, const int64_t *keys, int64_t n, int mode, int heuristic, int keep_pruned, uint8_t *out) {
+    int any = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        int32_t id = hget(g, keys[i]);
+        out[i] = 0;
+        if (id < 0 || g->nlayers == 0) continue;
+        hdel(g, keys[i]);
+        g->dead[id] = 1;
+        any = 1;
+        for (int l = 0; l < g->nlayers; ++l) { /* graph.go:852-861 */
+            if (g->layers[l].deg[id] == -2) continue;
+            g->layers[l].count--;
+            out[i] = 1;
+            if (mode == 0) isolate(g, l, id, g->M); /* cap M on every layer (Q13) */
+        }
+    }
+    if (any && mode == 1)
+        for (int l = 0; l < g->nlayers; ++l) repair_layer(g, l, l == 0 ? g->M0 : g->M, heuristic, keep_pruned);
+    if (any) fix_entries(g);
+    return OG_OK;
+}
+
 /* one query of Graph.Search (graph.go:534-625) / BatchSearch loop body
  * (graph.go:1076-1106), compat or beam, or exact brute force */
 typedef struct {
@@ -806,12 +968,12 @@ typedef struct {
 static int search_one(og_graph *g, og_scratch *s, qbuf *qb, const float *q, int dim, int k, int mode, int ef,
                       int32_t entry, int64_t *ok, float *odd) {
     float qn = og_dev_norm(q, dim);
-    int top = g->nlayers - 1;
+    int top = top_live_layer(g);
     if (mode == OG_MODE_EXACT) {
         int n = 0;
         og_layer *L0 = &g->layers[0];
         for (int32_t v = 0; v < (int32_t)g->n; ++v) {
-            if (L0->deg[v] == -2) continue;
+            if (L0->deg[v] == -2 || g->dead[v]) continue;
             beam_insert(qb->lst, &n, k, dist_q(g, v, q, qn), v);
             qb->st[0]++;
         }
@@ -824,7 +986,10 @@ static int search_one(og_graph *g, og_scratch *s, qbuf *qb, const float *q, int 
     if (mode == OG_MODE_COMPAT) {
         int32_t elevator = -1;
         for (int l = top; l >= 0; --l) { /* graph.go:571-622 */
-            int32_t p = elevator >= 0 ? elevator : (l == top ? entry : g->layers[l].entry);
+            /* searchPoint = layers[l].entry() (nil when empty), or
+             * layers[l].nodes[*elevator] (nil when that node was deleted) */
+            int32_t p = elevator >= 0 ? (member(g, l, elevator) ? elevator : -1)
+                                      : (l == top ? entry : (g->layers[l].count > 0 ? g->layers[l].entry : -1));
             if (l > 0) {
                 int c = compat_layer_search(g, s, l, p, 1, ef, q, qn, qb->ids, qb->ds, &qb->st[0], &qb->st[1]);
                 if (c == 0) continue;
@@ -843,14 +1008,19 @@ static int search_one(og_graph *g, og_scratch *s, qbuf *qb, const float *q, int 
     int efl = ef > k ? ef : k;
     int32_t p = entry;
     for (int l = top; l >= 1; --l) {
+        if (g->layers[l].deg[p] == -2) p = g->layers[l].entry; /* not a member of this layer */
         int c = beam_layer_search(g, s, l, p, 1, q, qn, qb->lst, &qb->st[0], &qb->st[1]);
         if (c > 0) p = qb->lst[0].id;
     }
+    if (g->layers[0].deg[p] == -2) p = g->layers[0].entry;
     int c = beam_layer_search(g, s, 0, p, efl, q, qn, qb->lst, &qb->st[0], &qb->st[1]);
-    int nout = c < k ? c : k;
-    for (int i = 0; i < nout; ++i) {
-        ok[i] = g->keys[qb->lst[i].id];
-        odd[i] = qb->lst[i].d;
+    /* deleted rows still route the search (their edges stay) but are not returned */
+    int nout = 0;
+    for (int i = 0; i < c && nout < k; ++i) {
+        if (g->dead[qb->lst[i].id]) continue;
+        ok[nout] = g->keys[qb->lst[i].id];
+        odd[nout] = qb->lst[i].d;
+        ++nout;
     }
     return nout;
 }
@@ -867,11 +1037,11 @@ static int search_prologue(og_graph *g, int64_t B, int dim, int k, const int64_t
     for (int64_t b = 0; b < B; ++b) out_n[b] = 0;
     *entry = -1;
     if (!g->layers_exist || og_len(g) == 0) return 1; /* graph.go:554-556: nil, nil */
-    int top = g->nlayers - 1;
+    int top = top_live_layer(g);
     *entry = g->layers[top].entry;
     if (entry_key) {
         int32_t e = hget(g, *entry_key);
-        if (e < 0 || g->layers[top].deg[e] == -2)
+        if (e < 0 || !member(g, top, e))
             return set_err(g, OG_EINVAL, "entry key %lld not in top layer", (long long)*entry_key);
         *entry = e;
     }
@@ -985,7 +1155,8 @@ int og_export_sizes(og_graph *g, int64_t *N, int *dim, int *L, int *cap) {
     return OG_OK;
 }
 
-int og_export(og_graph *g, int64_t *keys, float *vecs, int32_t *deg, int32_t *adj, int cap, int32_t *entry) {
+int og_export(og_graph *g, int64_t *keys, float *vecs, int32_t *deg, int32_t *adj, int cap, int32_t *entry,
+              uint8_t *dead) {
     if (cap < g->acap) {
         for (int l = 0; l < g->nlayers; ++l)
             for (int64_t i = 0; i < g->n; ++i)
@@ -993,6 +1164,7 @@ int og_export(og_graph *g, int64_t *keys, float *vecs, int32_t *deg, int32_t *ad
     }
     memcpy(keys, g->keys, sizeof(int64_t) * (size_t)g->n);
     memcpy(vecs, g->vecs, sizeof(float) * (size_t)g->n * (size_t)g->dim);
+    if (dead) memcpy(dead, g->dead, (size_t)g->n);
     for (int l = 0; l < g->nlayers; ++l) {
         og_layer *L = &g->layers[l];
         entry[l] = L->entry;
@@ -1007,11 +1179,13 @@ int og_export(og_graph *g, int64_t *keys, float *vecs, int32_t *deg, int32_t *ad
 }
 
 int og_import(og_graph *g, int64_t N, int dim, int L, int cap, const int64_t *keys, const float *vecs,
-              const int32_t *deg, const int32_t *adj, const int32_t *entry) {
+              const int32_t *deg, const int32_t *adj, const int32_t *entry, const uint8_t *dead) {
     free_layers(g);
     free(g->keys);
     free(g->vecs);
     free(g->norms);
+    free(g->dead);
+    g->dead = NULL;
     free(g->scr.visited);
     free(g->hkeys);
     free(g->hvals);
@@ -1036,7 +1210,8 @@ int og_import(og_graph *g, int64_t N, int dim, int L, int cap, const int64_t *ke
     g->n = N;
     for (int64_t i = 0; i < N; ++i) {
         g->norms[i] = og_dev_norm(vecs + (size_t)i * dim, dim);
-        if (hget(g, keys[i]) < 0) hput(g, keys[i], (int32_t)i);
+        g->dead[i] = dead ? dead[i] : 0;
+        if (!g->dead[i] && hget(g, keys[i]) < 0) hput(g, keys[i], (int32_t)i);
     }
     for (int l = 0; l < L; ++l) {
         og_layer *Ly = &g->layers[l];
@@ -1045,7 +1220,7 @@ int og_import(og_graph *g, int64_t N, int dim, int L, int cap, const int64_t *ke
         for (int64_t i = 0; i < N; ++i) {
             int d = deg[(size_t)l * N + i];
             Ly->deg[i] = d;
-            if (d != -2) Ly->count++;
+            if (d != -2 && !g->dead[i]) Ly->count++;
             for (int j = 0; j < d; ++j) Ly->adj[(size_t)i * g->acap + j] = adj[((size_t)l * N + i) * cap + j];
         }
     }

@@ -17,6 +17,7 @@
  *   graph.go:370-417         maxLevel / randomLevel      (RNG made injectable)
  *   graph.go:437-531         Graph.Add
  *   graph.go:534-625         Graph.Search
+ *   graph.go:221-235, 843-895 isolate / Delete / BatchDelete
  *   graph.go:916-937         Graph.Validate
  *   graph.go:1047-1110       Graph.BatchSearch
  *   parquet/graph.go:924-1076, arrow/graph.go:576-659   beam-search precedent
@@ -105,14 +106,21 @@ int og_search_mt(og_graph *g, const float *queries, int64_t B, int dim, int k, i
 int og_layer_search_compat(og_graph *g, int layer, int32_t entry_id, int k, int ef,
                            const float *q, int32_t *out_ids, float *out_d);
 
+/* Graph.Delete / BatchDelete (graph.go:843-895).  mode 0: the reference's
+ * isolate + replenish per key (graph.go:172-235); mode 1: the engine's
+ * batched-graph repair (see oracle.c repair_layer).  out[i] = 1 if deleted. */
+int og_delete(og_graph *g, const int64_t *keys, int64_t n, int mode, int heuristic, int keep_pruned,
+              uint8_t *out);
+
 /* ---- graph exchange (same format as mhnsw_export/mhnsw_import) ----
  * keys[N], vecs[N*dim], per layer: deg[N] (-2 absent, -1 nil map, >=0),
- * adj[N*cap] (internal ids), entry[L]. */
+ * adj[N*cap] (internal ids), entry[L], dead[N] (nullable). */
 int og_export_sizes(og_graph *g, int64_t *N, int *dim, int *L, int *cap);
 int og_export(og_graph *g, int64_t *keys, float *vecs, int32_t *deg, int32_t *adj, int cap,
-              int32_t *entry);
+              int32_t *entry, uint8_t *dead);
 int og_import(og_graph *g, int64_t N, int dim, int L, int cap, const int64_t *keys,
-              const float *vecs, const int32_t *deg, const int32_t *adj, const int32_t *entry);
+              const float *vecs, const int32_t *deg, const int32_t *adj, const int32_t *entry,
+              const uint8_t *dead);
 
 /* counters: [0]=distance evals (search), [1]=expansions (search),
  * [2]=distance evals (build), [3]=expansions (build) */

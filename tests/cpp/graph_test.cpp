@@ -41,7 +41,7 @@ static void Test_layerNode_search() {
     for (int& a : adj) a = -1;
     adj[0] = 1, adj[1] = 2, adj[2] = 3, adj[3 * 7 + 0] = 4, adj[3 * 7 + 1] = 5;
     const int32_t entry[1] = {0};
-    REQUIRE(mhnsw_import(g.handle(), 6, 1, 1, 7, keys, vals, deg, adj, entry) == 0, "Test_layerNode_search import");
+    REQUIRE(mhnsw_import(g.handle(), 6, 1, 1, 7, keys, vals, deg, adj, entry, nullptr) == 0, "Test_layerNode_search import");
     auto r = g.Search({4}, 2);
     REQUIRE(!r.second, "Test_layerNode_search err");
     REQUIRE(r.first.size() == 2 && r.first[0].Key == 5 && r.first[1].Key == 3, "Test_layerNode_search keys");
@@ -110,6 +110,44 @@ static void TestDimensionMismatch() {
     REQUIRE(g->Len() == 1 && g->Dims() == 3, "Len/Dims");
 }
 
+// batch_delete_test.go:10-105 TestBatchDelete
+static void TestBatchDelete() {
+    auto cfg = hnsw::NewGraphWithConfig<int>(16, 0.25, 20, &hnsw::CosineDistance, 5);
+    REQUIRE(!cfg.second, "NewGraphWithConfig");
+    auto& g = *cfg.first;
+    for (int i = 1; i <= 10; ++i) g.Add(hnsw::MakeNode(i, {(float)i, (float)i, (float)i}));
+    REQUIRE(g.Len() == 10, "initial size");
+    auto r = g.BatchDelete({1, 3, 5});
+    REQUIRE(r == std::vector<bool>({true, true, true}), "delete existing");
+    REQUIRE(g.Len() == 7, "size after delete");
+    for (int k : {1, 3, 5}) REQUIRE(!g.Lookup(k).second, "deleted lookup");
+    for (int k : {2, 4, 6, 7, 8, 9, 10}) REQUIRE(g.Lookup(k).second, "kept lookup");
+    r = g.BatchDelete({11, 12, 13});
+    REQUIRE(r == std::vector<bool>({false, false, false}), "delete missing");
+    REQUIRE(g.Len() == 7, "size unchanged");
+    r = g.BatchDelete({2, 15, 4, 20});
+    REQUIRE(r == std::vector<bool>({true, false, true, false}), "delete mixed");
+    REQUIRE(g.Len() == 5, "size after mixed");
+    REQUIRE(g.BatchDelete({}).empty(), "delete empty");
+    r = g.BatchDelete({6, 7, 8, 9, 10});
+    REQUIRE(r == std::vector<bool>({true, true, true, true, true}), "delete rest");
+    REQUIRE(g.Len() == 0, "empty graph");
+    auto s = g.Search({1, 1, 1}, 3);
+    REQUIRE(!s.second && s.first.empty(), "search on emptied graph");
+}
+
+// graph_test.go:135-172 TestGraph_AddDelete (levels from this engine's RNG)
+static void TestGraph_AddDelete() {
+    hnsw::Graph<int> g(6, 0.5, 20, &hnsw::EuclideanDistance, 0);
+    for (int i = 0; i < 128; ++i) REQUIRE(!g.Add(hnsw::MakeNode(i, {(float)i})), "add");
+    REQUIRE(g.Len() == 128, "len 128");
+    for (int i = 0; i < 128; i += 2) REQUIRE(g.Delete(i), "delete even");
+    REQUIRE(g.Len() == 64, "len 64");
+    REQUIRE(!g.Delete(-1), "DeleteNotFound");
+    auto s = g.Search({65.f}, 4);
+    REQUIRE(!s.second, "search after delete");
+}
+
 int main() {
     TestDistances();
     Test_layerNode_search();
@@ -117,6 +155,8 @@ int main() {
     TestGraph_DefaultCosine();
     TestGraphValidation();
     TestDimensionMismatch();
+    TestBatchDelete();
+    TestGraph_AddDelete();
     std::printf("%s (%d failures)\n", failures ? "FAIL" : "PASS", failures);
     return failures;
 }

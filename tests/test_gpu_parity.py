@@ -45,6 +45,8 @@ def _same_graph(a, b):
             if d > 0:
                 assert set(a["adj"][l, i, :d].tolist()) == set(b["adj"][l, i, :d].tolist()), (l, i)
     assert np.array_equal(a["entry"], b["entry"])
+    if "dead" in a and "dead" in b:
+        assert np.array_equal(a["dead"], b["dead"])
 
 
 def _same_results(gk, gd, gn, rk, rd, rn, bitwise=True):
@@ -316,3 +318,146 @@ def test_batch_build_recall_and_exact_parity(H, O, metric):
     _same_results(ek, ed, en, rk, rd, rn)
     rk, rd, rn = o.search(Q, 10, mode=O.MODE_BEAM, ef=64)
     _same_results(bk, bd, bn, rk, rd, rn)
+
+
+# ---------------------------------------------------------------- Delete (graph.go:843-895)
+def _live_connectivity(ex):
+    out = []
+    for l in range(ex["deg"].shape[0]):
+        live = (ex["deg"][l] != -2) & (ex["dead"] == 0)
+        if live.sum():
+            out.append(float(np.maximum(ex["deg"][l][live], 0).sum()) / float(live.sum()))
+    return out
+
+
+def _search_parity(H, O, g, o, Q, k=10, efs=(20, 64)):
+    for mode in (H.MODE_COMPAT, H.MODE_BEAM, H.MODE_EXACT):
+        for ef in efs:
+            gk, gd, gn = g.search_arrays(Q, k, mode=mode, ef=ef)
+            rk, rd, rn = o.search(Q, k, mode=mode, ef=ef)
+            _same_results(gk, gd, gn, rk, rd, rn)
+
+
+@pytest.mark.parametrize("metric,M,ml,d", [(0, 8, 0.25, 24), (1, 6, 0.5, 3), (0, 16, 0.25, 768)])
+def test_compat_delete_parity(H, O, metric, M, ml, d):
+    """Delete/BatchDelete with the reference's isolate + replenish: identical
+    graphs (rows, dead flags, entries), Len/Topography/Connectivity, and
+    identical compat/beam/exact results afterwards; then more Adds."""
+    rng = np.random.default_rng(21 + d)
+    n = 700
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    Q = rng.uniform(-1, 1, (48, d)).astype(np.float32)
+    keys = np.arange(n, dtype=np.int64) * 3 - 500
+    lv = _levels(O, metric, M, ml, 20, 31, n)
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=ml, EfSearch=20)
+    g = H.Graph(M=M, Ml=ml, EfSearch=20, Distance=_metric_fn(H, metric))
+    o.add(keys, X, lv)
+    g.add_arrays(keys, X, levels=lv)
+    gone = [int(x) for x in rng.choice(keys, 180, replace=False)]
+    gone += gone[:3] + [123457]  # repeats and a missing key -> False
+    ro = o.delete(gone)
+    rg = g.BatchDelete(gone)
+    assert ro == rg and rg[-4:] == [False] * 4
+    ex = g.export()
+    _same_graph(ex, o.export())
+    assert g.Len() == len(o) == n - 180 and g.Topography() == o.topography()
+    assert g.Connectivity() == _live_connectivity(ex)
+    assert all(g.Lookup(k) == (None, False) for k in gone[:5])
+    _search_parity(H, O, g, o, Q)
+    # Adds after deletes (levels drawn from the live Len, graph.go:400).  A
+    # deleted node reached through a dangling edge can become the elevator, and
+    # the reference's Add then fails (graph.go:489-505); both sides must agree.
+    lv2 = o.preview_levels(40)
+    assert np.array_equal(lv2, g.preview_levels(40))
+    _adds_agree(H, O, g, o, rng.uniform(-1, 1, (40, d)).astype(np.float32), 10**6, Q)
+
+
+def _adds_agree(H, O, g, o, X2, key0, Q):
+    """Add rows one at a time on both sides; identical graphs and results after
+    each, or the same reference error on the same row (state after a failed
+    Add is unspecified, so the walk stops there).  Returns rows added."""
+    for i in range(len(X2)):
+        lvl = o.preview_levels(1)
+        oe = ge = None
+        try:
+            o.add([key0 + i], X2[i:i + 1], lvl)
+        except O.OracleError as e:
+            oe = str(e)
+        try:
+            g.add_arrays(np.array([key0 + i]), X2[i:i + 1], levels=lvl)
+        except H.HnswError as e:
+            ge = str(e)
+        assert (oe is None) == (ge is None), (i, oe, ge)
+        if oe is not None:
+            assert "no nodes found in neighborhood search" in oe and "no nodes found in neighborhood search" in ge
+            return i
+        if i % 8 == 0 or i == len(X2) - 1:
+            _same_graph(g.export(), o.export())
+            _search_parity(H, O, g, o, Q, efs=(20,))
+    return len(X2)
+
+
+def test_compat_delete_top_layer_then_add(H, O):
+    """Deleting every node of the top layers empties them; the next Add is
+    taken by the emptied layers whatever its level (graph.go:485-488), and a
+    later Add whose elevator is not in the layer below fails with the
+    reference's "no nodes found in neighborhood search" (graph.go:500-505).
+    Adds go one at a time so both sides hold identical graphs up to the first
+    error."""
+    rng = np.random.default_rng(9)
+    n, d, M = 400, 8, 6
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    lv = _levels(O, 0, M, 0.25, 20, 13, n)
+    o = O.Graph(metric=0, order=O.ORDER_DEV, M=M, Ml=0.25, EfSearch=20)
+    g = H.Graph(M=M, Ml=0.25, EfSearch=20)
+    o.add(np.arange(n), X, lv)
+    g.add_arrays(np.arange(n), X, levels=lv)
+    top = int(lv.max())
+    gone = [int(i) for i in np.flatnonzero(lv >= max(top - 1, 1))]
+    assert o.delete(gone) == g.BatchDelete(gone) == [True] * len(gone)
+    _same_graph(g.export(), o.export())
+    Q = rng.uniform(-1, 1, (16, d)).astype(np.float32)
+    _search_parity(H, O, g, o, Q, efs=(20,))
+    added = _adds_agree(H, O, g, o, rng.uniform(-1, 1, (30, d)).astype(np.float32), n, Q)
+    assert added >= 1 and o.topography()[top] >= 1  # the emptied top layer was taken by a new node
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_batch_delete_repair_parity(H, O, metric):
+    """Batched-graph repair (k_delete_repair) == oracle repair_layer on the same
+    graph; deleted keys never come back; recall holds; Adds continue."""
+    rng = np.random.default_rng(40 + metric)
+    n, d = 6000, 48
+    X = _clustered(rng, n, d)
+    Q = _clustered(rng, 200, d)
+    g = H.Graph(M=12, Ml=0.25, EfSearch=64, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
+                m0=24, ef_construction=64, heuristic=2, keep_pruned=1)
+    g.add_arrays(np.arange(n), X)
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=12, M0=24, Ml=0.25, EfSearch=64)
+    o.import_graph(**g.export())
+    ex0 = g.export()
+    top = ex0["deg"].shape[0] - 1
+    gone = [int(ex0["keys"][ex0["entry"][top]])] + [int(x) for x in rng.permutation(n)[:900]]
+    gone = list(dict.fromkeys(gone))
+    assert g.BatchDelete(gone) == o.delete(gone, mode=1, heuristic=2, keep_pruned=1) == [True] * len(gone)
+    ex = g.export()
+    _same_graph(ex, o.export())
+    dead = ex["dead"].astype(bool)
+    for l in range(ex["deg"].shape[0]):
+        rows = np.flatnonzero(~dead & (ex["deg"][l] > 0))
+        for i in rows:
+            assert not dead[ex["adj"][l, i, : ex["deg"][l, i]]].any()
+    ek, ed, en = g.search_arrays(Q, 10, mode=H.MODE_EXACT)
+    rk, rd, rn = o.search(Q, 10, mode=O.MODE_EXACT)
+    _same_results(ek, ed, en, rk, rd, rn)
+    bk, bd, bn = g.search_arrays(Q, 10, mode=H.MODE_BEAM, ef=64)
+    rk, rd, rn = o.search(Q, 10, mode=O.MODE_BEAM, ef=64)
+    _same_results(bk, bd, bn, rk, rd, rn)
+    assert not set(bk[bn > 0].ravel().tolist()) & set(gone)
+    r = np.mean([len(set(bk[b, : bn[b]]) & set(ek[b, : en[b]])) / 10 for b in range(len(Q))])
+    assert r >= 0.85, r
+    X2 = _clustered(rng, 1000, d)
+    g.add_arrays(np.arange(n, n + 1000), X2)
+    assert g.Len() == n - len(gone) + 1000
+    ek, _, en = g.search_arrays(X2[:50], 1, mode=H.MODE_BEAM, ef=64)
+    assert np.mean(ek[:, 0] == np.arange(n, n + 50)) >= 0.9

@@ -179,3 +179,108 @@ def test_beam_recall_dominates_compat(O):
 
     assert recall(bk, bn) > recall(ck, cn)
     assert recall(bk, bn) > 0.9
+
+
+# ----------------------------------------------------------------- Delete
+def _live_connectivity(ex):
+    """Analyzer.Connectivity (analyzer.go:20-38) from an export: mean
+    len(neighbors) over the live members of each non-empty layer."""
+    out = []
+    for l in range(ex["deg"].shape[0]):
+        live = (ex["deg"][l] != -2) & (ex["dead"] == 0)
+        if live.sum() == 0:
+            continue
+        out.append(float(np.maximum(ex["deg"][l][live], 0).sum()) / float(live.sum()))
+    return out
+
+
+def test_batch_delete_semantics(O):
+    """batch_delete_test.go:10-105 TestBatchDelete on the restatement."""
+    g = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=16, Ml=0.25, EfSearch=20, seed=5)
+    g.add(np.arange(1, 11), np.repeat(np.arange(1, 11, dtype=np.float32)[:, None], 3, axis=1))
+    assert len(g) == 10
+    assert g.delete([1, 3, 5]) == [True, True, True] and len(g) == 7
+    assert g.delete([11, 12, 13]) == [False, False, False] and len(g) == 7
+    assert g.delete([2, 15, 4, 20]) == [True, False, True, False] and len(g) == 5
+    assert g.delete([]) == [] and len(g) == 5
+    k, d, n = g.search(np.ones((1, 3), np.float32), 10, mode=O.MODE_EXACT)
+    assert sorted(k[0, : n[0]].tolist()) == [6, 7, 8, 9, 10]
+    assert g.delete([6, 7, 8, 9, 10]) == [True] * 5 and len(g) == 0
+    k, d, n = g.search(np.ones((1, 3), np.float32), 3)
+    assert n[0] == 0
+    assert g.delete([6]) == [False]  # already gone, also within one batch
+    g.add([6], np.ones((1, 3), np.float32))  # a deleted key can be added again
+    assert len(g) == 1
+
+
+def test_add_delete_connectivity(O):
+    """graph_test.go:135-172 TestGraph_AddDelete: 128 1-D nodes (newTestGraph:
+    M=6, Ml=0.5, Euclidean), delete every even key -> Len 64, Delete(-1) false.
+    The reference also asserts layer-0 connectivity is unchanged; that equality
+    holds for Go's seed-0 level stream, which cannot be regenerated here, so the
+    restatement checks it is preserved within one edge per node."""
+    g = O.Graph(metric=O.EUCLIDEAN, order=O.ORDER_DEV, M=6, Ml=0.5, EfSearch=20, seed=0)
+    g.add(np.arange(128), np.arange(128, dtype=np.float32)[:, None])
+    pre = _live_connectivity(g.export())
+    assert all(g.delete([i]) == [True] for i in range(0, 128, 2))
+    assert len(g) == 64
+    post = _live_connectivity(g.export())
+    assert abs(pre[0] - post[0]) <= 1.0, (pre, post)
+    assert g.delete([-1]) == [False]
+
+
+def test_compat_delete_keeps_reference_quirks(O):
+    """isolate/replenish (graph.go:172-235): the deleted row keeps its edges;
+    exact and beam never return deleted keys; compat search may still reach them
+    through one-directional edges, as the reference does."""
+    rng = np.random.default_rng(4)
+    n, d = 600, 16
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    g = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=8, Ml=0.25, EfSearch=20, seed=3)
+    g.add(np.arange(n), X)
+    gone = rng.permutation(n)[:120]
+    last = int(gone[-1])
+    assert all(g.delete(gone[:-1]))
+    before = g.export()
+    assert g.delete([last]) == [True]
+    ex = g.export()
+    assert ex["dead"][gone].all() and ex["dead"].sum() == 120
+    for l in range(ex["deg"].shape[0]):  # isolate leaves the deleted node's own map intact
+        assert ex["deg"][l, last] == before["deg"][l, last]
+        dl = ex["deg"][l, last]
+        assert set(ex["adj"][l, last, :dl]) == set(before["adj"][l, last, :dl])
+    assert all(e < 0 or not ex["dead"][e] for e in ex["entry"])
+    Q = rng.uniform(-1, 1, (50, d)).astype(np.float32)
+    for mode in (O.MODE_EXACT, O.MODE_BEAM):
+        k, _, nn = g.search(Q, 10, mode=mode, ef=40)
+        assert not set(k[nn > 0].ravel().tolist()) & set(gone.tolist())
+    assert len(g) == n - 120 and sum(g.topography()[:1]) == n - 120
+
+
+def test_batch_repair_removes_dead_edges(O):
+    """Engine repair mode: no live row keeps an edge to a deleted node, degrees
+    stay within the cap, and beam recall against the live exact set holds."""
+    rng = np.random.default_rng(6)
+    n, d = 2000, 12
+    X = rng.normal(size=(n, d)).astype(np.float32)
+    Q = rng.normal(size=(100, d)).astype(np.float32)
+    g = O.Graph(metric=O.EUCLIDEAN, order=O.ORDER_DEV, M=16, M0=32, Ml=0.25, EfSearch=40, seed=2)
+    g.add(np.arange(n), X)  # compat-built graph, repaired with the batched rule
+
+    def recall():
+        ek, _, en = g.search(Q, 10, mode=O.MODE_EXACT)
+        bk, _, bn = g.search(Q, 10, mode=O.MODE_BEAM, ef=80)
+        return np.mean([len(set(bk[b, : bn[b]]) & set(ek[b, : en[b]])) / 10 for b in range(len(Q))])
+
+    r0 = recall()
+    gone = rng.permutation(n)[:300]
+    assert all(g.delete(gone, mode=1, heuristic=1, keep_pruned=1))
+    ex = g.export()
+    dead = ex["dead"].astype(bool)
+    for l in range(ex["deg"].shape[0]):
+        for i in np.flatnonzero(~dead & (ex["deg"][l] > 0)):
+            row = ex["adj"][l, i, : ex["deg"][l, i]]
+            assert not dead[row].any(), (l, i)
+            assert ex["deg"][l, i] <= (32 if l == 0 else 16) + 1
+    r1 = recall()
+    assert r1 >= 0.85 and r1 >= r0 - 0.02, (r0, r1)

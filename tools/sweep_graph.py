@@ -16,12 +16,14 @@ dev = torch.device("cuda")
 X = gen_vectors(n, 768, 1234, 12, 1000, dev, "cosine")
 Q = gen_vectors(16384, 768, 1234 + 7777, 12, 1000, dev, "cosine")
 configs = [
-    dict(M=16, m0=48, ef_construction=400, heuristic=2),
-    dict(M=16, m0=63, ef_construction=400, heuristic=2),
-    dict(M=16, m0=32, ef_construction=400, heuristic=2),
+    dict(M=16, m0=32, ef_construction=400, heuristic=2, keep_pruned=1),
+    dict(M=16, m0=40, ef_construction=400, heuristic=2, keep_pruned=1),
+    dict(M=16, m0=40, ef_construction=400, heuristic=2),
     dict(M=16, m0=48, ef_construction=400, heuristic=2, keep_pruned=1),
-    dict(M=24, m0=48, ef_construction=200, heuristic=2),
+    dict(M=16, m0=32, ef_construction=512, heuristic=2, keep_pruned=1),
+    dict(M=12, m0=32, ef_construction=400, heuristic=2, keep_pruned=1),
 ]
+EFS = (64, 72, 80, 88, 96)
 for cfg in configs:
     cfg = dict(cfg)
     M = cfg.pop("M")
@@ -35,7 +37,7 @@ for cfg in configs:
     G = Searcher(g, 4096, 10, 768, dev)
     tk, td, tn = (x.clone() for x in G.run(Q[:4096], H.MODE_EXACT, 0))
     S = Searcher(g, 16384, 10, 768, dev)
-    for ef in (48, 64, 96):
+    for ef in EFS:
         S.run(Q, H.MODE_BEAM, ef)
         torch.cuda.synchronize()
         t0 = time.time()
