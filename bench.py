@@ -53,7 +53,10 @@ def parse():
     p.add_argument("--metric", choices=["cosine", "euclidean"], default="cosine")
     p.add_argument("--M", type=int, default=16)
     p.add_argument("--M0", type=int, default=48)
-    p.add_argument("--efc", type=int, default=200)
+    p.add_argument("--efc", type=int, default=400)
+    p.add_argument("--keep-pruned", type=int, default=1)
+    p.add_argument("--ef-sweep", default="32,48,64,72,80,96,128,256",
+                   help="extra operating points (ef values) reported at N=1; '' disables")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--intrinsic", type=int, default=12)
     p.add_argument("--clusters", type=int, default=1000)
@@ -132,12 +135,15 @@ def cpu_baseline(g, queries_np, k, ef, metric, seconds):
     o.import_graph(**ex)
     del ex
     out = {}
-    for name, mode in (("beam", O.MODE_BEAM), ("compat", O.MODE_COMPAT)):
+    threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
+    for name, mode, nt, frac in (("beam", O.MODE_BEAM, 1, 0.4), ("compat", O.MODE_COMPAT, 1, 0.3),
+                                 ("beam_mt", O.MODE_BEAM, threads, 0.3)):
+        chunk = 32 * nt
         done, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < seconds / 2 and done < len(queries_np):
-            o.search(queries_np[done:done + 32], k, mode=mode, ef=ef)
-            done += min(32, len(queries_np) - done)
-        out[name] = (done / (time.perf_counter() - t0), done)
+        while time.perf_counter() - t0 < seconds * frac and done < len(queries_np):
+            o.search(queries_np[done:done + chunk], k, mode=mode, ef=ef, threads=nt)
+            done += min(chunk, len(queries_np) - done)
+        out[name] = (done / (time.perf_counter() - t0), done, nt)
     return out
 
 
@@ -162,7 +168,7 @@ def main():
     base_off = shard_range(a.nbase * world, world, rank)[0] if shard else 0
     X = gen_vectors(a.nbase, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=base_off)
     g = H.Graph(M=a.M, Ml=0.25, EfSearch=a.ef, Distance=metric, Rng=a.seed + (rank if shard else 0),
-                build_mode=H.BUILD_BATCH, m0=a.M0, ef_construction=a.efc, heuristic=2)
+                build_mode=H.BUILD_BATCH, m0=a.M0, ef_construction=a.efc, heuristic=2, keep_pruned=a.keep_pruned)
     g.reserve(a.nbase, a.dim)
     keys = np.arange(base_off, base_off + a.nbase, dtype=np.int64)
     torch.cuda.synchronize()
@@ -225,17 +231,44 @@ def main():
     qps = queries_done / elapsed
 
     # roofline of the search kernel (per launch = one step on this GPU)
-    E = st["search_dist_evals"] / a.steps
-    Xp = st["search_expansions"] / a.steps
     cap0 = a.M0 + 1
-    alg_bytes = E * 4 * a.dim + Xp * 4 * cap0 + a.batch * 4 * a.dim
+
+    def alg_bytes_of(stats, launches):
+        E = stats["search_dist_evals"] / launches
+        Xp = stats["search_expansions"] / launches
+        return E * 4 * a.dim + Xp * 4 * cap0 + a.batch * 4 * a.dim, E, Xp
+
+    alg_bytes, E, Xp = alg_bytes_of(st, a.steps)
     kms = float(np.mean(kernel_ms))
     achieved = alg_bytes / (kms * 1e-3) / 1e9
+
+    # other operating points of the same graph (N=1 only): recall / QPS per ef
+    points = []
+    if world == 1 and a.ef_sweep:
+        for ef in [int(x) for x in a.ef_sweep.split(",") if x]:
+            kk, _, nn = (x.clone() for x in S.run(Q, H.MODE_BEAM, ef))
+            r = recall_at_k(kk[:ngt], nn[:ngt], tk, tn, a.k)
+            g.reset_stats()
+            ms = []
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(3):
+                S.run(Q, H.MODE_BEAM, ef)
+                ms.append(g.last_kernel_ms())
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t1) / 3
+            ab, e_, _ = alg_bytes_of(g.stats(), 3)
+            km = float(np.mean(ms))
+            points.append({"ef": ef, "recall_at_10": round(r, 4), "qps": round(a.batch / dt, 1),
+                           "kernel_ms": round(km, 4), "dist_evals_per_query": round(e_ / a.batch, 1),
+                           "roofline_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+    at99 = next((p for p in points if p["recall_at_10"] >= 0.99), None)
     traffic = None
     if os.path.exists(a.pmc_json):
         try:
             pm = json.load(open(a.pmc_json))
-            if pm.get("n") == a.nbase and pm.get("dim") == a.dim and pm.get("batch") == a.batch and pm.get("ef") == a.ef:
+            want = dict(n=a.nbase, dim=a.dim, batch=a.batch, ef=a.ef, efc=a.efc, m0=a.M0, keep_pruned=a.keep_pruned)
+            if all(pm.get(k) == v for k, v in want.items()):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -259,7 +292,7 @@ def main():
             "workload": f"{a.nbase // 1000}k x {a.dim}-d {a.metric}, batched beam search ef={a.ef} k={a.k}, "
                         f"{a.batch} queries/step/GPU (BASELINE configs[1])",
             "n_base": a.nbase * (world if shard else 1), "dim": a.dim, "batch_per_gpu": a.batch, "ef": a.ef,
-            "k": a.k, "M": a.M, "M0": a.M0, "ef_construction": a.efc,
+            "k": a.k, "M": a.M, "M0": a.M0, "ef_construction": a.efc, "keep_pruned": a.keep_pruned,
             "parallelism": f"{'shard' if shard else 'replica'}{world}",
         },
         "recall_at_10": round(recall, 4),
@@ -274,6 +307,8 @@ def main():
                   "dist_evals_per_insert": round(bstats["build_dist_evals"] / a.nbase, 1),
                   "dropped_proposals": bstats["dropped_proposals"]},
         "cpu_baseline": None,
+        "operating_points": points,
+        "at_recall_0.99": at99,
     }
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
         qn = Q[: min(a.batch, 4096)].cpu().numpy()
@@ -281,9 +316,10 @@ def main():
         out["cpu_baseline"] = {
             "value": round(cb["beam"][0], 2), "unit": "queries/s", "cores": 1, "kind": "port",
             "sample": f"{cb['beam'][1]} of the same queries, same 1M graph, oracle beam search (ORDER_REF "
-                      f"sequential fp32), single thread, ~{a.cpu_seconds / 2:.0f}s time box",
+                      f"sequential fp32), single thread, ~{a.cpu_seconds * 0.4:.0f}s time box",
             "compat_search_qps": round(cb["compat"][0], 2), "compat_sample": cb["compat"][1],
-            "host_cpus": os.cpu_count(),
+            "beam_mt_qps": round(cb["beam_mt"][0], 2), "beam_mt_threads": cb["beam_mt"][2],
+            "beam_mt_sample": cb["beam_mt"][1], "host_cpus": os.cpu_count(),
         }
     if rank == 0:
         print(json.dumps(out), flush=True)
