@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/mhnsw.h"
+#include "codec.hpp"
 #include "engine.hpp"
 
 using namespace mh;
@@ -986,9 +987,44 @@ int mhnsw_export(mhnsw_index* h, int64_t* keys, float* vecs, int32_t* deg, int32
     return 0;
 }
 
-int mhnsw_import(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t* keys, const float* vecs,
-                 const int32_t* deg, const int32_t* adj, const int32_t* entry, const uint8_t* dead) {
-    std::unique_lock<std::shared_mutex> lk(h->mu);
+}  // extern "C"
+
+namespace {
+
+// drop every row and layer (Graph.Import replaces the graph, encode.go:208)
+void reset_graph(mhnsw_index* h) {
+    (void)hipStreamSynchronize(h->stream);
+    auto F = [](auto*& p) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+    };
+    F(h->vecs);
+    F(h->norms);
+    F(h->keys);
+    F(h->levels);
+    F(h->dead);
+    F(h->cur_entry);
+    F(h->inc_cnt);
+    F(h->inc_src);
+    F(h->inc_dist);
+    for (auto& L : h->layers) {
+        F(L.deg);
+        F(L.adj);
+        F(L.adjd);
+    }
+    h->layers.clear();
+    memset(h->layers_host, 0, sizeof(h->layers_host));
+    h->capn = h->n = 0;
+    h->dim = h->pitch = h->lpr = h->vpl = 0;
+    h->layers_exist = h->any_dead = false;
+    h->key2id.clear();
+    h->hlevels.clear();
+    h->hmask.clear();
+    h->hdead.clear();
+}
+
+int import_csr(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t* keys, const float* vecs,
+               const int32_t* deg, const int32_t* adj, const int32_t* entry, const uint8_t* dead) {
     if (h->n > 0) return fail(h, MHNSW_EINVAL, "import requires an empty index");
     if (L > MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "more than %d layers", MH_MAXL);
     if (cap > 64) return fail(h, MHNSW_EUNSUPPORTED, "degree cap above 64 unsupported");
@@ -1047,6 +1083,199 @@ int mhnsw_import(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64
         if (!h->hdead[i] && !h->key2id.count(keys[i])) h->key2id[keys[i]] = (int32_t)i;
     h->n = N;
     h->layers_exist = L > 0;
+    return 0;
+}
+
+const char* metric_name(int m) { return m == COSINE ? "cosine" : "euclidean"; }
+
+bool key_fits(int64_t k, int kind) {
+    switch (kind) {
+        case KEY_INT32: return k >= INT32_MIN && k <= INT32_MAX;
+        case KEY_UINT32: return k >= 0 && k <= (int64_t)UINT32_MAX;
+        case KEY_UINT64: return k >= 0;
+        default: return true;
+    }
+}
+
+// encode.go:128-174 Graph.Export: nodes in id (insertion) order, neighbour keys
+// ascending (Go writes both in map order, which is unspecified)
+int export_go(mhnsw_index* h, int key_kind, std::vector<uint8_t>& out) {
+    if (!key_kind_ok(key_kind)) return fail(h, MHNSW_EINVAL, "unsupported key kind %d", key_kind);
+    int r = validate(h);
+    if (r) return r;
+    GoWriter w;
+    w.varint(1);  // encodingVersion
+    w.varint(h->M);
+    w.f64(h->ml);
+    w.varint(h->ef);
+    w.str(metric_name(h->metric));
+    const int L = (int)h->layers.size();
+    w.varint(L);
+    const int64_t N = h->n;
+    std::vector<int64_t> keys((size_t)std::max<int64_t>(N, 1));
+    std::vector<float> vecs((size_t)std::max<int64_t>(N, 1) * std::max(h->dim, 1));
+    if (N > 0) {
+        HIPCHK(h, hipMemcpy(keys.data(), h->keys, N * 8, hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemcpy2D(vecs.data(), (size_t)h->dim * 4, h->vecs, (size_t)h->pitch * 4, (size_t)h->dim * 4, N,
+                              hipMemcpyDeviceToHost));
+    }
+    std::vector<int32_t> deg, adj;
+    std::vector<int64_t> nb;
+    for (int l = 0; l < L; ++l) {
+        const Layer& Ly = h->layers[l];
+        deg.resize((size_t)N);
+        adj.resize((size_t)N * Ly.cap);
+        if (N > 0) {
+            HIPCHK(h, hipMemcpy(deg.data(), Ly.deg, N * 4, hipMemcpyDeviceToHost));
+            HIPCHK(h, hipMemcpy(adj.data(), Ly.adj, (size_t)N * Ly.cap * 4, hipMemcpyDeviceToHost));
+        }
+        w.varint(Ly.count);
+        for (int64_t i = 0; i < N; ++i) {
+            if (!in_layer(h, i, l) || h->hdead[i]) continue;
+            if (!key_fits(keys[i], key_kind)) return fail(h, MHNSW_EINVAL, "key %lld does not fit the key type", (long long)keys[i]);
+            w.key(keys[i], key_kind);
+            w.floats(vecs.data() + (size_t)i * h->dim, h->dim);
+            const int d = std::min(std::max(deg[i], 0), Ly.cap);
+            nb.clear();
+            for (int j = 0; j < d; ++j) nb.push_back(keys[(size_t)adj[(size_t)i * Ly.cap + j]]);
+            std::sort(nb.begin(), nb.end());
+            w.varint(d);
+            for (int64_t k : nb) w.key(k, key_kind);
+        }
+    }
+    out.swap(w.out);
+    return 0;
+}
+
+// encode.go:178-262 Graph.Import.  Neighbour keys that are not nodes of the
+// same layer (dangling edges to deleted nodes in a Go-written file) become nil
+// map entries in the reference; they are dropped here.
+int import_go(mhnsw_index* h, const uint8_t* buf, int64_t size, int key_kind) {
+    GoGraph gg;
+    const std::string e = go_decode(buf, (size_t)std::max<int64_t>(size, 0), key_kind, gg);
+    if (!e.empty()) return fail(h, MHNSW_EINVAL, "%s", e.c_str());
+    h->M = (int)gg.M;
+    h->ml = gg.ml;
+    h->ef = (int)gg.ef;
+    h->metric = gg.dist == "cosine" ? COSINE : EUCLIDEAN;
+    const int L = (int)gg.layers.size();
+    const int64_t N = L ? (int64_t)gg.layers[0].keys.size() : 0;
+    reset_graph(h);
+    if (N == 0) return 0;
+    if (L > MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "more than %d layers", MH_MAXL);
+    std::unordered_map<int64_t, int32_t> id;
+    id.reserve((size_t)N * 2);
+    for (int64_t j = 0; j < N; ++j) id[gg.layers[0].keys[(size_t)j]] = (int32_t)j;
+    std::vector<int32_t> deg((size_t)L * N, -2), entry((size_t)L, -1);
+    std::vector<uint8_t> member((size_t)N);
+    std::vector<std::vector<int32_t>> rows((size_t)L);  // resolved neighbour ids, CSR per layer
+    std::vector<std::vector<int64_t>> roff((size_t)L);
+    int maxd = 0;
+    for (int l = 0; l < L; ++l) {
+        const GoLayer& G = gg.layers[(size_t)l];
+        std::fill(member.begin(), member.end(), 0);
+        std::vector<int32_t> ids(G.keys.size());
+        for (size_t j = 0; j < G.keys.size(); ++j) {
+            auto it = id.find(G.keys[j]);
+            if (it == id.end())
+                return fail(h, MHNSW_EINVAL, "node %lld of layer %d is missing from layer 0", (long long)G.keys[j], l);
+            ids[j] = it->second;
+            member[(size_t)it->second] = 1;
+            if (entry[(size_t)l] < 0 || it->second < entry[(size_t)l]) entry[(size_t)l] = it->second;
+        }
+        std::vector<int32_t>& R = rows[(size_t)l];
+        std::vector<int64_t>& O = roff[(size_t)l];
+        O.assign((size_t)N + 1, 0);
+        // resolve neighbours, bucket by node id
+        std::vector<int32_t> cnt((size_t)N, 0);
+        std::vector<int32_t> tmp;
+        std::vector<int64_t> tmpo(G.keys.size() + 1, 0);
+        for (size_t j = 0; j < G.keys.size(); ++j) {
+            for (int64_t t = G.nb_off[j]; t < G.nb_off[j + 1]; ++t) {
+                auto it = id.find(G.nb_keys[(size_t)t]);
+                if (it != id.end() && member[(size_t)it->second]) tmp.push_back(it->second);
+            }
+            tmpo[j + 1] = (int64_t)tmp.size();
+            cnt[(size_t)ids[j]] = (int32_t)(tmpo[j + 1] - tmpo[j]);
+            maxd = std::max(maxd, cnt[(size_t)ids[j]]);
+        }
+        for (int64_t i = 0; i < N; ++i) O[(size_t)i + 1] = O[(size_t)i] + cnt[(size_t)i];
+        R.assign((size_t)O[(size_t)N], 0);
+        for (size_t j = 0; j < G.keys.size(); ++j) {
+            const int32_t i = ids[j];
+            deg[(size_t)l * N + i] = cnt[(size_t)i];  // a decoded map is never nil (encode.go:237)
+            std::copy(tmp.begin() + tmpo[j], tmp.begin() + tmpo[j + 1], R.begin() + O[(size_t)i]);
+        }
+    }
+    int cap = 0;
+    for (int l = 0; l < L; ++l) cap = std::max(cap, cap_of(h, l));
+    cap = std::max(cap, maxd);
+    if (cap > 64) return fail(h, MHNSW_EUNSUPPORTED, "degree %d above 64 unsupported", maxd);
+    std::vector<int32_t> adj((size_t)L * N * cap, -1);
+    for (int l = 0; l < L; ++l)
+        for (int64_t i = 0; i < N; ++i)
+            for (int64_t t = roff[(size_t)l][(size_t)i]; t < roff[(size_t)l][(size_t)i + 1]; ++t)
+                adj[((size_t)l * N + i) * cap + (size_t)(t - roff[(size_t)l][(size_t)i])] = rows[(size_t)l][(size_t)t];
+    return import_csr(h, N, gg.dim, L, cap, gg.layers[0].keys.data(), gg.vals0.data(), deg.data(), adj.data(),
+                      entry.data(), nullptr);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mhnsw_import(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t* keys, const float* vecs,
+                 const int32_t* deg, const int32_t* adj, const int32_t* entry, const uint8_t* dead) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    return import_csr(h, N, dim, L, cap, keys, vecs, deg, adj, entry, dead);
+}
+
+int mhnsw_export_go(mhnsw_index* h, int key_kind, uint8_t* buf, int64_t cap, int64_t* size) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    std::vector<uint8_t> out;
+    int r = export_go(h, key_kind, out);
+    if (r) return r;
+    if (size) *size = (int64_t)out.size();
+    if (!buf) return 0;
+    if (cap < (int64_t)out.size())
+        return fail(h, MHNSW_EINVAL, "buffer too small: need %lld bytes", (long long)out.size());
+    memcpy(buf, out.data(), out.size());
+    return 0;
+}
+
+int mhnsw_import_go(mhnsw_index* h, const uint8_t* buf, int64_t size, int key_kind) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    return import_go(h, buf, size, key_kind);
+}
+
+// encode.go:301-327 SavedGraph.Save: write to a temp file, then rename over path
+int mhnsw_save(mhnsw_index* h, const char* path, int key_kind) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    std::vector<uint8_t> out;
+    int r = export_go(h, key_kind, out);
+    if (r) return r;
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) return fail(h, MHNSW_EINVAL, "open %s failed", tmp.c_str());
+    const bool ok = fwrite(out.data(), 1, out.size(), f) == out.size();
+    if (fclose(f) != 0 || !ok) return fail(h, MHNSW_EINVAL, "write %s failed", tmp.c_str());
+    if (rename(tmp.c_str(), path) != 0) return fail(h, MHNSW_EINVAL, "rename to %s failed", path);
+    return 0;
+}
+
+// encode.go:280-299 LoadSavedGraph: a missing or empty file leaves the graph empty
+int mhnsw_load(mhnsw_index* h, const char* path, int key_kind) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    FILE* f = fopen(path, "rb");
+    if (!f) return 0;
+    std::vector<uint8_t> buf;
+    uint8_t tmp[1 << 16];
+    size_t got;
+    while ((got = fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + got);
+    fclose(f);
+    if (buf.empty()) return 0;
+    const int r = import_go(h, buf.data(), (int64_t)buf.size(), key_kind);
+    if (r) return fail(h, r, "import: %s", h->err.c_str());
     return 0;
 }
 

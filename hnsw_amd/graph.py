@@ -9,12 +9,13 @@ run on the GPU (a custom Python callable cannot, and is rejected).
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Iterable, List, NamedTuple, Optional, Sequence
 
 import numpy as np
 
-from ._lib import (BUILD_BATCH, BUILD_COMPAT, COSINE, EUCLIDEAN, MODE_BEAM, MODE_COMPAT, MODE_EXACT, HnswError,
-                   check, load)
+from ._lib import (BUILD_BATCH, BUILD_COMPAT, COSINE, EUCLIDEAN, KEY_INT, MODE_BEAM, MODE_COMPAT, MODE_EXACT,
+                   HnswError, check, load)
 
 Vector = np.ndarray
 
@@ -322,6 +323,34 @@ class Graph:
                                      _ptr(adj, C.c_int32), cap, _ptr(entry, C.c_int32), _ptr(dead, C.c_uint8)))
         return dict(keys=keys, vecs=vecs, deg=deg, adj=adj, entry=entry[:L], dead=dead[:N])
 
+    # -- encode.go:128-262 binary format ------------------------------------------
+    def export_bytes(self, key_kind: int = KEY_INT) -> bytes:
+        self._sync()
+        lib = load()
+        size = C.c_int64()
+        self._check(lib.mhnsw_export_go(self._h, key_kind, None, 0, C.byref(size)))
+        buf = np.zeros(max(size.value, 1), np.uint8)
+        self._check(lib.mhnsw_export_go(self._h, key_kind, _ptr(buf, C.c_uint8), buf.size, C.byref(size)))
+        return buf[: size.value].tobytes()
+
+    def import_bytes(self, data: bytes, key_kind: int = KEY_INT):
+        buf = np.frombuffer(data, np.uint8).copy() if len(data) else np.zeros(1, np.uint8)
+        self._check(load().mhnsw_import_go(self._h, _ptr(buf, C.c_uint8), len(data), key_kind))
+        self._values.clear()
+        self._pull_params()
+
+    def Export(self, w, key_kind: int = KEY_INT):  # encode.go:131-176 (w: has .write)
+        w.write(self.export_bytes(key_kind))
+
+    def Import(self, r, key_kind: int = KEY_INT):  # encode.go:181-262 (r: has .read)
+        self.import_bytes(r.read(), key_kind)
+
+    def _pull_params(self):
+        m, M, ml, ef = C.c_int(), C.c_int(), C.c_double(), C.c_int()
+        self._check(load().mhnsw_get_params(self._h, C.byref(m), C.byref(M), C.byref(ml), C.byref(ef)))
+        self.M, self.Ml, self.EfSearch = M.value, ml.value, ef.value
+        self.Distance = CosineDistance if m.value == COSINE else EuclideanDistance
+
     def import_graph(self, keys, vecs, deg, adj, entry, dead=None):
         keys = np.ascontiguousarray(keys, np.int64)
         vecs = _f32(vecs)
@@ -334,6 +363,29 @@ class Graph:
         self._check(load().mhnsw_import(self._h, N, vecs.shape[1], L, adj.shape[2], _ptr(keys, C.c_int64),
                                         _ptr(vecs, C.c_float), _ptr(deg, C.c_int32), _ptr(adj, C.c_int32),
                                         _ptr(entry, C.c_int32), None if dd is None else _ptr(dd, C.c_uint8)))
+
+
+class SavedGraph(Graph):
+    """encode.go:264-327: a Graph persisted to `Path` by Save() (temp file +
+    atomic rename)."""
+
+    Path: str = ""
+
+    def Save(self, key_kind: int = KEY_INT):
+        self._sync()
+        self._check(load().mhnsw_save(self._h, os.fsencode(self.Path), key_kind))
+
+
+def LoadSavedGraph(path: str, key_kind: int = KEY_INT) -> SavedGraph:  # encode.go:280-299
+    """Opens (or creates) `path`; an empty or new file gives NewGraph()."""
+    import time
+    open(path, "ab").close()  # os.O_RDWR|os.O_CREATE
+    g = SavedGraph(M=16, Ml=0.25, EfSearch=20, Distance=CosineDistance, Rng=time.time_ns())
+    g.Path = path
+    g._check(load().mhnsw_load(g._h, os.fsencode(path), key_kind))
+    if g.Len() or os.path.getsize(path):
+        g._pull_params()
+    return g
 
 
 def NewGraph() -> Graph:  # graph.go:340-348

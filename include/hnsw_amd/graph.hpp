@@ -192,6 +192,29 @@ class Graph {  // graph.go:305-332
         return c;
     }
 
+    // encode.go:131-176 Export (Go key type K: MHNSW_KEY_INT for `int`, ...)
+    std::pair<std::vector<uint8_t>, Error> Export(int key_kind = MHNSW_KEY_INT) {
+        sync();
+        int64_t size = 0;
+        int rc = mhnsw_export_go(h_, key_kind, nullptr, 0, &size);
+        if (rc < 0) return {{}, make_error(rc, h_)};
+        std::vector<uint8_t> buf((size_t)size);
+        rc = mhnsw_export_go(h_, key_kind, buf.data(), size, &size);
+        if (rc < 0) return {{}, make_error(rc, h_)};
+        return {buf, {}};
+    }
+
+    // encode.go:181-262 Import: parameters and distance come from the file
+    Error Import(const std::vector<uint8_t>& buf, int key_kind = MHNSW_KEY_INT) {
+        int rc = mhnsw_import_go(h_, buf.data(), (int64_t)buf.size(), key_kind);
+        if (rc < 0) return make_error(rc, h_);
+        int metric = 0;
+        mhnsw_get_params(h_, &metric, &M, &Ml, &EfSearch);
+        Distance = metric == MHNSW_COSINE ? &CosineDistance : &EuclideanDistance;
+        values_.clear();
+        return {};
+    }
+
     // graph.go:843-864
     bool Delete(K key) { return BatchDelete(std::vector<K>{key})[0]; }
 

@@ -128,6 +128,21 @@ int mhnsw_export(mhnsw_index *h, int64_t *keys, float *vecs, int32_t *deg, int32
 int mhnsw_import(mhnsw_index *h, int64_t N, int dim, int L, int cap, const int64_t *keys, const float *vecs,
                  const int32_t *deg, const int32_t *adj, const int32_t *entry, const uint8_t *dead);
 
+/* ---- the reference's binary format (encode.go:128-262) and SavedGraph (encode.go:264-327) ----
+ * key_kind = the Go key type K: MHNSW_KEY_INT (Go `int`, varint-encoded),
+ * MHNSW_KEY_INT64 / _INT32 / _UINT64 / _UINT32 (fixed-width little-endian).
+ * Export: *size receives the byte count; buf == NULL only sizes.  Nodes are
+ * written in insertion order and neighbour keys ascending (Go: map order).
+ * Import replaces the graph (M, Ml, EfSearch and the distance come from the
+ * file) and reports the reference's errors ("unknown distance function %q",
+ * "incompatible encoding version: %d", ...).  Save writes path.tmp then
+ * renames; Load of a missing or empty file leaves the graph empty. */
+enum { MHNSW_KEY_INT = 0, MHNSW_KEY_INT64 = 1, MHNSW_KEY_INT32 = 2, MHNSW_KEY_UINT64 = 3, MHNSW_KEY_UINT32 = 4 };
+int mhnsw_export_go(mhnsw_index *h, int key_kind, uint8_t *buf, int64_t cap, int64_t *size);
+int mhnsw_import_go(mhnsw_index *h, const uint8_t *buf, int64_t size, int key_kind);
+int mhnsw_save(mhnsw_index *h, const char *path, int key_kind);
+int mhnsw_load(mhnsw_index *h, const char *path, int key_kind);
+
 /* levels randomLevel() would draw for the next n Adds (does not consume the RNG) */
 int mhnsw_preview_levels(mhnsw_index *h, int64_t n, int32_t *out);
 

@@ -148,6 +148,23 @@ static void TestGraph_AddDelete() {
     REQUIRE(!s.second, "search after delete");
 }
 
+// encode_test.go:120-160 TestGraph_ExportImport
+static void TestGraph_ExportImport() {
+    hnsw::Graph<int> g1(6, 0.5, 20, &hnsw::EuclideanDistance, 0);
+    for (int i = 0; i < 128; ++i) g1.Add(hnsw::MakeNode(i, {(float)((i * 37) % 128) / 128.f}));
+    auto ex = g1.Export();
+    REQUIRE(!ex.second && !ex.first.empty(), "Export");
+    hnsw::Graph<int> g2;
+    REQUIRE(!g2.Import(ex.first), "Import");
+    REQUIRE(g1.Len() == g2.Len() && g1.Topography() == g2.Topography(), "Len/Topography");
+    REQUIRE(g1.Connectivity() == g2.Connectivity(), "Connectivity");
+    REQUIRE(g2.M == 6 && g2.Ml == 0.5 && g2.EfSearch == 20 && g2.Distance == &hnsw::EuclideanDistance, "params");
+    auto n1 = g1.Search({0.5f}, 10), n2 = g2.Search({0.5f}, 10);
+    REQUIRE(!n1.second && !n2.second && n1.first.size() == n2.first.size(), "Search");
+    for (size_t i = 0; i < n1.first.size() && i < n2.first.size(); ++i)
+        REQUIRE(n1.first[i] == n2.first[i], "Search nodes");
+}
+
 int main() {
     TestDistances();
     Test_layerNode_search();
@@ -157,6 +174,7 @@ int main() {
     TestDimensionMismatch();
     TestBatchDelete();
     TestGraph_AddDelete();
+    TestGraph_ExportImport();
     std::printf("%s (%d failures)\n", failures ? "FAIL" : "PASS", failures);
     return failures;
 }
