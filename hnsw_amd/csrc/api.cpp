@@ -94,6 +94,10 @@ struct mhnsw_index {
     DevBuf<int64_t> okeys;
     DevBuf<float> odist;
     DevBuf<int32_t> on;
+    DevBuf<float> nq, nneg, ncd;  // negatives: queries, padded negative rows, candidate distances
+    DevBuf<int64_t> nck, nok;
+    DevBuf<int32_t> ncn, nci, noff, non;
+    DevBuf<float> nos;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool have_timing = false;
     // host mirrors
@@ -574,7 +578,8 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
 }
 
 int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B, int dim, int k, int mode, int ef,
-                const int64_t* entry_key, int64_t* okeys, float* odist, int32_t* on, hipStream_t s, bool timing) {
+                const int64_t* entry_key, int64_t* okeys, float* odist, int32_t* on, hipStream_t s, bool timing,
+                int32_t* out_ids = nullptr) {
     int r = validate(h);
     if (r) return r;
     if (k <= 0) return fail(h, MHNSW_EK, "k must be greater than 0, got %d", k);  // graph.go:542-544
@@ -654,7 +659,7 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             LCHK(h, launch_exact_scores(a, s));
             LCHK(h, launch_exact_select(a, s));
             LCHK(h, launch_rerank(a.Q, g, h->cand.p, kk, nb, h->lpr, h->vpl, k, dk + q0 * k, dd + q0 * k, dn + q0,
-                                  nullptr, s));
+                                  out_ids ? out_ids + q0 * k : nullptr, s));
         }
         if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));
     } else {
@@ -672,7 +677,7 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         a.out_keys = dk;
         a.out_dist = dd;
         a.out_n = dn;
-        a.out_ids = nullptr;
+        a.out_ids = out_ids;
         a.stats = h->d_stats;
         a.err = h->d_err;
         a.vis_log2 = h->vis_log2;
@@ -777,6 +782,16 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->okeys.p);
     F(h->odist.p);
     F(h->on.p);
+    F(h->nq.p);
+    F(h->nneg.p);
+    F(h->ncd.p);
+    F(h->nck.p);
+    F(h->nok.p);
+    F(h->ncn.p);
+    F(h->nci.p);
+    F(h->noff.p);
+    F(h->non.p);
+    F(h->nos.p);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1276,6 +1291,116 @@ int mhnsw_load(mhnsw_index* h, const char* path, int key_kind) {
     if (buf.empty()) return 0;
     const int r = import_go(h, buf.data(), (int64_t)buf.size(), key_kind);
     if (r) return fail(h, r, "import: %s", h->err.c_str());
+    return 0;
+}
+
+// graph.go:1116-1537 SearchWithNegative(s) / BatchSearchWithNegatives
+int mhnsw_search_negatives(mhnsw_index* h, const float* queries, int64_t B, int dim, const float* negatives,
+                           const int32_t* neg_count, int k, float neg_weight, int mode, int ef, int flags,
+                           int64_t* out_keys, float* out_score, int32_t* out_n) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    int r = validate(h);
+    if (r) return r;
+    if (k <= 0) return fail(h, MHNSW_EK, "k must be greater than 0, got %d", k);
+    if (!(neg_weight >= 0.0f && neg_weight <= 1.0f))
+        return fail(h, MHNSW_EINVAL, "negWeight must be between 0.0 and 1.0, got %f", (double)neg_weight);
+    if (h->layers_exist && h->dim != dim)
+        return fail(h, MHNSW_EDIM, "query embedding dimension mismatch: %d != %d", h->dim, dim);
+    if (B <= 0) return 0;
+    for (int64_t b = 0; b < B; ++b) out_n[b] = 0;
+    if (!h->layers_exist || live_count(h) == 0) return 0;  // graph.go:1144-1146
+    const int kx = std::max(3 * k, 10);                    // graph.go:1150-1153
+    if (kx > NEG_MAX_CAND) return fail(h, MHNSW_EUNSUPPORTED, "negatives support k <= %d", NEG_MAX_CAND / 3);
+    // queries without negatives are a plain Search(near, k) (graph.go:1395-1398)
+    std::vector<int64_t> plain, rer;
+    std::vector<int32_t> off(1, 0);
+    for (int64_t b = 0; b < B; ++b) {
+        if (neg_count[b] < 0) return fail(h, MHNSW_EINVAL, "negative count %d for query %lld", neg_count[b], (long long)b);
+        (neg_count[b] == 0 ? plain : rer).push_back(b);
+    }
+    const int64_t ntot = [&] {
+        int64_t t = 0;
+        for (int64_t b = 0; b < B; ++b) t += neg_count[b];
+        return t;
+    }();
+    hipStream_t s = h->stream;
+    if (!plain.empty()) {
+        std::vector<float> q(plain.size() * (size_t)dim);
+        for (size_t i = 0; i < plain.size(); ++i)
+            memcpy(&q[i * dim], queries + (size_t)plain[i] * dim, (size_t)dim * 4);
+        std::vector<int64_t> kk(plain.size() * (size_t)k);
+        std::vector<float> dd(plain.size() * (size_t)k);
+        std::vector<int32_t> nn(plain.size());
+        if ((r = search_impl(h, q.data(), false, (int64_t)plain.size(), dim, k, mode, ef, nullptr, kk.data(), dd.data(),
+                             nn.data(), s, false)))
+            return r;
+        for (size_t i = 0; i < plain.size(); ++i) {
+            memcpy(out_keys + (size_t)plain[i] * k, &kk[i * k], (size_t)k * 8);
+            memcpy(out_score + (size_t)plain[i] * k, &dd[i * k], (size_t)k * 4);
+            out_n[plain[i]] = nn[i];
+        }
+    }
+    if (rer.empty()) return 0;
+    const int64_t R = (int64_t)rer.size();
+    // gather the re-ranked queries and their negatives
+    std::vector<float> q((size_t)R * dim), ng((size_t)std::max<int64_t>(ntot, 1) * dim);
+    std::vector<int64_t> noff_b((size_t)B + 1, 0);
+    for (int64_t b = 0; b < B; ++b) noff_b[(size_t)b + 1] = noff_b[(size_t)b] + neg_count[b];
+    int64_t w = 0;
+    for (int64_t i = 0; i < R; ++i) {
+        const int64_t b = rer[(size_t)i];
+        memcpy(&q[(size_t)i * dim], queries + (size_t)b * dim, (size_t)dim * 4);
+        memcpy(&ng[(size_t)w * dim], negatives + (size_t)noff_b[(size_t)b] * dim, (size_t)neg_count[b] * dim * 4);
+        w += neg_count[b];
+        off.push_back((int32_t)w);
+    }
+    if ((r = ensure_buf(h, h->nq, (size_t)R * dim)) || (r = ensure_buf(h, h->nneg, (size_t)std::max<int64_t>(w, 1) * h->pitch)) ||
+        (r = ensure_buf(h, h->nck, (size_t)R * kx)) || (r = ensure_buf(h, h->ncd, (size_t)R * kx)) ||
+        (r = ensure_buf(h, h->nci, (size_t)R * kx)) || (r = ensure_buf(h, h->ncn, (size_t)R)) ||
+        (r = ensure_buf(h, h->noff, (size_t)R + 1)) || (r = ensure_buf(h, h->nok, (size_t)R * k)) ||
+        (r = ensure_buf(h, h->nos, (size_t)R * k)) || (r = ensure_buf(h, h->non, (size_t)R)))
+        return r;
+    HIPCHK(h, hipMemcpyAsync(h->nq.p, q.data(), q.size() * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(h, hipMemcpyAsync(h->noff.p, off.data(), off.size() * 4, hipMemcpyHostToDevice, s));
+    if (w > 0) {
+        if ((r = ensure_buf(h, h->tmp, (size_t)w * dim))) return r;
+        HIPCHK(h, hipMemcpyAsync(h->tmp.p, ng.data(), (size_t)w * dim * 4, hipMemcpyHostToDevice, s));
+        LCHK(h, launch_pad_rows(h->tmp.p, w, dim, h->nneg.p, h->pitch, s));
+    }
+    // candidates: Search(near, kx) in the requested mode, internal ids kept
+    if ((r = search_impl(h, h->nq.p, true, R, dim, kx, mode, ef, nullptr, h->nck.p, h->ncd.p, h->ncn.p, s, false,
+                         h->nci.p)))
+        return r;
+    if ((r = sync_layer_table(h))) return r;
+    NegArgs a;
+    a.g = graph_view(h);
+    a.neg = h->nneg.p;
+    a.neg_off = h->noff.p;
+    a.cand_ids = h->nci.p;
+    a.cand_d = h->ncd.p;
+    a.cand_n = h->ncn.p;
+    a.B = R;
+    a.kx = kx;
+    a.k = k;
+    a.w = neg_weight;
+    a.flags = flags;
+    a.out_keys = h->nok.p;
+    a.out_score = h->nos.p;
+    a.out_n = h->non.p;
+    LCHK(h, launch_negatives(a, h->lpr, h->vpl, s));
+    std::vector<int64_t> kk((size_t)R * k);
+    std::vector<float> ss((size_t)R * k);
+    std::vector<int32_t> nn((size_t)R);
+    HIPCHK(h, hipMemcpyAsync(kk.data(), h->nok.p, kk.size() * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(ss.data(), h->nos.p, ss.size() * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(nn.data(), h->non.p, nn.size() * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    for (int64_t i = 0; i < R; ++i) {
+        const int64_t b = rer[(size_t)i];
+        memcpy(out_keys + (size_t)b * k, &kk[(size_t)i * k], (size_t)k * 8);
+        memcpy(out_score + (size_t)b * k, &ss[(size_t)i * k], (size_t)k * 4);
+        out_n[b] = nn[(size_t)i];
+    }
     return 0;
 }
 

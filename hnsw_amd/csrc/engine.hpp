@@ -42,6 +42,25 @@ struct SearchArgs {
     int vis_log2;
 };
 
+// negative-example re-ranking epilogue (graph.go:1116-1537)
+struct NegArgs {
+    GraphDev g;
+    const float* neg;          // padded negative rows [total * pitch]
+    const int32_t* neg_off;    // [B + 1] row offsets of each query's negatives
+    const int32_t* cand_ids;   // [B * kx] Search(near, kx) internal ids
+    const float* cand_d;       // [B * kx] their distances to the query
+    const int32_t* cand_n;     // [B]
+    int64_t B;
+    int kx, k;
+    float w;
+    int flags;                 // bit 0: the reference's key 7..9 boost (test hack)
+    int64_t* out_keys;         // [B * k]
+    float* out_score;          // [B * k]
+    int32_t* out_n;            // [B]
+};
+constexpr int NEG_MAX_CAND = 256;
+int launch_negatives(const NegArgs& a, int lpr, int vpl, hipStream_t s);
+
 int launch_pad_rows(const float* src, int64_t n, int dim, float* dst, int pitch, hipStream_t s);
 int launch_norms(const float* X, int64_t n0, int64_t n1, int pitch, int lpr, int vpl, float* out, hipStream_t s);
 int launch_sweep(const float* q, const float* X, int64_t n, int pitch, int lpr, int vpl, int metric, float* out,

@@ -282,6 +282,84 @@ __global__ __launch_bounds__(64) void k_search_compat(SearchArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// negative-example re-ranking (graph.go:1116-1537), one wave per query: the
+// Search(near, kx) candidates are scored against the query's negatives with
+// the reference's float32 formula, then ranked by descending score (ties in
+// candidate order, NaN last).  Restated in oracle/oracle.c og_search_negatives.
+// ---------------------------------------------------------------------------
+template <class C, int G>
+__global__ __launch_bounds__(64) void k_negatives(NegArgs a) {
+#pragma clang fp contract(off)
+    __shared__ float sc[NEG_MAX_CAND];
+    __shared__ int32_t sid[NEG_MAX_CAND];
+    const int64_t b = blockIdx.x;
+    if (b >= a.B) return;
+    const int lane = lane_id();
+    const int n = min(a.cand_n[b], a.kx);
+    const int j0 = a.neg_off[b], j1 = a.neg_off[b + 1];
+    const int nn = j1 - j0;
+    for (int base = 0; base < n; base += 64) {
+        const int cnt = min(64, n - base);
+        const bool mine = lane < cnt;
+        const uint32_t cid = mine ? (uint32_t)a.cand_ids[b * a.kx + base + lane] : 0u;
+        const float qd = mine ? a.cand_d[b * a.kx + base + lane] : 0.f;
+        float total = 0.f;
+        bool close = false;
+        for (int j = j0; j < j1; ++j) {
+            QReg<C> nq;
+            load_query(nq, a.neg + (size_t)j * C::PITCH);
+            const float nqn = query_norm(nq);
+            float nd = 0.f;
+            int t = 0;
+            eval_list<C, G>(a.g, nq, nqn, cid, cnt, a.g.metric, [&](float d, uint32_t) {
+                if (lane == t) nd = d;
+                ++t;
+            });
+            total = total + (1.0f - nd);
+            close = close || nd < 0.1f;
+        }
+        const float qs = 1.0f - qd;
+        const float avg = total / (float)nn;
+        float score;
+        if (qd < 0.001f) {
+            score = 2.0f;
+        } else if (close) {
+            score = qs - a.w * 2.0f;
+        } else {
+            const int64_t key = mine ? a.g.keys[cid] : 0;
+            const float boost = ((a.flags & 1) && key >= 7 && key <= 9) ? 0.2f : 0.0f;
+            score = qs - a.w * avg + boost;
+        }
+        if (mine) {
+            sc[base + lane] = score;
+            sid[base + lane] = (int32_t)cid;
+        }
+    }
+    __syncthreads();
+    for (int e = lane; e < n; e += 64) {
+        const float se = sc[e];
+        const bool en = se != se;
+        int rank = 0;
+        for (int f = 0; f < n; ++f) {
+            const float sf = sc[f];
+            const bool fn = sf != sf;
+            const bool before = (fn != en) ? en : ((!fn && sf != se) ? sf > se : f < e);
+            rank += before ? 1 : 0;
+        }
+        if (rank < a.k) {
+            a.out_keys[b * a.k + rank] = a.g.keys[sid[e]];
+            a.out_score[b * a.k + rank] = se;
+        }
+    }
+    const int m = min(n, a.k);
+    for (int i = m + lane; i < a.k; i += 64) {
+        a.out_keys[b * a.k + i] = (int64_t)-1;
+        a.out_score[b * a.k + i] = __int_as_float(0x7fc00000);
+    }
+    if (lane == 0) a.out_n[b] = m;
+}
+
 template <class C, int R, int G>
 static int launch_beam_t(const SearchArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 << a.vis_log2;
@@ -335,6 +413,19 @@ int launch_search_beam(const SearchArgs& a, int lpr, int vpl, hipStream_t s) {
         if (efl <= 256) return launch_beam_t<Cfg<L, V>, 4, G>(a, s);             \
         if (efl <= 512) return launch_beam_t<Cfg<L, V>, 8, G>(a, s);             \
         return -4;                                                               \
+    }
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return -3;
+}
+
+int launch_negatives(const NegArgs& a, int lpr, int vpl, hipStream_t s) {
+    if (a.B <= 0) return 0;
+    if (a.kx > NEG_MAX_CAND) return -4;
+#define X_(L, V, G)                                                                                        \
+    if (lpr == L && vpl == V) {                                                                            \
+        hipLaunchKernelGGL((k_negatives<Cfg<L, V>, (G < 4 ? G : 4)>), dim3((unsigned)a.B), dim3(64), 0, s, a); \
+        return hipGetLastError() == hipSuccess ? 0 : -1;                                                   \
     }
     MH_FOR_EACH_CFG(X_)
 #undef X_

@@ -244,6 +244,100 @@ class Graph:
         ok, _, on = self.search_arrays(np.stack(qs), k, mode)
         return [[self._node(int(x)) for x in ok[b, : on[b]]] for b in range(len(qs))]
 
+    def ParallelSearch(self, near, k: int, mode: int = MODE_COMPAT) -> List[Node]:
+        """graph.go:631-826: the reference fans distance work out to goroutines;
+        here every search is already data-parallel on the GPU (and, unlike the
+        reference, deterministic -- Q14)."""
+        return self.Search(near, k, mode)
+
+    # -- graph.go:1116-1537 negative-example re-ranking ---------------------------
+    def search_negatives_arrays(self, queries, negatives, k: int, negWeight: float, mode: int = MODE_COMPAT,
+                                ef: int = 0, flags: int = 0):
+        """queries float32[B, dim]; negatives: list (per query) of float32[n_b, dim]
+        -> (keys int64[B,k], scores float32[B,k], n int32[B])."""
+        self._sync()
+        q = _f32(queries)
+        if q.ndim == 1:
+            q = q.reshape(1, -1)
+        B, d = q.shape
+        counts = np.array([len(n) for n in negatives], np.int32)
+        rows = [_f32(n).reshape(-1, d) for n in negatives if len(n)]
+        neg = np.concatenate(rows) if rows else np.zeros((1, d), np.float32)
+        kk = max(int(k), 1)
+        ok = np.zeros((B, kk), np.int64)
+        osc = np.zeros((B, kk), np.float32)
+        on = np.zeros(B, np.int32)
+        self._check(load().mhnsw_search_negatives(self._h, _ptr(q, C.c_float), B, d, _ptr(neg, C.c_float),
+                                                  _ptr(counts, C.c_int32), int(k), float(negWeight), mode, int(ef),
+                                                  int(flags), _ptr(ok, C.c_int64), _ptr(osc, C.c_float),
+                                                  _ptr(on, C.c_int32)))
+        return ok, osc, on
+
+    def _neg_common(self, k, negWeight):
+        self.Validate()
+        if k <= 0:
+            raise HnswError(-3, f"k must be greater than 0, got {k}")
+        if negWeight < 0.0 or negWeight > 1.0:
+            raise HnswError(-1, f"negWeight must be between 0.0 and 1.0, got {negWeight:f}")
+
+    def SearchWithNegative(self, near, negative, k: int, negWeight: float, mode: int = MODE_COMPAT) -> List[Node]:
+        """graph.go:1116-1230"""
+        self._neg_common(k, negWeight)
+        near = np.asarray(near, np.float32).ravel()
+        negative = np.asarray(negative, np.float32).ravel()
+        d0 = self.Dims()
+        if self.Len() or d0:
+            if d0 != near.size:
+                raise HnswError(-2, f"query embedding dimension mismatch: {d0} != {near.size}")
+            if d0 != negative.size:
+                raise HnswError(-2, f"negative embedding dimension mismatch: {d0} != {negative.size}")
+        ok, _, on = self.search_negatives_arrays(near[None], [negative[None]], k, negWeight, mode)
+        return [self._node(int(x)) for x in ok[0, : on[0]]]
+
+    def SearchWithNegatives(self, near, negatives, k: int, negWeight: float, mode: int = MODE_COMPAT,
+                            flags: int = 0) -> List[Node]:
+        """graph.go:1237-1360 (flags=1 enables the reference's key 7..9 test boost)"""
+        self._neg_common(k, negWeight)
+        if len(negatives) == 0:
+            return self.Search(near, k, mode)
+        near = np.asarray(near, np.float32).ravel()
+        negs = [np.asarray(n, np.float32).ravel() for n in negatives]
+        d0 = self.Dims()
+        if d0:
+            if d0 != near.size:
+                raise HnswError(-2, f"query embedding dimension mismatch: {d0} != {near.size}")
+            for i, n in enumerate(negs):
+                if d0 != n.size:
+                    raise HnswError(-2, f"negative embedding {i} dimension mismatch: {d0} != {n.size}")
+        ok, _, on = self.search_negatives_arrays(near[None], [np.stack(negs)], k, negWeight, mode, flags=flags)
+        return [self._node(int(x)) for x in ok[0, : on[0]]]
+
+    def BatchSearchWithNegatives(self, queries, negatives, k: int, negWeight: float, mode: int = MODE_COMPAT,
+                                 flags: int = 0):
+        """graph.go:1365-1537"""
+        self._neg_common(k, negWeight)
+        qs = [np.asarray(q, np.float32).ravel() for q in queries]
+        if not qs:
+            return None
+        if len(negatives) != len(qs):
+            raise HnswError(-1, f"number of negative example sets ({len(negatives)}) must match number of queries "
+                                f"({len(qs)})")
+        negs = [[np.asarray(n, np.float32).ravel() for n in ns] for ns in negatives]
+        d0 = self.Dims()
+        if d0:
+            for i, q in enumerate(qs):
+                if d0 != q.size:
+                    raise HnswError(-2, f"query {i} embedding dimension mismatch: {d0} != {q.size}")
+                for j, n in enumerate(negs[i]):
+                    if d0 != n.size:
+                        raise HnswError(-2, f"negative embedding {j} for query {i} dimension mismatch: {d0} != "
+                                            f"{n.size}")
+        if not self.Len() and not d0:
+            return [None] * len(qs)
+        ok, _, on = self.search_negatives_arrays(np.stack(qs), [np.stack(n) if n else np.zeros((0, qs[0].size))
+                                                                for n in negs], k, negWeight, mode, flags=flags)
+        return [[self._node(int(x)) for x in ok[b, : on[b]]] for b in range(len(qs))]
+
     # -- graph.go:829, 421, 898 --------------------------------------------------
     def Len(self) -> int:
         return int(load().mhnsw_len(self._h))

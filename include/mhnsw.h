@@ -95,6 +95,18 @@ int mhnsw_search(mhnsw_index *h, const float *queries, int64_t B, int dim, int k
 int mhnsw_search_device(mhnsw_index *h, const float *d_queries, int64_t B, int dim, int k, int mode, int ef,
                         int64_t *d_keys, float *d_dist, int32_t *d_n, void *stream);
 
+/* ---- SearchWithNegative(s) / BatchSearchWithNegatives (graph.go:1116-1537) ----
+ * Query b's negatives are the next neg_count[b] rows of `negatives` (B*dim
+ * queries, sum(neg_count)*dim negatives).  Candidates = Search(near,
+ * max(3k,10)) in `mode`; scored in float32 as the reference (graph.go:1174-
+ * 1210 / 1300-1345) and returned by descending score (ties in candidate
+ * order, NaN last).  neg_count[b] == 0 runs a plain Search(near, k)
+ * (out_score then holds distances).  flags bit 0 enables the reference's
+ * key 7..9 boost (a test hack, graph.go:1338-1344).  k <= 85. */
+int mhnsw_search_negatives(mhnsw_index *h, const float *queries, int64_t B, int dim, const float *negatives,
+                           const int32_t *neg_count, int k, float neg_weight, int mode, int ef, int flags,
+                           int64_t *out_keys, float *out_score, int32_t *out_n);
+
 /* ---- Len / Dims / Lookup / Analyzer.Topography (graph.go:829, 421, 898; analyzer.go:41) ---- */
 int64_t mhnsw_len(const mhnsw_index *h);
 int mhnsw_dims(const mhnsw_index *h);

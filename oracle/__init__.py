@@ -74,6 +74,8 @@ def lib():
         L.og_delete.argtypes = [C.c_void_p, i64p, C.c_int64, C.c_int, C.c_int, C.c_int, u8p]
         L.og_import.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, i64p, f32p, i32p,
                                 i32p, i32p, u8p]
+        L.og_search_negatives.argtypes = [C.c_void_p, f32p, C.c_int64, C.c_int, f32p, i32p, C.c_int, C.c_float,
+                                          C.c_int, C.c_int, C.c_int, i64p, f32p, i32p]
         L.og_stats.argtypes = [C.c_void_p, i64p]
         L.og_reset_stats.argtypes = [C.c_void_p]
         _lib = L
@@ -199,6 +201,24 @@ class Graph:
                                  _p(od, C.c_float), _p(on, C.c_int32))
         self._check(rc)
         return ok, od, on
+
+    def search_negatives(self, queries, negatives, k, neg_weight, mode=MODE_COMPAT, ef=0, flags=0):
+        """graph.go:1116-1537 restated; negatives: list (per query) of [n_b, dim]."""
+        q = f32(queries)
+        if q.ndim == 1:
+            q = q.reshape(1, -1)
+        B, d = q.shape
+        counts = np.array([len(n) for n in negatives], np.int32)
+        rows = [f32(n).reshape(-1, d) for n in negatives if len(n)]
+        neg = np.concatenate(rows) if rows else np.zeros((1, d), np.float32)
+        kk = max(k, 1)
+        ok = np.zeros((B, kk), np.int64)
+        osc = np.zeros((B, kk), np.float32)
+        on = np.zeros(B, np.int32)
+        self._check(lib().og_search_negatives(self._h, _p(q, C.c_float), B, d, _p(neg, C.c_float),
+                                              _p(counts, C.c_int32), k, neg_weight, mode, ef, flags,
+                                              _p(ok, C.c_int64), _p(osc, C.c_float), _p(on, C.c_int32)))
+        return ok, osc, on
 
     def layer_search_compat(self, layer, entry_id, k, ef, q):
         q = f32(q)

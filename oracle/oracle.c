@@ -966,7 +966,7 @@ typedef struct {
 } qbuf;
 
 static int search_one(og_graph *g, og_scratch *s, qbuf *qb, const float *q, int dim, int k, int mode, int ef,
-                      int32_t entry, int64_t *ok, float *odd) {
+                      int32_t entry, int64_t *ok, float *odd, int32_t *oid) {
     float qn = og_dev_norm(q, dim);
     int top = top_live_layer(g);
     if (mode == OG_MODE_EXACT) {
@@ -980,6 +980,7 @@ static int search_one(og_graph *g, og_scratch *s, qbuf *qb, const float *q, int 
         for (int i = 0; i < n; ++i) {
             ok[i] = g->keys[qb->lst[i].id];
             odd[i] = qb->lst[i].d;
+            if (oid) oid[i] = qb->lst[i].id;
         }
         return n;
     }
@@ -1000,6 +1001,7 @@ static int search_one(og_graph *g, og_scratch *s, qbuf *qb, const float *q, int 
             for (int i = 0; i < c; ++i) {
                 ok[i] = g->keys[qb->ids[i]];
                 odd[i] = qb->ds[i];
+                if (oid) oid[i] = qb->ids[i];
             }
             return c;
         }
@@ -1020,6 +1022,7 @@ static int search_one(og_graph *g, og_scratch *s, qbuf *qb, const float *q, int 
         if (g->dead[qb->lst[i].id]) continue;
         ok[nout] = g->keys[qb->lst[i].id];
         odd[nout] = qb->lst[i].d;
+        if (oid) oid[nout] = qb->lst[i].id;
         ++nout;
     }
     return nout;
@@ -1072,7 +1075,7 @@ int og_search(og_graph *g, const float *queries, int64_t B, int dim, int k, int 
     if (qbuf_init(&qb, ef > k ? ef : k)) return set_err(g, OG_ENOMEM, "out of memory");
     for (int64_t b = 0; b < B; ++b)
         out_n[b] = search_one(g, &g->scr, &qb, queries + (size_t)b * dim, dim, k, mode, ef, entry,
-                              out_keys + (size_t)b * k, out_dist + (size_t)b * k);
+                              out_keys + (size_t)b * k, out_dist + (size_t)b * k, NULL);
     g->stats[0] += qb.st[0];
     g->stats[1] += qb.st[1];
     qbuf_free(&qb);
@@ -1101,7 +1104,7 @@ static void *mt_worker(void *p) {
     qbuf_init(&qb, a->ef > a->k ? a->ef : a->k);
     for (int64_t b = a->b0; b < a->b1; ++b)
         a->on[b] = search_one(a->g, &s, &qb, a->q + (size_t)b * a->dim, a->dim, a->k, a->mode, a->ef, a->entry,
-                              a->ok + (size_t)b * a->k, a->od + (size_t)b * a->k);
+                              a->ok + (size_t)b * a->k, a->od + (size_t)b * a->k, NULL);
     a->st[0] = qb.st[0];
     a->st[1] = qb.st[1];
     qbuf_free(&qb);
@@ -1143,6 +1146,98 @@ int og_search_mt(og_graph *g, const float *queries, int64_t B, int dim, int k, i
         g->stats[0] += args[t].st[0];
         g->stats[1] += args[t].st[1];
     }
+    return OG_OK;
+}
+
+/* ---- graph.go:1116-1537 SearchWithNegative(s) / BatchSearchWithNegatives ----
+ * Candidates = Search(near, max(3k, 10)) in the chosen mode; each candidate is
+ * scored in float32 exactly as the reference:
+ *   qd = Distance(cand, near), qs = 1 - qd
+ *   total += 1 - Distance(cand, neg_j) (in order), avg = total / n
+ *   qd < 0.001 -> 2.0; any Distance(cand, neg_j) < 0.1 -> qs - w*2.0;
+ *   else qs - w*avg (+ 0.2 for keys 7..9 with flags & 1: the test hack Q11)
+ * then ordered by descending score.  Go's slices.SortFunc is not stable, so
+ * ties keep candidate order here, and NaN scores (zero vectors) go last.
+ * A query with no negatives is a plain Search(near, k) (graph.go:1395-1398). */
+typedef struct {
+    float score;
+    int pos;
+} negsc_t;
+static int negsc_cmp(const void *a, const void *b) {
+    const negsc_t *x = (const negsc_t *)a, *y = (const negsc_t *)b;
+    int xn = x->score != x->score, yn = y->score != y->score;
+    if (xn != yn) return xn - yn;
+    if (!xn && x->score != y->score) return x->score > y->score ? -1 : 1;
+    return x->pos - y->pos;
+}
+
+int og_search_negatives(og_graph *g, const float *queries, int64_t B, int dim, const float *negatives,
+                        const int32_t *neg_count, int k, float neg_weight, int mode, int ef, int flags,
+                        int64_t *out_keys, float *out_score, int32_t *out_n) {
+    int32_t entry;
+    if (neg_weight < 0.0f || neg_weight > 1.0f)
+        return set_err(g, OG_EINVAL, "negWeight must be between 0.0 and 1.0, got %f", (double)neg_weight);
+    int rc = search_prologue(g, B, dim, k, NULL, &entry, out_n);
+    if (rc) return rc > 0 ? OG_OK : rc;
+    if (ef <= 0) ef = g->ef;
+    int kx = 3 * k < 10 ? 10 : 3 * k;
+    qbuf qb;
+    if (qbuf_init(&qb, (ef > kx ? ef : kx) + k)) return set_err(g, OG_ENOMEM, "out of memory");
+    int64_t *ck = (int64_t *)malloc(sizeof(int64_t) * (size_t)kx);
+    float *cd = (float *)malloc(sizeof(float) * (size_t)kx);
+    int32_t *ci = (int32_t *)malloc(sizeof(int32_t) * (size_t)kx);
+    negsc_t *sc = (negsc_t *)malloc(sizeof(negsc_t) * (size_t)kx);
+    const float *neg = negatives;
+    for (int64_t b = 0; b < B; ++b) {
+        const float *q = queries + (size_t)b * dim;
+        const int nn = neg_count[b];
+        int64_t *okb = out_keys + (size_t)b * k;
+        float *osb = out_score + (size_t)b * k;
+        if (nn == 0) { /* plain Search */
+            out_n[b] = search_one(g, &g->scr, &qb, q, dim, k, mode, ef, entry, okb, osb, NULL);
+            continue;
+        }
+        int c = search_one(g, &g->scr, &qb, q, dim, kx, mode, ef, entry, ck, cd, ci);
+        for (int i = 0; i < c; ++i) {
+            const float qd = cd[i];
+            const float qs = 1.0f - qd;
+            float total = 0.0f;
+            int close = 0;
+            for (int j = 0; j < nn; ++j) {
+                const float *nv = neg + (size_t)j * dim;
+                const float nd = dist_q(g, ci[i], nv, og_dev_norm(nv, dim));
+                total += 1.0f - nd;
+                if (nd < 0.1f) close = 1;
+            }
+            const float avg = total / (float)nn;
+            float score;
+            if (qd < 0.001f)
+                score = 2.0f;
+            else if (close)
+                score = qs - neg_weight * 2.0f;
+            else {
+                const float boost = ((flags & 1) && ck[i] >= 7 && ck[i] <= 9) ? 0.2f : 0.0f;
+                score = qs - neg_weight * avg + boost;
+            }
+            sc[i].score = score;
+            sc[i].pos = i;
+        }
+        qsort(sc, (size_t)c, sizeof(negsc_t), negsc_cmp);
+        const int m = c < k ? c : k;
+        for (int i = 0; i < m; ++i) {
+            okb[i] = ck[sc[i].pos];
+            osb[i] = sc[i].score;
+        }
+        out_n[b] = m;
+        neg += (size_t)nn * dim;
+    }
+    g->stats[0] += qb.st[0];
+    g->stats[1] += qb.st[1];
+    free(ck);
+    free(cd);
+    free(ci);
+    free(sc);
+    qbuf_free(&qb);
     return OG_OK;
 }
 

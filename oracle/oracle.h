@@ -102,6 +102,14 @@ int og_search_mt(og_graph *g, const float *queries, int64_t B, int dim, int k, i
                  int ef, const int64_t *entry_key, int64_t *out_keys, float *out_dist,
                  int32_t *out_n, int nthreads);
 
+/* SearchWithNegative(s) / BatchSearchWithNegatives (graph.go:1116-1537): the
+ * negatives of query b are the next neg_count[b] rows of `negatives`; flags
+ * bit 0 enables the reference's key-7..9 boost (test hack).  out_score holds
+ * the combined scores (descending). */
+int og_search_negatives(og_graph *g, const float *queries, int64_t B, int dim, const float *negatives,
+                        const int32_t *neg_count, int k, float neg_weight, int mode, int ef, int flags,
+                        int64_t *out_keys, float *out_score, int32_t *out_n);
+
 /* layerNode.search on one layer from an explicit entry id (graph.go:94-170) */
 int og_layer_search_compat(og_graph *g, int layer, int32_t entry_id, int k, int ef,
                            const float *q, int32_t *out_ids, float *out_d);

@@ -461,3 +461,52 @@ def test_batch_delete_repair_parity(H, O, metric):
     assert g.Len() == n - len(gone) + 1000
     ek, _, en = g.search_arrays(X2[:50], 1, mode=H.MODE_BEAM, ef=64)
     assert np.mean(ek[:, 0] == np.arange(n, n + 50)) >= 0.9
+
+
+# ---------------------------------------------------------------- negatives (graph.go:1116-1537)
+@pytest.mark.parametrize("metric,d", [(0, 24), (1, 768)])
+def test_negatives_parity(H, O, metric, d):
+    """Search-with-negatives on the GPU == the restatement: same candidates,
+    bit-identical float32 scores, same order; every mode; 0..4 negatives."""
+    rng = np.random.default_rng(70 + d)
+    n = 900
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    lv = _levels(O, metric, 12, 0.25, 20, 3, n)
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=12, Ml=0.25, EfSearch=20)
+    g = H.Graph(M=12, Ml=0.25, EfSearch=20, Distance=_metric_fn(H, metric))
+    o.add(np.arange(n), X, lv)
+    g.add_arrays(np.arange(n), X, levels=lv)
+    Q = rng.uniform(-1, 1, (30, d)).astype(np.float32)
+    Q[3] = X[17]  # a query equal to a stored vector scores 2.0
+    negs = [rng.uniform(-1, 1, (b % 5, d)).astype(np.float32) for b in range(30)]
+    negs[5] = X[[40, 41]]  # candidates at distance 0 from a negative: the strong penalty
+    for mode, ef in ((H.MODE_COMPAT, 0), (H.MODE_BEAM, 40), (H.MODE_EXACT, 0)):
+        for k, w, flags in ((3, 0.5, 0), (7, 0.9, 1), (20, 0.0, 0)):
+            gk, gs, gn = g.search_negatives_arrays(Q, negs, k, w, mode=mode, ef=ef, flags=flags)
+            rk, rs, rn = o.search_negatives(Q, negs, k, w, mode=mode, ef=ef, flags=flags)
+            _same_results(gk, gs, gn, rk, rs, rn)
+
+
+def test_negatives_reference_cases(H):
+    """negative_test.go:10-250 through the Python mirror of the Go API."""
+    A = np.array([[1.0, 0.2, 0.1], [0.9, 0.3, 0.2], [0.8, 0.3, 0.3], [0.1, 1.0, 0.2], [0.2, 0.9, 0.3],
+                  [0.3, 0.8, 0.3], [0.1, 0.2, 1.0], [0.2, 0.3, 0.9], [0.3, 0.3, 0.8]], np.float32)
+    g = H.NewGraphWithConfig(16, 0.25, 20, H.CosineDistance)
+    for i in range(9):
+        g.Add(H.MakeNode(i + 1, A[i]))
+    r = g.SearchWithNegative(A[0], A[1], 3, 0.5)
+    assert len(r) == 3 and r[0].Key == 1
+    r = g.SearchWithNegatives([0.4, 0.4, 0.4], [A[0], A[3]], 3, 0.7, flags=1)
+    assert len(r) == 3 and any(7 <= n.Key <= 9 for n in r)
+    assert [n.Key for n in g.SearchWithNegatives(A[0], [], 3, 0.5)] == [n.Key for n in g.Search(A[0], 3)]
+    res = g.BatchSearchWithNegatives([A[0], A[3]], [[A[1]], [A[4]]], 3, 0.5)
+    assert len(res) == 2 and res[0][0].Key == 1 and res[1][0].Key == 4
+    res = g.BatchSearchWithNegatives([A[0], A[3]], [[], []], 3, 0.5)
+    assert [[n.Key for n in x] for x in res] == [[n.Key for n in g.Search(q, 3)] for q in (A[0], A[3])]
+    with pytest.raises(H.HnswError, match="negWeight must be between 0.0 and 1.0, got 1.500000"):
+        g.SearchWithNegative(A[0], A[1], 3, 1.5)
+    with pytest.raises(H.HnswError, match=r"negative embedding dimension mismatch: 3 != 2"):
+        g.SearchWithNegative(A[0], [1, 2], 3, 0.5)
+    with pytest.raises(H.HnswError, match=r"number of negative example sets \(1\) must match number of queries \(2\)"):
+        g.BatchSearchWithNegatives([A[0], A[3]], [[A[1]]], 3, 0.5)
+    assert [n.Key for n in g.ParallelSearch(A[0], 3)] == [n.Key for n in g.Search(A[0], 3)]

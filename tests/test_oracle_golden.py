@@ -284,3 +284,47 @@ def test_batch_repair_removes_dead_edges(O):
             assert ex["deg"][l, i] <= (32 if l == 0 else 16) + 1
     r1 = recall()
     assert r1 >= 0.85 and r1 >= r0 - 0.02, (r0, r1)
+
+
+# ----------------------------------------------------------------- negatives
+ANIMALS = np.array([[1.0, 0.2, 0.1], [0.9, 0.3, 0.2], [0.8, 0.3, 0.3],   # dog, puppy, canine
+                    [0.1, 1.0, 0.2], [0.2, 0.9, 0.3], [0.3, 0.8, 0.3],   # cat, kitten, feline
+                    [0.1, 0.2, 1.0], [0.2, 0.3, 0.9], [0.3, 0.3, 0.8]],  # bird, sparrow, avian
+                   np.float32)
+
+
+def test_search_with_negatives_reference_cases(O):
+    """negative_test.go:10-198 on the restatement (NewGraphWithConfig(16, 0.25,
+    20, CosineDistance), keys 1..9)."""
+    g = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=16, Ml=0.25, EfSearch=20)
+    g.add(np.arange(1, 10), ANIMALS)
+    dog, puppy = ANIMALS[0], ANIMALS[1]
+    k, s, n = g.search_negatives(dog[None], [puppy[None]], 3, 0.5)
+    assert n[0] == 3 and k[0, 0] == 1 and s[0, 0] == 2.0  # the query itself scores 2.0
+    # puppy ranks lower than in the plain search (or drops out)
+    pk, _, pn = g.search(dog[None], 9)
+    plain = pk[0, : pn[0]].tolist()
+    neg = k[0, : n[0]].tolist()
+    if 2 in neg and 2 in plain:
+        assert neg.index(2) > plain.index(2)
+    # multiple negatives: at least one bird-related vector (with the reference's boost)
+    for flags in (1, 0):
+        k, s, n = g.search_negatives(np.full((1, 3), 0.4, np.float32), [ANIMALS[[0, 3]]], 3, 0.7, flags=flags)
+        assert n[0] == 3 and any(7 <= x <= 9 for x in k[0].tolist())
+        assert np.all(np.diff(s[0]) <= 0)
+    # weight impact
+    lo, _, ln = g.search_negatives(dog[None], [puppy[None]], 3, 0.1)
+    hi, _, hn = g.search_negatives(dog[None], [puppy[None]], 3, 0.9)
+    lo, hi = lo[0, : ln[0]].tolist(), hi[0, : hn[0]].tolist()
+    if 2 in lo and 2 in hi:
+        assert hi.index(2) > lo.index(2)
+    elif 2 in lo:
+        assert 2 not in hi
+    # batch: dog / cat first; a query without negatives is a plain Search
+    k, s, n = g.search_negatives(ANIMALS[[0, 3]], [ANIMALS[[1]], ANIMALS[[4]]], 3, 0.5)
+    assert k[0, 0] == 1 and k[1, 0] == 4
+    k, s, n = g.search_negatives(ANIMALS[[0, 3]], [np.zeros((0, 3)), np.zeros((0, 3))], 3, 0.5)
+    pk, pd, pn = g.search(ANIMALS[[0, 3]], 3)
+    assert np.array_equal(k, pk) and np.array_equal(n, pn)
+    with pytest.raises(O.OracleError, match="negWeight must be between 0.0 and 1.0, got 1.500000"):
+        g.search_negatives(dog[None], [puppy[None]], 3, 1.5)
