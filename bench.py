@@ -52,9 +52,10 @@ def parse():
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--metric", choices=["cosine", "euclidean"], default="cosine")
     p.add_argument("--M", type=int, default=16)
-    p.add_argument("--M0", type=int, default=48)
+    p.add_argument("--M0", type=int, default=40)
     p.add_argument("--efc", type=int, default=400)
     p.add_argument("--keep-pruned", type=int, default=1)
+    p.add_argument("--alpha", type=int, default=115, help="heuristic slack x100 (prune_alpha_pct; 100 = HNSW Alg. 4)")
     p.add_argument("--ef-sweep", default="32,48,64,72,80,96,128,256",
                    help="extra operating points (ef values) reported at N=1; '' disables")
     p.add_argument("--seed", type=int, default=1234)
@@ -168,7 +169,8 @@ def main():
     base_off = shard_range(a.nbase * world, world, rank)[0] if shard else 0
     X = gen_vectors(a.nbase, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=base_off)
     g = H.Graph(M=a.M, Ml=0.25, EfSearch=a.ef, Distance=metric, Rng=a.seed + (rank if shard else 0),
-                build_mode=H.BUILD_BATCH, m0=a.M0, ef_construction=a.efc, heuristic=2, keep_pruned=a.keep_pruned)
+                build_mode=H.BUILD_BATCH, m0=a.M0, ef_construction=a.efc, heuristic=2, keep_pruned=a.keep_pruned,
+                prune_alpha_pct=a.alpha)
     g.reserve(a.nbase, a.dim)
     keys = np.arange(base_off, base_off + a.nbase, dtype=np.int64)
     torch.cuda.synchronize()
@@ -267,7 +269,8 @@ def main():
     if os.path.exists(a.pmc_json):
         try:
             pm = json.load(open(a.pmc_json))
-            want = dict(n=a.nbase, dim=a.dim, batch=a.batch, ef=a.ef, efc=a.efc, m0=a.M0, keep_pruned=a.keep_pruned)
+            want = dict(n=a.nbase, dim=a.dim, batch=a.batch, ef=a.ef, efc=a.efc, m0=a.M0, keep_pruned=a.keep_pruned,
+                        alpha=a.alpha)
             if all(pm.get(k) == v for k, v in want.items()):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
@@ -293,6 +296,7 @@ def main():
                         f"{a.batch} queries/step/GPU (BASELINE configs[1])",
             "n_base": a.nbase * (world if shard else 1), "dim": a.dim, "batch_per_gpu": a.batch, "ef": a.ef,
             "k": a.k, "M": a.M, "M0": a.M0, "ef_construction": a.efc, "keep_pruned": a.keep_pruned,
+            "prune_alpha": a.alpha / 100,
             "parallelism": f"{'shard' if shard else 'replica'}{world}",
         },
         "recall_at_10": round(recall, 4),

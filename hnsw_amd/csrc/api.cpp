@@ -58,6 +58,7 @@ struct mhnsw_index {
     int efc = 0; // 0 => EfSearch
     int heuristic = 1;
     int keep_pruned = 0;
+    int alpha_pct = 100;
     int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
     int vis_log2 = 12;
     int exact_kk = 0;
@@ -424,6 +425,7 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         a.mcap = mcap;
         a.heuristic = h->heuristic;
         a.keep_pruned = h->keep_pruned;
+        a.alpha = (float)h->alpha_pct / 100.0f;
         a.inc_cnt = h->inc_cnt;
         a.inc_src = h->inc_src;
         a.inc_dist = h->inc_dist;
@@ -840,6 +842,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
         h->heuristic = (int)v;
     } else if (n == "keep_pruned") {
         h->keep_pruned = (int)(v != 0);
+    } else if (n == "prune_alpha_pct") {
+        if (v < 50 || v > 400) return fail(h, MHNSW_EINVAL, "prune_alpha_pct must be in [50, 400]");
+        h->alpha_pct = (int)v;
     } else if (n == "batch_min") {
         h->batch_min = (int)std::max<int64_t>(1, v);
     } else if (n == "batch_max") {
@@ -864,6 +869,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "ef_construction") *v = h->efc > 0 ? h->efc : h->ef;
     else if (n == "heuristic") *v = h->heuristic;
     else if (n == "keep_pruned") *v = h->keep_pruned;
+    else if (n == "prune_alpha_pct") *v = h->alpha_pct;
     else if (n == "batch_min") *v = h->batch_min;
     else if (n == "batch_max") *v = h->batch_max;
     else if (n == "batch_ratio_pct") *v = h->batch_ratio_pct;

@@ -299,7 +299,7 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
                 const float cn = a.g.norms[c];
                 st.E += nsel;
                 eval_list<C, G>(a.g, qc, cn, sel, nsel, a.g.metric, [&](float dcs, uint32_t) {
-                    if (dcs < dc) good = false;
+                    if (a.alpha * dcs < dc) good = false;
                 });
             }
             if (good) {
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
                 const float cn = a.g.norms[guard_id(a.g, c)];
                 st.E += nkeep;
                 eval_list<C, G>(a.g, qc, cn, kept, nkeep, a.g.metric, [&](float dcs, uint32_t) {
-                    if (dcs < dcv) good = false;
+                    if (a.alpha * dcs < dcv) good = false;
                 });
             }
             if (good) {

@@ -69,8 +69,9 @@ int mhnsw_get_params(const mhnsw_index *h, int *metric, int *M, double *ml, int 
 int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(seed)) analogue */
 /* engine options: "build_mode", "m0" (layer-0 degree cap, batch mode),
  * "ef_construction" (<= 512), "heuristic" (0 closest-M, 1 HNSW heuristic on new rows,
- * 2 also when a reverse edge overflows a row), "keep_pruned", "batch_min",
- * "batch_max", "batch_ratio_pct", "vis_log2", "exact_kk" */
+ * 2 also when a reverse edge overflows a row), "keep_pruned", "prune_alpha_pct"
+ * (heuristic slack x100: c is dropped when alpha*d(c,kept) < d(u,c); 100 = HNSW
+ * Alg. 4), "batch_min", "batch_max", "batch_ratio_pct", "vis_log2", "exact_kk" */
 int mhnsw_set_option(mhnsw_index *h, const char *name, int64_t value);
 int mhnsw_get_option(const mhnsw_index *h, const char *name, int64_t *value);
 /* Graph.Validate (graph.go:916-937) */

@@ -3,9 +3,15 @@
             throughput on a bounded prefix), plus the resulting recall@10.
   config 5: 1M x 1536 cosine, batch 1024, exact MFMA path: queries/s and
             k_scores TFLOP/s.
+  config 4: 10M x 768 cosine in 8 node-ID range shards of 1.25M (the per-GPU
+            share at 8 GPUs), emulated on ONE GPU: every shard is built and
+            searched with the same queries in turn, the 8 top-k lists are merged
+            with k_merge; reports per-shard search time, merge time, recall vs
+            the sharded exact path, and the projected 8-GPU throughput.
+  4m      : the same 10M vectors as ONE index on one GPU (replica layout).
   compat  : the reference's Search() semantics on the GPU vs the oracle on the
             host, same graph.
-Usage: python tools/bench_configs.py [3] [5] [compat]"""
+Usage: python tools/bench_configs.py [3] [5] [4] [4m] [compat]"""
 import json
 import os
 import sys
@@ -18,6 +24,7 @@ import torch  # noqa: E402
 
 import hnsw_amd as H  # noqa: E402
 from bench import Searcher, gen_vectors, recall_at_k  # noqa: E402
+from hnsw_amd.shard import merge_topk  # noqa: E402
 
 dev = torch.device("cuda")
 which = sys.argv[1:] or ["3", "5", "compat"]
@@ -84,6 +91,73 @@ if "5" in which:
                       "recall": 1.0}), flush=True)
     g.close()
     del X
+
+def build_index(n, off, seed, efc, X=None):
+    if X is None:
+        X = gen_vectors(n, 768, 1234, 12, 1000, dev, "cosine", offset=off)
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=seed, build_mode=H.BUILD_BATCH, m0=48,
+                ef_construction=efc, heuristic=2, keep_pruned=1)
+    g.reserve(n, 768)
+    bt, _ = timed(lambda: g.add_device(np.arange(off, off + n), X.data_ptr(), n, 768))
+    return g, bt
+
+
+if "4" in which:
+    S_, per, B, NGT = 8, 1_250_000, 16384, 2048
+    Q = gen_vectors(B, 768, 1234 + 7777, 12, 1000, dev, "cosine")
+    lists, truth, ms, builds = [], [], [], []
+    for s_ in range(S_):
+        g, bt = build_index(per, s_ * per, 1234 + s_, 400)
+        S = Searcher(g, B, 10, 768, dev)
+        S.run(Q, H.MODE_BEAM, 64)
+        dt, res = timed(lambda: S.run(Q, H.MODE_BEAM, 64), reps=3)
+        lists.append([x.clone() for x in res])
+        truth.append([x.clone() for x in Searcher(g, NGT, 10, 768, dev).run(Q[:NGT], H.MODE_EXACT, 0)])
+        ms.append(dt * 1e3)
+        builds.append(bt)
+        g.close()
+        print(f"shard {s_}: build {bt:.1f}s search {dt * 1e3:.2f} ms", flush=True)
+
+    def stack(ls):
+        return (torch.stack([x[0] for x in ls]), torch.stack([x[1] for x in ls]), torch.stack([x[2] for x in ls]))
+
+    ak, ad, an = stack(lists)
+    merge_topk(ak, ad, an, 10)
+    mt, (mk, md, mn) = timed(lambda: merge_topk(ak, ad, an, 10), reps=5)
+    tk, td, tn = merge_topk(*stack(truth), 10)
+    rec = recall_at_k(mk[:NGT], mn[:NGT], tk, tn, 10)
+    gather_bytes = S_ * B * 10 * 12
+    print(json.dumps({"config": "configs[3] 10M x 768 cosine, 8 node-ID range shards of 1.25M, emulated on 1 GPU",
+                      "batch": B, "ef": 64, "k": 10, "recall_at_10": round(rec, 4),
+                      "shard_search_ms": [round(x, 3) for x in ms], "merge_ms": round(mt * 1e3, 3),
+                      "shard_build_s": [round(x, 2) for x in builds],
+                      "one_gpu_serial_qps": round(B / ((sum(ms) + mt * 1e3) / 1e3), 1),
+                      "projected_8gpu_qps": round(B / ((max(ms) + mt * 1e3) / 1e3), 1),
+                      "allgather_bytes_per_gpu": gather_bytes,
+                      "note": "projection = slowest shard + merge; the RCCL all-gather of the per-shard top-k "
+                              "(B*k*12 B per GPU) is not included"}), flush=True)
+
+if "4m" in which:
+    n, B, NGT = 10_000_000, 16384, 2048
+    X = gen_vectors(n, 768, 1234, 12, 1000, dev, "cosine")
+    Q = gen_vectors(B, 768, 1234 + 7777, 12, 1000, dev, "cosine")
+    g, bt = build_index(n, 0, 1234, 200, X)
+    del X
+    print(f"10M build {bt:.1f}s", flush=True)
+    tk, td, tn = (x.clone() for x in Searcher(g, NGT, 10, 768, dev).run(Q[:NGT], H.MODE_EXACT, 0))
+    S = Searcher(g, B, 10, 768, dev)
+    for ef in (64, 96, 128):
+        S.run(Q, H.MODE_BEAM, ef)
+        g.reset_stats()
+        dt, res = timed(lambda: S.run(Q, H.MODE_BEAM, ef), reps=3)
+        st = g.stats()
+        E = st["search_dist_evals"] / 3 / B
+        rec = recall_at_k(res[0][:NGT], res[2][:NGT], tk, tn, 10)
+        print(json.dumps({"config": "10M x 768 cosine, one index on 1 GPU (replica layout)", "ef_construction": 200,
+                          "build_s": round(bt, 1), "inserts_per_s": round(n / bt, 1), "ef": ef,
+                          "qps": round(B / dt, 1), "recall_at_10": round(rec, 4), "dist_evals_per_query": round(E, 1),
+                          "alg_GBps": round((E * 768 * 4) * B / dt / 1e9, 1)}), flush=True)
+    g.close()
 
 if "compat" in which:
     import oracle as O  # CPU baseline only

@@ -12,6 +12,7 @@ import hnsw_amd as H  # noqa: E402
 from bench import Searcher, gen_vectors, recall_at_k  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+which = sys.argv[2] if len(sys.argv) > 2 else "base"
 dev = torch.device("cuda")
 X = gen_vectors(n, 768, 1234, 12, 1000, dev, "cosine")
 Q = gen_vectors(16384, 768, 1234 + 7777, 12, 1000, dev, "cosine")
@@ -23,7 +24,19 @@ configs = [
     dict(M=16, m0=32, ef_construction=512, heuristic=2, keep_pruned=1),
     dict(M=12, m0=32, ef_construction=400, heuristic=2, keep_pruned=1),
 ]
+if which == "alpha":  # heuristic slack (prune_alpha_pct) on the bench graph
+    configs = [dict(M=16, m0=48, ef_construction=400, heuristic=2, keep_pruned=1, prune_alpha_pct=a)
+               for a in (100, 90, 115, 130)]
+    configs.append(dict(M=16, m0=48, ef_construction=400, heuristic=2, keep_pruned=0, prune_alpha_pct=120))
 EFS = (64, 72, 80, 88, 96)
+if which == "alpha2":  # finer: the ef at which each slack first reaches recall 0.99
+    configs = [dict(M=16, m0=48, ef_construction=400, heuristic=2, keep_pruned=1, prune_alpha_pct=a)
+               for a in (105, 110, 115, 120)]
+    EFS = (48, 56, 64, 72)
+if which == "alpha3":  # slack x layer-0 degree
+    configs = [dict(M=16, m0=m0, ef_construction=400, heuristic=2, keep_pruned=1, prune_alpha_pct=a)
+               for (a, m0) in ((110, 40), (115, 40), (120, 40), (110, 44), (115, 44), (120, 32))]
+    EFS = (56, 64, 72)
 for cfg in configs:
     cfg = dict(cfg)
     M = cfg.pop("M")
