@@ -62,6 +62,8 @@ struct mhnsw_index {
     int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
     int vis_log2 = 12;
     int exact_kk = 0;
+    int exact_precision = 1;
+    int exact_tile = 0;       // bf16x3 GEMM tile variant (exact.hip launch_exact_scores_x3)  // 0: f32-input MFMA scores, 1: bf16x3 split MFMA scores (both certified)
     // shape
     int dim = 0, pitch = 0, lpr = 0, vpl = 0;
     bool layers_exist = false;
@@ -99,6 +101,13 @@ struct mhnsw_index {
     DevBuf<int64_t> nck, nok;
     DevBuf<int32_t> ncn, nci, noff, non;
     DevBuf<float> nos;
+    // exact path: cached bf16 hi/lo planes of the first xsplit_rows rows (rows are
+    // immutable once added; import resets), per-chunk query planes, certificate state
+    DevBuf<uint16_t> xsplit, qsplit;
+    int64_t xsplit_rows = 0, xsplit_plane = 0;  // rows converted; plane stride they were written with
+    DevBuf<float> xbound, xmaxn;
+    DevBuf<uint8_t> xflag;
+    DevBuf<int32_t> xflagged, xnflag;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool have_timing = false;
     // host mirrors
@@ -630,20 +639,59 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
     if (mode == MHNSW_MODE_EXACT) {
         if (k > 64) return fail(h, MHNSW_EUNSUPPORTED, "exact mode supports k <= 64");
         const int kk = h->exact_kk > 0 ? std::min(64, std::max(h->exact_kk, k)) : std::min(64, std::max(2 * k, k + 16));
+        const bool split = h->exact_precision == 1;
         const int64_t ldS = (h->n + 255) / 256 * 256;
         const int64_t budget = (int64_t)4 << 30;  // score workspace bytes
         int64_t qc = std::max<int64_t>(1, std::min<int64_t>(B, budget / (ldS * 4)));
         qc = std::min<int64_t>(qc, 4096);
         if ((r = ensure_buf(h, h->scores, (size_t)qc * ldS)) || (r = ensure_buf(h, h->qnorm, (size_t)B)) ||
-            (r = ensure_buf(h, h->cand, (size_t)qc * kk)))
+            (r = ensure_buf(h, h->cand, (size_t)qc * kk)) || (r = ensure_buf(h, h->xbound, (size_t)qc)) ||
+            (r = ensure_buf(h, h->xflag, (size_t)qc)) || (r = ensure_buf(h, h->xflagged, (size_t)qc)) ||
+            (r = ensure_buf(h, h->xnflag, 1)) || (r = ensure_buf(h, h->xmaxn, 1)))
             return r;
+        if (split) {
+            const int64_t plane = h->capn * h->pitch;
+            if (h->xsplit.n < (size_t)plane * 2 || h->xsplit_plane != plane) {
+                if ((r = ensure_buf(h, h->xsplit, (size_t)plane * 2))) return r;
+                h->xsplit_rows = 0;
+                h->xsplit_plane = plane;
+            }
+            if ((r = ensure_buf(h, h->qsplit, (size_t)qc * h->pitch * 2))) return r;
+        }
         LCHK(h, launch_norms(h->qpad.p, 0, B, h->pitch, h->lpr, h->vpl, h->qnorm.p, s));
         if ((r = sync_layer_table(h))) return r;
         GraphDev g = graph_view(h);
+        // certificate constants (u = 2^-24; gamma_n = n u / (1 - n u) bounds any
+        // order of n-term f32 summation relative to the sum of magnitudes)
+        const double u = std::ldexp(1.0, -24);
+        auto gam = [&](double nn) { return nn * u / (1.0 - nn * u); };
+        const double g_mfma = gam((split ? 3.0 : 1.0) * h->pitch + 1);
+        const double e_split = split ? 3.02 * std::ldexp(1.0, -16) : 0.0;
+        const double g_can = gam(4.0 * h->vpl + 8);  // canonical: 4*VPL fmaf per lane + 6 butterfly levels
+        CertArgs cert{};
+        cert.qnorm = h->qnorm.p;
+        cert.xmax = h->xmaxn.p;
+        cert.eps_cos = (float)(1.01 * ((g_mfma + e_split + g_can) * (1.0 + 1e-4) + 16 * u));
+        cert.eps_dot = (float)(1.01 * (g_mfma + e_split + g_can));
+        cert.c_l2 = (float)(1.01 * (2.0 * gam(4.0 * h->vpl + 10) + 16 * u));
+        cert.flag = h->xflag.p;
+        cert.flagged = h->xflagged.p;
+        cert.nflag = h->xnflag.p;
+        cert.stats = h->d_stats + 3;
         if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
+        if (split && h->xsplit_rows < h->n) {
+            uint16_t* xh = h->xsplit.p;
+            uint16_t* xl = h->xsplit.p + (size_t)h->capn * h->pitch;
+            LCHK(h, launch_split_rows(h->vecs, h->xsplit_rows, h->n, h->pitch, h->capn, xh, xl, s));
+            h->xsplit_rows = h->n;
+        }
+        if (h->metric == EUCLIDEAN) {
+            HIPCHK(h, hipMemsetAsync(h->xmaxn.p, 0, sizeof(float), s));
+            LCHK(h, launch_max_norm(h->norms, h->n, h->xmaxn.p, s));
+        }
         for (int64_t q0 = 0; q0 < B; q0 += qc) {
             const int64_t nb = std::min(qc, B - q0);
-            ExactArgs a;
+            ExactArgs a{};
             a.X = h->vecs;
             a.xnorm = h->norms;
             a.dead = h->any_dead ? h->dead : nullptr;
@@ -658,10 +706,38 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             a.ldS = ldS;
             a.kk = kk;
             a.cand = h->cand.p;
-            LCHK(h, launch_exact_scores(a, s));
+            a.bound = h->xbound.p;
+            int64_t* ok_ = dk + q0 * k;
+            float* od_ = dd + q0 * k;
+            int32_t* on_ = dn + q0;
+            int32_t* oi_ = out_ids ? out_ids + q0 * k : nullptr;
+            if (split) {
+                a.Xh = h->xsplit.p;
+                a.Xl = h->xsplit.p + (size_t)h->capn * h->pitch;
+                a.ldXs = h->capn;
+                a.Qh = h->qsplit.p;
+                a.Ql = h->qsplit.p + (size_t)qc * h->pitch;
+                a.ldQs = qc;
+                LCHK(h, launch_split_rows(a.Q, 0, nb, h->pitch, qc, h->qsplit.p, h->qsplit.p + (size_t)qc * h->pitch, s));
+                LCHK(h, launch_exact_scores_x3(a, h->exact_tile, s));
+            } else {
+                LCHK(h, launch_exact_scores(a, s));
+            }
             LCHK(h, launch_exact_select(a, s));
-            LCHK(h, launch_rerank(a.Q, g, h->cand.p, kk, nb, h->lpr, h->vpl, k, dk + q0 * k, dd + q0 * k, dn + q0,
-                                  out_ids ? out_ids + q0 * k : nullptr, s));
+            HIPCHK(h, hipMemsetAsync(h->xnflag.p, 0, sizeof(int32_t), s));
+            CertArgs c1 = cert;
+            c1.bound = h->xbound.p;
+            c1.qnorm = h->qnorm.p + q0;
+            LCHK(h, launch_rerank(a.Q, g, h->cand.p, kk, nb, h->lpr, h->vpl, k, ok_, od_, on_, oi_, c1, s));
+            // uncertified queries: canonical distances of every row, then select + re-rank again
+            LCHK(h, launch_exact_fallback(a.Q, g, h->n, h->xflagged.p, h->xnflag.p, h->scores.p, ldS, h->lpr, h->vpl, s));
+            ExactArgs a2 = a;
+            a2.only = h->xflag.p;
+            a2.bound = nullptr;
+            LCHK(h, launch_exact_select(a2, s));
+            CertArgs c2{};
+            c2.only = h->xflag.p;
+            LCHK(h, launch_rerank(a.Q, g, h->cand.p, kk, nb, h->lpr, h->vpl, k, ok_, od_, on_, oi_, c2, s));
         }
         if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));
     } else {
@@ -794,6 +870,13 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->noff.p);
     F(h->non.p);
     F(h->nos.p);
+    F(h->xsplit.p);
+    F(h->qsplit.p);
+    F(h->xbound.p);
+    F(h->xmaxn.p);
+    F(h->xflag.p);
+    F(h->xflagged.p);
+    F(h->xnflag.p);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -856,6 +939,11 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
         h->vis_log2 = (int)v;
     } else if (n == "exact_kk") {
         h->exact_kk = (int)v;
+    } else if (n == "exact_tile") {
+        h->exact_tile = (int)v;
+    } else if (n == "exact_precision") {
+        if (v != 0 && v != 1) return fail(h, MHNSW_EINVAL, "exact_precision must be 0 (f32) or 1 (bf16x3)");
+        h->exact_precision = (int)v;
     } else {
         return fail(h, MHNSW_EINVAL, "unknown option '%s'", n.c_str());
     }
@@ -875,6 +963,8 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "batch_ratio_pct") *v = h->batch_ratio_pct;
     else if (n == "vis_log2") *v = h->vis_log2;
     else if (n == "exact_kk") *v = h->exact_kk;
+    else if (n == "exact_precision") *v = h->exact_precision;
+    else if (n == "exact_tile") *v = h->exact_tile;
     else if (n == "pitch") *v = h->pitch;
     else if (n == "capacity") *v = h->capn;
     else return MHNSW_EINVAL;
@@ -1036,6 +1126,7 @@ void reset_graph(mhnsw_index* h) {
     h->layers.clear();
     memset(h->layers_host, 0, sizeof(h->layers_host));
     h->capn = h->n = 0;
+    h->xsplit_rows = h->xsplit_plane = 0;
     h->dim = h->pitch = h->lpr = h->vpl = 0;
     h->layers_exist = h->any_dead = false;
     h->key2id.clear();
@@ -1070,6 +1161,7 @@ int import_csr(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t
     HIPCHK(h, hipMemcpy(h->tmp.p, vecs, (size_t)N * dim * 4, hipMemcpyHostToDevice));
     LCHK(h, launch_pad_rows(h->tmp.p, N, dim, h->vecs, h->pitch, h->stream));
     LCHK(h, launch_norms(h->vecs, 0, N, h->pitch, h->lpr, h->vpl, h->norms, h->stream));
+    h->xsplit_rows = 0;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     std::vector<int32_t> row;
     h->hlevels.assign(N, 0);
@@ -1505,9 +1597,9 @@ int mhnsw_stats(const mhnsw_index* h, int64_t* out, int n) {
     int err = 0;
     HIPCHK(hh, hipMemcpy(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (err & 4) return fail(hh, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
-    const int64_t v[7] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4],
-                          (int64_t)d[5], (int64_t)d[6], h->stats_host[6]};
-    for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
+    const int64_t v[8] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4],
+                          (int64_t)d[5], (int64_t)d[6], h->stats_host[6], (int64_t)d[3]};
+    for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
     return 0;
 }
 

@@ -125,6 +125,10 @@ int launch_build_batch_search(const BatchBuildArgs& a, int lpr, int vpl, hipStre
 int launch_build_batch_commit(const BatchBuildArgs& a, int lpr, int vpl, int64_t n_touched, hipStream_t s);
 
 // ---- exact / merge ----
+// Brute-force path: approximate scores on MFMA (f32-input, or the bf16x3 split
+// hi*hi + hi*lo + lo*hi), top-kk preselection, canonical re-rank of the kk,
+// then a per-query certificate that no row outside the kk can belong to the
+// canonical top-k; uncertified queries are redone by a full canonical sweep.
 struct ExactArgs {
     const float* X;       // [N * pitch]
     const float* xnorm;   // [N]
@@ -138,12 +142,41 @@ struct ExactArgs {
     int64_t ldS;          // row stride of scores (multiple of 4, >= N)
     int kk;               // preselect width (<= 64)
     uint32_t* cand;       // [B * kk]
+    float* bound;         // [B] k_select: kk-th preselected score (+inf when fewer)
+    const uint8_t* only;  // k_select: skip rows b with only[b] == 0 (nullable)
+    const uint16_t* Xh;   // split mode: bf16 hi / lo planes of X, K-blocked (k_split_rows)
+    const uint16_t* Xl;
+    int64_t ldXs;         // rows per K-block of the X planes
+    const uint16_t* Qh;   // split mode: bf16 hi / lo planes of Q, K-blocked
+    const uint16_t* Ql;
+    int64_t ldQs;
 };
-int launch_exact_scores(const ExactArgs& a, hipStream_t s);
+int launch_exact_scores(const ExactArgs& a, hipStream_t s);     // f32-input MFMA
+int launch_exact_scores_x3(const ExactArgs& a, int tile, hipStream_t s);  // bf16x3 split MFMA
 int launch_exact_select(const ExactArgs& a, hipStream_t s);
+int launch_split_rows(const float* src, int64_t r0, int64_t r1, int pitch, int64_t rows, uint16_t* hi, uint16_t* lo,
+                      hipStream_t s);
+int launch_max_norm(const float* norms, int64_t n, float* out, hipStream_t s);
 
+// certificate of the re-rank (nullable pieces disable it)
+struct CertArgs {
+    const float* bound;          // [B] from k_select; nullptr = no certificate
+    const float* qnorm;          // [B]
+    const float* xmax;           // [1] largest row norm (L2)
+    float eps_cos;               // cosine: |approx - canonical| distance bound
+    float eps_dot, c_l2;         // L2: 2*eps_dot*|q|*xmax + c_l2*(|q|+xmax)^2 bounds |approx - canonical^2|
+    uint8_t* flag;               // [B] out: 1 = not certified
+    int32_t* flagged;            // [B] out: list of uncertified rows
+    int32_t* nflag;              // [1] out: list length
+    unsigned long long* stats;   // [0] += uncertified queries
+    const uint8_t* only;         // re-rank only rows with only[b] != 0 (nullable)
+};
 int launch_rerank(const float* Q, const GraphDev& g, const uint32_t* cand, int kk, int64_t B, int lpr, int vpl, int k,
-                  int64_t* out_keys, float* out_dist, int32_t* out_n, int32_t* out_ids, hipStream_t s);
+                  int64_t* out_keys, float* out_dist, int32_t* out_n, int32_t* out_ids, const CertArgs& c,
+                  hipStream_t s);
+// canonical distances of every row for the flagged queries (overwrites their score rows)
+int launch_exact_fallback(const float* Q, const GraphDev& g, int64_t N, const int32_t* flagged, const int32_t* nflag,
+                          float* scores, int64_t ldS, int lpr, int vpl, hipStream_t s);
 
 int launch_merge_topk(const int64_t* keys_in, const float* dist_in, const int32_t* n_in, int shards, int64_t B,
                       int k, int64_t* out_keys, float* out_dist, int32_t* out_n, hipStream_t s);

@@ -6,13 +6,25 @@
 //             |x|^2 - 2 q.x).  128x128x32 block tile, 4 waves of 64x64, LDS
 //             double-buffered, rows padded to 36 floats so the 16-lane groups
 //             of ds_read_b128 hit distinct 16-B slots.
+//  k_scores_x3 : the same scores from the bf16x3 split (x = hi + lo, both
+//             bf16; q.x ~ qh.xh + qh.xl + ql.xh on v_mfma_f32_32x32x16_bf16,
+//             16x the f32-input rate per instruction), 256x256 block tile,
+//             8 waves of 128x64, operands staged by LDS-DMA into a 4-deep
+//             ring of swizzled buffers (three K-stages in flight).
 //  k_select : per query, stream its score row and keep the best kk (<= 64)
-//             (score, id) in a lane-per-entry sorted list (threshold filter).
-//  k_rerank : recompute the kk candidates with the canonical distance engine
-//             and keep the best k by (distance, id) -- bit-identical to the
-//             oracle's brute force whenever the true top-k is inside the
-//             GEMM top-kk.
+//             (score, id) in a lane-per-entry sorted list (threshold filter);
+//             the kk-th score is the query's preselection bound.
+//  k_rerank : recompute the kk candidates with the canonical distance engine,
+//             keep the best k by (distance, id), and certify the query: with
+//             eps bounding |approx - canonical| for every row, no row left
+//             out of the kk can enter the canonical top-k when the k-th
+//             canonical distance is below bound - eps.  Uncertified queries
+//             are redone exactly (k_exact_fallback: canonical distances of
+//             every row, then select + re-rank), so the output is the
+//             oracle's brute force bit for bit.
 //  k_merge  : per query, merge S shard top-k lists by (distance, key).
+#include <algorithm>
+
 #include "device_search.hpp"
 #include "engine.hpp"
 
@@ -123,11 +135,280 @@ __global__ __launch_bounds__(256) void k_scores(ExactArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// bf16x3 split path
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int X3K = 16;  // K-block of the split planes = GEMM K-stage (one 32x32x16 MFMA step)
+
+// round-to-nearest-even f32 -> bf16 bits (NaN stays NaN)
+__device__ __forceinline__ uint32_t bf16_rne(float v) {
+    const uint32_t u = __float_as_uint(v);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float bf16_val(uint32_t h) { return __uint_as_float(h << 16); }
+
+// x = hi + lo + r with hi = bf16(x), lo = bf16(x - hi) (x - hi is exact in f32),
+// |r| <= 2^-16 |x|.  Rows [r0, r1) of a pitch-strided f32 array go to K-blocked
+// planes: element (row, k) at ((k / 16) * rows + row) * 16 + k % 16, so one GEMM
+// K-stage of consecutive rows is a single contiguous run.
+__global__ void k_split_rows(const float* __restrict__ src, int64_t r0, int64_t r1, int pitch, int64_t rows,
+                             uint16_t* __restrict__ hi, uint16_t* __restrict__ lo) {
+    const int q4 = pitch / 4;
+    const int64_t total = (r1 - r0) * (int64_t)q4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = r0 + i / q4;
+        const int k = (int)(i % q4) * 4;
+        const float4 v = *reinterpret_cast<const float4*>(src + row * (int64_t)pitch + k);
+        const uint32_t a0 = bf16_rne(v.x), a1 = bf16_rne(v.y), a2 = bf16_rne(v.z), a3 = bf16_rne(v.w);
+        const uint32_t b0 = bf16_rne(v.x - bf16_val(a0)), b1 = bf16_rne(v.y - bf16_val(a1));
+        const uint32_t b2 = bf16_rne(v.z - bf16_val(a2)), b3 = bf16_rne(v.w - bf16_val(a3));
+        const int64_t o = ((int64_t)(k / X3K) * rows + row) * X3K + (k % X3K);
+        *reinterpret_cast<uint2*>(hi + o) = make_uint2(a0 | (a1 << 16), a2 | (a3 << 16));
+        *reinterpret_cast<uint2*>(lo + o) = make_uint2(b0 | (b1 << 16), b2 | (b3 << 16));
+    }
+}
+
+int launch_split_rows(const float* src, int64_t r0, int64_t r1, int pitch, int64_t rows, uint16_t* hi, uint16_t* lo,
+                      hipStream_t s) {
+    if (r1 <= r0) return 0;
+    if (pitch % X3K || r1 > rows) return -5;
+    const int64_t total = (r1 - r0) * (int64_t)pitch / 4;
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_split_rows, dim3(grid), dim3(256), 0, s, src, r0, r1, pitch, rows, hi, lo);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// largest row norm (NaN skipped) into *out (zeroed by the caller)
+__global__ __launch_bounds__(256) void k_max_norm(const float* __restrict__ norms, int64_t n, float* out) {
+    float m = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = norms[i];
+        if (v > m) m = v;
+    }
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(m));
+}
+
+int launch_max_norm(const float* norms, int64_t n, float* out, hipStream_t s) {
+    if (n <= 0) return 0;
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_max_norm, dim3(grid), dim3(256), 0, s, norms, n, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Block tile BM (queries) x BN (rows) = (WAVES_M*TM*32) x (WAVES_N*TN*32); one
+// K-stage = 16 deep.  LDS image of one stage: [A hi][A lo][B hi][B lo], each
+// rows x 16 bf16 (two 16-B chunks per row); chunk c of row r sits at chunk
+// position c ^ ((r >> 3) & 1), so the 16 consecutive rows one quarter of a
+// ds_read_b128 touches land in 16 distinct 16-B slots of the 256-B bank window.
+template <int WAVES_M, int WAVES_N, int TM, int TN>
+struct X3Tile {
+    static constexpr int BM = WAVES_M * TM * 32, BN = WAVES_N * TN * 32;
+    static constexpr int NT = 64 * WAVES_M * WAVES_N, NW = WAVES_M * WAVES_N;
+    static constexpr int STAGE = (BM + BN) * 2 * X3K;  // bf16 elements per stage
+    static constexpr int PIECES = STAGE * 2 / 1024;     // 1-KiB LDS-DMA pieces per stage
+    static_assert(PIECES % NW == 0, "DMA split");
+    static constexpr int PER = PIECES / NW;
+};
+
+__device__ __forceinline__ int swz16(int r, int c) { return r * X3K + ((c ^ ((r >> 3) & 1)) << 3); }
+
+__device__ __forceinline__ void x3_dma(const uint16_t* src, uint16_t* lds) {
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                     (__attribute__((address_space(3))) void*)(lds), 16, 0, 0);
+}
+
+// one 16-deep K-stage of a wave's TM x TN tiles: q.x += ql.xh + qh.xl + qh.xh
+template <class T, int TM, int TN>
+__device__ __forceinline__ void x3_stage(const uint16_t* base, f32x16 (&acc)[TM][TN], int wm, int wn, int li,
+                                         int lh) {
+    const uint16_t* Ah = base;
+    const uint16_t* Al = base + T::BM * X3K;
+    const uint16_t* Bh = base + 2 * T::BM * X3K;
+    const uint16_t* Bl = Bh + T::BN * X3K;
+    bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int r = wm * TM * 32 + i * 32 + li;
+        ah[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(Ah + swz16(r, lh)));
+        al[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(Al + swz16(r, lh)));
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int r = wn * TN * 32 + j * 32 + li;
+        bh[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(Bh + swz16(r, lh)));
+        bl[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(Bl + swz16(r, lh)));
+    }
+    // small cross terms first, the dominant hi*hi last (one f32 accumulator)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+}
+
+// Staged by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave instruction
+// straight into LDS -- no staging registers, no ds_write pass) into a ring of
+// four buffers, four separate __shared__ objects so the compiler's wait
+// counting can tell which buffer a pending DMA targets.  Stage t lives in
+// buffer t % 4.  Step t: wait for this wave's stage-t pieces (vmcnt leaves
+// stages t+1 and t+2 in flight), barrier (everyone's stage t landed, everyone
+// finished step t-1), issue stage t+3 into the buffer step t-1 read, multiply.
+// The loop is unrolled by four; DMA issue is unconditional (past the end it
+// re-reads the last K-block into a buffer nobody reads) so the in-flight count
+// is the same every step.  A lane's source chunk is pre-swizzled on the global
+// side so the linear LDS-DMA image matches swz16().
+template <int WAVES_M, int WAVES_N, int TM, int TN>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_x3(ExactArgs a) {
+    using T = X3Tile<WAVES_M, WAVES_N, TM, TN>;
+    __shared__ __attribute__((aligned(16))) uint16_t B0[T::STAGE];
+    __shared__ __attribute__((aligned(16))) uint16_t B1[T::STAGE];
+    __shared__ __attribute__((aligned(16))) uint16_t B2[T::STAGE];
+    __shared__ __attribute__((aligned(16))) uint16_t B3[T::STAGE];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    // XCD-aware tile order: round-robin dispatch puts block i on XCD i % 8; give
+    // every XCD a contiguous run of logical tiles, query tiles fastest, so one
+    // base tile is read into an XCD's L2 once and reused by all query tiles.
+    const int64_t nqt = (a.B + T::BM - 1) / T::BM;
+    const int64_t nnt = (a.N + T::BN - 1) / T::BN;
+    const int64_t nblk = nqt * nnt;
+    const int64_t per = nblk / 8, rem = nblk % 8;
+    const int64_t xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
+    const int64_t logical = xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+    const int64_t qt = logical % nqt, nt = logical / nqt;
+    const int64_t q0 = qt * T::BM, n0 = nt * T::BN;
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // this wave's DMA pieces: lane source (K-block 0), K-block stride, LDS offset.
+    // A piece = 32 rows x 32 B of one plane.  Rows past B / N are clamped to
+    // the last row (valid loads; their products land in outputs never stored).
+    const uint16_t* gp[T::PER];
+    int64_t gks[T::PER];
+    int lofs[T::PER];
+#pragma unroll
+    for (int j = 0; j < T::PER; ++j) {
+        const int I = wave * T::PER + j;
+        const int apieces = T::BM / 16;  // 2 planes x BM/32 pieces
+        int r;
+        const uint16_t* base;
+        int64_t row0, rmax, ld;
+        if (I < apieces) {
+            const int plane = I / (T::BM / 32);
+            r = (I % (T::BM / 32)) * 32 + (lane >> 1);
+            base = plane ? a.Ql : a.Qh;
+            row0 = q0;
+            rmax = a.B - 1;
+            ld = a.ldQs;
+        } else {
+            const int I2 = I - apieces;
+            const int plane = I2 / (T::BN / 32);
+            r = (I2 % (T::BN / 32)) * 32 + (lane >> 1);
+            base = plane ? a.Xl : a.Xh;
+            row0 = n0;
+            rmax = a.N - 1;
+            ld = a.ldXs;
+        }
+        const int c = (lane & 1) ^ ((r >> 3) & 1);
+        gp[j] = base + min(row0 + r, rmax) * X3K + c * 8;
+        gks[j] = ld * X3K;
+        lofs[j] = I * 512;
+    }
+    const int nk = a.pitch / X3K;
+    const int li = lane & 31, lh = lane >> 5;
+    auto issue = [&](uint16_t* buf, int k) {
+        const int64_t kb = min(k, nk - 1);
+#pragma unroll
+        for (int j = 0; j < T::PER; ++j) x3_dma(gp[j] + kb * gks[j], buf + lofs[j]);
+    };
+    // vmcnt(2*PER): this wave's pieces of the two newest stages stay in flight
+    constexpr int NW2 = 2 * T::PER;
+    constexpr int WAIT = (NW2 & 15) | ((NW2 >> 4) << 14) | (0x7 << 4) | (0xF << 8);
+    issue(B0, 0);
+    issue(B1, 1);
+    issue(B2, 2);
+    for (int kt = 0; kt < nk; kt += 4) {
+        __builtin_amdgcn_s_waitcnt(WAIT);
+        __builtin_amdgcn_s_barrier();
+        issue(B3, kt + 3);
+        x3_stage<T, TM, TN>(B0, acc, wm, wn, li, lh);
+        __builtin_amdgcn_s_waitcnt(WAIT);
+        __builtin_amdgcn_s_barrier();
+        issue(B0, kt + 4);
+        if (kt + 1 < nk) x3_stage<T, TM, TN>(B1, acc, wm, wn, li, lh);
+        __builtin_amdgcn_s_waitcnt(WAIT);
+        __builtin_amdgcn_s_barrier();
+        issue(B1, kt + 5);
+        if (kt + 2 < nk) x3_stage<T, TM, TN>(B2, acc, wm, wn, li, lh);
+        __builtin_amdgcn_s_waitcnt(WAIT);
+        __builtin_amdgcn_s_barrier();
+        issue(B2, kt + 6);
+        if (kt + 3 < nk) x3_stage<T, TM, TN>(B3, acc, wm, wn, li, lh);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no DMA may land after the workgroup ends
+    // epilogue: D col = lane&31 (base row), row = (r&3) + 8*(r>>2) + 4*(lane>>5) (query)
+    const float inf = __int_as_float(0x7f800000);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int64_t xr = n0 + wn * TN * 32 + j * 32 + li;
+        if (xr >= a.N) continue;
+        const bool xok = !(a.dead && a.dead[xr]);
+        const float xn = a.xnorm[xr];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t qr = q0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (qr >= a.B) continue;
+                const float dot = acc[i][j][r];
+                const float qn = a.qnorm[qr];
+                float sc = a.metric == COSINE ? 1.0f - dot / (qn * xn) : fmaf(-2.f, dot, qn * qn + xn * xn);
+                if (!xok || !(sc == sc)) sc = inf;
+                a.scores[(size_t)qr * a.ldS + xr] = sc;
+            }
+        }
+    }
+}
+
+template <int WM_, int WN_, int TM_, int TN_>
+static int launch_x3_t(const ExactArgs& a, hipStream_t s) {
+    using T = X3Tile<WM_, WN_, TM_, TN_>;
+    const int64_t nqt = (a.B + T::BM - 1) / T::BM, nnt = (a.N + T::BN - 1) / T::BN;
+    hipLaunchKernelGGL((k_scores_x3<WM_, WN_, TM_, TN_>), dim3((unsigned)(nqt * nnt)), dim3(T::NT), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_exact_scores_x3(const ExactArgs& a, int tile, hipStream_t s) {
+    if (a.B <= 0 || a.N <= 0) return 0;
+    if (a.pitch % X3K) return -5;
+    switch (tile) {
+        case 1: return launch_x3_t<2, 4, 2, 2>(a, s);  // 128 x 256, 8 waves of 64 x 64
+        case 2: return launch_x3_t<2, 2, 2, 2>(a, s);  // 128 x 128, 4 waves of 64 x 64
+        default: return launch_x3_t<2, 4, 4, 2>(a, s);  // 256 x 256, 8 waves of 128 x 64
+    }
+}
+
+// ---------------------------------------------------------------------------
 // top-kk preselect per query row (one wave per query)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_select(ExactArgs a) {
     const int64_t b = blockIdx.x;
     if (b >= a.B) return;
+    if (a.only && !a.only[b]) return;
     const int lane = lane_id();
     const float* row = a.scores + (size_t)b * a.ldS;
     const float inf = __int_as_float(0x7f800000);
@@ -167,6 +448,7 @@ __global__ __launch_bounds__(64) void k_select(ExactArgs a) {
         }
     }
     if (lane < kk) a.cand[b * kk + lane] = (L.i[0] == EMPTY_ID) ? EMPTY_ID : (L.i[0] & ID_MASK);
+    if (lane == 0 && a.bound) a.bound[b] = worst;
 }
 
 // ---------------------------------------------------------------------------
@@ -175,16 +457,17 @@ __global__ __launch_bounds__(64) void k_select(ExactArgs a) {
 template <class C, int G>
 __global__ __launch_bounds__(64) void k_rerank(const float* __restrict__ Q, GraphDev g, const uint32_t* cand, int kk,
                                                int64_t B, int k, int64_t* out_keys, float* out_dist, int32_t* out_n,
-                                               int32_t* out_ids) {
+                                               int32_t* out_ids, CertArgs c) {
     const int64_t b = blockIdx.x;
     if (b >= B) return;
+    if (c.only && !c.only[b]) return;
     const int lane = lane_id();
     QReg<C> q;
     load_query(q, Q + (size_t)b * C::PITCH);
     const float qn = query_norm(q);
-    const uint32_t c = lane < kk ? cand[b * kk + lane] : EMPTY_ID;
+    const uint32_t cc = lane < kk ? cand[b * kk + lane] : EMPTY_ID;
     int cnt;
-    const uint32_t cid = compact(c, c != EMPTY_ID, cnt);
+    const uint32_t cid = compact(cc, cc != EMPTY_ID, cnt);
     BList<1> L;
     bl_init(L);
     eval_list<C, G>(g, q, qn, cid, cnt, g.metric, [&](float d, uint32_t u) { bl_insert(L, k, d, u); });
@@ -197,6 +480,75 @@ __global__ __launch_bounds__(64) void k_rerank(const float* __restrict__ Q, Grap
     }
     const int nv = __popcll(__ballot(ok));
     if (lane == 0) out_n[b] = nv;
+    if (c.bound) {
+        const float t = c.bound[b];
+        bool cert = true;
+        if (t < __int_as_float(0x7f800000)) {  // rows were left out of the preselection
+            float dk;
+            uint32_t ik;
+            bl_at(L, k - 1, dk, ik);
+            if (ik == EMPTY_ID) {
+                cert = false;
+            } else if (g.metric == COSINE) {
+                cert = (double)dk < (double)t - (double)c.eps_cos;
+            } else {
+                const double qnd = c.qnorm[b], xm = *c.xmax;
+                const double delta = 2.0 * c.eps_dot * qnd * xm + c.c_l2 * (qnd + xm) * (qnd + xm);
+                cert = (double)dk * (double)dk < (double)t - delta;
+            }
+        }
+        if (lane == 0) {
+            c.flag[b] = cert ? 0 : 1;
+            if (!cert) {
+                c.flagged[atomicAdd(c.nflag, 1)] = (int32_t)b;
+                atomicAdd(c.stats, 1ull);
+            }
+        }
+    }
+}
+
+// Canonical distance of every row for each uncertified query (the same
+// arithmetic as the re-rank: eval_rows + stored canonical norms + finalize),
+// written over that query's score row; deleted rows get +inf.  Blocks stride
+// over row groups; with no flagged query every block exits at once.
+template <class C, int G>
+__global__ __launch_bounds__(256) void k_exact_fallback(const float* __restrict__ Q, GraphDev g, int64_t N,
+                                                        const int32_t* flagged, const int32_t* nflag,
+                                                        float* __restrict__ scores, int64_t ldS) {
+    using RM = RowMap<C, G>;
+    constexpr int GROUP = C::LPR >> RM::LG;
+    const int nf = *nflag;
+    if (nf == 0) return;
+    const int lane = lane_id();
+    const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const int64_t ngroups = (N + RM::T - 1) / RM::T;
+    for (int f = 0; f < nf; ++f) {
+        const int64_t b = flagged[f];
+        QReg<C> q;
+        load_query(q, Q + (size_t)b * C::PITCH);
+        const float qn = query_norm(q);
+        for (int64_t grp = gw; grp < ngroups; grp += nw) {
+            const int64_t base = grp * RM::T;
+            uint32_t ids[G];
+            bool valid[G];
+#pragma unroll
+            for (int gg = 0; gg < G; ++gg) {
+                const int64_t r = base + RM::reg_row(gg, lane);
+                valid[gg] = r < N;
+                ids[gg] = valid[gg] ? (uint32_t)r : 0u;
+            }
+            const float sacc = g.metric == EUCLIDEAN ? eval_rows<C, G, true>(q, g.vecs, g.pitch, ids, valid)
+                                                     : eval_rows<C, G, false>(q, g.vecs, g.pitch, ids, valid);
+            const int64_t rown = base + RM::owned_row(lane);
+            if (rown < N && (lane & (GROUP - 1)) == 0) {
+                const float xn = g.metric == COSINE ? g.norms[rown] : 1.f;
+                float d = finalize(g.metric, sacc, xn, qn);
+                if (g.dead && g.dead[rown]) d = __int_as_float(0x7f800000);
+                scores[(size_t)b * ldS + rown] = d;
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -273,14 +625,29 @@ int launch_exact_select(const ExactArgs& a, hipStream_t s) {
     X(64, 8, 2)
 
 int launch_rerank(const float* Q, const GraphDev& g, const uint32_t* cand, int kk, int64_t B, int lpr, int vpl, int k,
-                  int64_t* out_keys, float* out_dist, int32_t* out_n, int32_t* out_ids, hipStream_t s) {
+                  int64_t* out_keys, float* out_dist, int32_t* out_n, int32_t* out_ids, const CertArgs& c,
+                  hipStream_t s) {
     if (B <= 0) return 0;
     if (k > 64 || kk > 64) return -4;
 #define X_(L, V, G)                                                                                           \
     if (lpr == L && vpl == V) {                                                                               \
         hipLaunchKernelGGL((k_rerank<Cfg<L, V>, G>), dim3((unsigned)B), dim3(64), 0, s, Q, g, cand, kk, B, k, \
-                           out_keys, out_dist, out_n, out_ids);                                               \
+                           out_keys, out_dist, out_n, out_ids, c);                                            \
         return hipGetLastError() == hipSuccess ? 0 : -1;                                                      \
+    }
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return -3;
+}
+
+int launch_exact_fallback(const float* Q, const GraphDev& g, int64_t N, const int32_t* flagged, const int32_t* nflag,
+                          float* scores, int64_t ldS, int lpr, int vpl, hipStream_t s) {
+    if (N <= 0) return 0;
+#define X_(L, V, G)                                                                                          \
+    if (lpr == L && vpl == V) {                                                                              \
+        hipLaunchKernelGGL((k_exact_fallback<Cfg<L, V>, (G < 4 ? G : 4)>), dim3(1024), dim3(256), 0, s, Q, g, N, \
+                           flagged, nflag, scores, ldS);                                                     \
+        return hipGetLastError() == hipSuccess ? 0 : -1;                                                     \
     }
     MH_FOR_EACH_CFG(X_)
 #undef X_

@@ -388,10 +388,10 @@ class Graph:
         return out
 
     def stats(self) -> dict:
-        o = np.zeros(7, np.int64)
-        self._check(load().mhnsw_stats(self._h, _ptr(o, C.c_int64), 7))
+        o = np.zeros(8, np.int64)
+        self._check(load().mhnsw_stats(self._h, _ptr(o, C.c_int64), 8))
         names = ["search_dist_evals", "search_expansions", "visited_resets", "build_dist_evals",
-                 "build_expansions", "dropped_proposals", "searches"]
+                 "build_expansions", "dropped_proposals", "searches", "exact_uncertified"]
         return dict(zip(names, o.tolist()))
 
     def reset_stats(self):

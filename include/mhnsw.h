@@ -71,7 +71,9 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * "ef_construction" (<= 512), "heuristic" (0 closest-M, 1 HNSW heuristic on new rows,
  * 2 also when a reverse edge overflows a row), "keep_pruned", "prune_alpha_pct"
  * (heuristic slack x100: c is dropped when alpha*d(c,kept) < d(u,c); 100 = HNSW
- * Alg. 4), "batch_min", "batch_max", "batch_ratio_pct", "vis_log2", "exact_kk" */
+ * Alg. 4), "batch_min", "batch_max", "batch_ratio_pct", "vis_log2", "exact_kk",
+ * "exact_precision" (exact-mode scoring: 0 f32-input MFMA, 1 bf16x3 split MFMA;
+ * both preselect, re-rank canonically and certify, so results are identical) */
 int mhnsw_set_option(mhnsw_index *h, const char *name, int64_t value);
 int mhnsw_get_option(const mhnsw_index *h, const char *name, int64_t *value);
 /* Graph.Validate (graph.go:916-937) */
@@ -161,7 +163,8 @@ int mhnsw_preview_levels(mhnsw_index *h, int64_t n, int32_t *out);
 
 /* counters: [0] search distance evals, [1] search expansions, [2] visited-set
  * resets, [3] build distance evals, [4] build expansions, [5] dropped reverse
- * proposals, [6] searches issued */
+ * proposals, [6] searches issued, [7] exact-mode queries whose preselection
+ * could not be certified and were redone by a full canonical sweep */
 int mhnsw_stats(const mhnsw_index *h, int64_t *out, int n);
 int mhnsw_reset_stats(mhnsw_index *h);
 /* device time of the last search's main kernel (HIP events on its stream) */

@@ -320,6 +320,75 @@ def test_batch_build_recall_and_exact_parity(H, O, metric):
     _same_results(bk, bd, bn, rk, rd, rn)
 
 
+# ---------------------------------------------------------------- exact path: both scoring precisions
+def _exact_inputs(rng, n, d, nq, metric):
+    X = _clustered(rng, n, d)
+    X[5] = X[17]                      # exact duplicates: ties broken by id
+    X[6] = X[17]
+    Q = _clustered(rng, nq, d)
+    Q[1] = X[40]                      # a query equal to a stored row
+    if metric == 0:
+        X[9] = 0.0                    # zero row: NaN cosine, never returned
+        Q[2] = 0.0                    # zero query: NaN everywhere, no results
+    return X, Q
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("metric,d", [(0, 24), (1, 24), (0, 768), (1, 768), (0, 1536)])
+def test_exact_precision_parity(H, O, metric, d, precision):
+    """Exact mode with f32-input MFMA scores (0) and bf16x3 split scores (1):
+    after the canonical re-rank and the certificate (or its fallback) the
+    output is the oracle's brute force bit for bit."""
+    rng = np.random.default_rng(100 + d + metric)
+    n = 3000 if d < 1536 else 1500
+    X, Q = _exact_inputs(rng, n, d, 96, metric)
+    g = H.Graph(M=8, Ml=0.25, EfSearch=32, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
+                ef_construction=32)
+    g.add_arrays(np.arange(n) * 7 + 3, X)
+    g.set_option("exact_precision", precision)
+    g.reset_stats()
+    gk, gd, gn = g.search_arrays(Q, 10, mode=H.MODE_EXACT)
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=8, M0=16, Ml=0.25, EfSearch=32)
+    o.import_graph(**g.export())
+    rk, rd, rn = o.search(Q, 10, mode=O.MODE_EXACT)
+    _same_results(gk, gd, gn, rk, rd, rn)
+    if metric == 0:
+        assert gn[2] == 0
+    # clustered data leaves wide gaps at the preselection boundary: nearly every
+    # query is certified without the fallback sweep
+    assert g.stats()["exact_uncertified"] <= len(Q) // 4
+    # a deleted row never comes back, in either precision
+    g.Delete(int(gk[0, 0]))
+    gk2, gd2, gn2 = g.search_arrays(Q[:1], 10, mode=H.MODE_EXACT)
+    assert int(gk[0, 0]) not in gk2[0, : gn2[0]].tolist()
+    g.close()
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_exact_certificate_fallback(H, O, metric):
+    """Preselection width kk = k leaves no margin, so the certificate fails for
+    (nearly) every query; the canonical fallback sweep must still reproduce the
+    oracle exactly -- across two score-workspace chunks (B > 4096)."""
+    rng = np.random.default_rng(7 + metric)
+    n, d, B = 400, 24, 4500
+    X, _ = _exact_inputs(rng, n, d, 4, metric)
+    Q = _clustered(rng, B, d)
+    g = H.Graph(M=8, Ml=0.25, EfSearch=32, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
+                ef_construction=32)
+    g.add_arrays(np.arange(n), X)
+    g.set_option("exact_kk", 10)
+    for precision in (1, 0):
+        g.set_option("exact_precision", precision)
+        g.reset_stats()
+        gk, gd, gn = g.search_arrays(Q, 10, mode=H.MODE_EXACT)
+        assert g.stats()["exact_uncertified"] >= B // 2
+        o = O.Graph(metric=metric, order=O.ORDER_DEV, M=8, M0=16, Ml=0.25, EfSearch=32)
+        o.import_graph(**g.export())
+        rk, rd, rn = o.search(Q, 10, mode=O.MODE_EXACT)
+        _same_results(gk, gd, gn, rk, rd, rn)
+    g.close()
+
+
 # ---------------------------------------------------------------- Delete (graph.go:843-895)
 def _live_connectivity(ex):
     out = []

@@ -81,16 +81,45 @@ if "5" in which:
     g.reserve(n, d)
     g.add_device(np.arange(n), X.data_ptr(), n, d)
     S = Searcher(g, B, 10, d, dev)
-    S.run(Q, H.MODE_EXACT, 0)
-    dt, _ = timed(lambda: S.run(Q, H.MODE_EXACT, 0), reps=5)
-    kms = g.last_kernel_ms()
     flops = 2.0 * B * n * d
-    print(json.dumps({"config": "configs[4] 1M x 1536 cosine exact, batch 1024", "queries_per_s": round(B / dt, 1),
-                      "ms_per_batch": round(dt * 1e3, 3), "exact_path_ms_events": round(kms, 3),
-                      "gemm_tflops_end_to_end": round(flops / dt / 1e12, 1), "mfma_f32_peak_tflops": 157.3,
-                      "recall": 1.0}), flush=True)
+    res = {}
+    for prec, name in ((0, "f32"), (1, "bf16x3")):
+        g.set_option("exact_precision", prec)
+        S.run(Q, H.MODE_EXACT, 0)
+        g.reset_stats()
+        dt, out = timed(lambda: S.run(Q, H.MODE_EXACT, 0), reps=5)
+        res[name] = [x.clone() for x in out]
+        kms = g.last_kernel_ms()
+        unc = g.stats()["exact_uncertified"] / 5
+        print(json.dumps({"config": "configs[4] 1M x 1536 cosine exact, batch 1024", "scores": name,
+                          "queries_per_s": round(B / dt, 1), "ms_per_batch": round(dt * 1e3, 3),
+                          "exact_path_ms_events": round(kms, 3),
+                          "fp32_equiv_tflops_end_to_end": round(flops / dt / 1e12, 1),
+                          "uncertified_per_batch": unc, "mfma_f32_peak_tflops": 157.3,
+                          "mfma_bf16_dense_peak_tflops": 2500.0, "recall": 1.0}), flush=True)
+    same = all(torch.equal(a_, b_) for a_, b_ in zip(res["f32"], res["bf16x3"]))
+    print(json.dumps({"config": "configs[4] exact: f32 vs bf16x3 results", "identical": same}), flush=True)
     g.close()
     del X
+
+
+if "5t" in which:  # bf16x3 GEMM tile variants (exact_tile option), same workload as config 5
+    n, d, B = 1_000_000, 1536, 1024
+    X = gen_vectors(n, d, 55, 12, 1000, dev, "cosine")
+    Q = gen_vectors(B, d, 56, 12, 1000, dev, "cosine")
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_BATCH, m0=16,
+                ef_construction=16)
+    g.reserve(n, d)
+    g.add_device(np.arange(n), X.data_ptr(), n, d)
+    S = Searcher(g, B, 10, d, dev)
+    for tile in (1, 2):
+        g.set_option("exact_tile", tile)
+        S.run(Q, H.MODE_EXACT, 0)
+        dt, _ = timed(lambda: S.run(Q, H.MODE_EXACT, 0), reps=5)
+        print(json.dumps({"exact_tile": tile, "ms_per_batch": round(dt * 1e3, 3)}), flush=True)
+    g.close()
+    del X
+
 
 def build_index(n, off, seed, efc, X=None):
     if X is None:
