@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libmhnsw.so")
 COSINE, EUCLIDEAN, NO_DISTANCE = 0, 1, -1
 MODE_COMPAT, MODE_BEAM, MODE_EXACT = 0, 1, 2
 BUILD_COMPAT, BUILD_BATCH = 0, 1
-KEY_INT, KEY_INT64, KEY_INT32, KEY_UINT64, KEY_UINT32 = 0, 1, 2, 3, 4
+KEY_INT, KEY_INT64, KEY_INT32, KEY_UINT64, KEY_UINT32, KEY_STRING = 0, 1, 2, 3, 4, 5
 
 OK, EINVAL, EDIM, EK, ENOMEM, EDEVICE, EUNSUPPORTED, EINTERNAL = 0, -1, -2, -3, -4, -5, -6, -7
 
@@ -56,6 +56,8 @@ SIGNATURES = {
     "mhnsw_import": (C.c_int, [_vp, C.c_int64, C.c_int, C.c_int, C.c_int, _i64p, _f32p, _i32p, _i32p, _i32p,
                                _u8p]),
     "mhnsw_export_go": (C.c_int, [_vp, C.c_int, _u8p, C.c_int64, _i64p]),
+    "mhnsw_strkeys_encode": (C.c_int, [_vp, C.c_char_p, _i64p, C.c_int64, C.c_int, _i64p]),
+    "mhnsw_strkeys_decode": (C.c_int, [_vp, _i64p, C.c_int64, _vp, C.c_int64, _i64p, _i64p]),
     "mhnsw_import_go": (C.c_int, [_vp, _u8p, C.c_int64, C.c_int]),
     "mhnsw_save": (C.c_int, [_vp, C.c_char_p, C.c_int]),
     "mhnsw_load": (C.c_int, [_vp, C.c_char_p, C.c_int]),

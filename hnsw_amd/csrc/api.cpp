@@ -12,6 +12,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <shared_mutex>
 #include <string>
@@ -112,6 +113,12 @@ struct mhnsw_index {
     bool have_timing = false;
     // host mirrors
     std::unordered_map<int64_t, int32_t> key2id;  // live keys only
+    // Go string keys (Graph[string]): order-maintenance labels -- every string
+    // ever added maps to an int64 label in lexicographic order, so the engine's
+    // key comparisons (compat expansion order, tie-breaks) see the string order
+    std::map<std::string, int64_t> s2l;
+    std::unordered_map<int64_t, std::string> l2s;
+    int64_t relabels = 0;
     std::vector<int32_t> hlevels;
     std::vector<uint32_t> hmask;  // bit l: row is in layer l (compat may promote into emptied layers)
     std::vector<uint8_t> hdead;
@@ -965,6 +972,8 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "exact_kk") *v = h->exact_kk;
     else if (n == "exact_precision") *v = h->exact_precision;
     else if (n == "exact_tile") *v = h->exact_tile;
+    else if (n == "strkey_relabels") *v = h->relabels;
+    else if (n == "strkeys") *v = (int64_t)h->s2l.size();
     else if (n == "pitch") *v = h->pitch;
     else if (n == "capacity") *v = h->capn;
     else return MHNSW_EINVAL;
@@ -1133,6 +1142,8 @@ void reset_graph(mhnsw_index* h) {
     h->hlevels.clear();
     h->hmask.clear();
     h->hdead.clear();
+    h->s2l.clear();
+    h->l2s.clear();
 }
 
 int import_csr(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t* keys, const float* vecs,
@@ -1201,8 +1212,80 @@ int import_csr(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t
 
 const char* metric_name(int m) { return m == COSINE ? "cosine" : "euclidean"; }
 
-bool key_fits(int64_t k, int kind) {
+// ---- Go string keys: order-maintenance labels -------------------------------
+constexpr int64_t SK_LO = -(int64_t(1) << 62), SK_HI = int64_t(1) << 62, SK_STEP = int64_t(1) << 32;
+
+// Re-space every label evenly in string order and rewrite the keys stored on
+// the device (every row, deleted ones included -- compat search can still
+// return them) and in key2id.  Entries with label INT64_MIN are new strings
+// that are not on the device yet.
+int strkey_relabel(mhnsw_index* h) {
+    const int64_t n = (int64_t)h->s2l.size();
+    const int64_t step = (int64_t)(((uint64_t)SK_HI - (uint64_t)SK_LO) / (uint64_t)(n + 1));
+    std::unordered_map<int64_t, int64_t> remap;
+    remap.reserve((size_t)n * 2);
+    int64_t i = 1;
+    for (auto& kv : h->s2l) {
+        const int64_t nl = SK_LO + i++ * step;
+        if (kv.second != INT64_MIN) remap[kv.second] = nl;
+        kv.second = nl;
+    }
+    h->l2s.clear();
+    for (auto& kv : h->s2l) h->l2s[kv.second] = kv.first;
+    if (h->n > 0 && !remap.empty()) {
+        std::vector<int64_t> keys((size_t)h->n);
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        HIPCHK(h, hipMemcpy(keys.data(), h->keys, (size_t)h->n * 8, hipMemcpyDeviceToHost));
+        for (auto& k : keys) {
+            auto it = remap.find(k);
+            if (it != remap.end()) k = it->second;
+        }
+        HIPCHK(h, hipMemcpy(h->keys, keys.data(), (size_t)h->n * 8, hipMemcpyHostToDevice));
+    }
+    std::unordered_map<int64_t, int32_t> k2;
+    k2.reserve(h->key2id.size() * 2);
+    for (auto& kv : h->key2id) {
+        auto it = remap.find(kv.first);
+        k2[it != remap.end() ? it->second : kv.first] = kv.second;
+    }
+    h->key2id.swap(k2);
+    h->relabels++;
+    return 0;
+}
+
+// Label for a new string: a fixed step past the ends, the midpoint inside;
+// no room left -> relabel everything.
+int strkey_insert(mhnsw_index* h, const std::string& s) {
+    auto it = h->s2l.emplace(s, INT64_MIN).first;
+    const bool first = it == h->s2l.begin();
+    auto nx = std::next(it);
+    const bool last = nx == h->s2l.end();
+    const int64_t prev = first ? SK_LO : std::prev(it)->second;
+    const int64_t next = last ? SK_HI : nx->second;
+    int64_t lab = INT64_MIN;
+    if (last && !first && next - prev > SK_STEP) lab = prev + SK_STEP;
+    else if (first && !last && next - prev > SK_STEP) lab = next - SK_STEP;
+    else if (next - prev >= 2) lab = prev + (next - prev) / 2;
+    if (lab == INT64_MIN) return strkey_relabel(h);
+    it->second = lab;
+    h->l2s[lab] = s;
+    return 0;
+}
+
+// import: distinct strings (file order) -> labels evenly spaced in string order
+void strkey_table(mhnsw_index* h, const std::vector<std::string>& strs, std::vector<int64_t>& lab) {
+    h->s2l.clear();
+    h->l2s.clear();
+    for (const auto& x : strs) h->s2l.emplace(x, INT64_MIN);
+    (void)strkey_relabel(h);  // nothing on the device yet
+    h->relabels--;
+    lab.resize(strs.size());
+    for (size_t i = 0; i < strs.size(); ++i) lab[i] = h->s2l[strs[i]];
+}
+
+bool key_fits(const mhnsw_index* h, int64_t k, int kind) {
     switch (kind) {
+        case KEY_STRING: return h->l2s.count(k) != 0;
         case KEY_INT32: return k >= INT32_MIN && k <= INT32_MAX;
         case KEY_UINT32: return k >= 0 && k <= (int64_t)UINT32_MAX;
         case KEY_UINT64: return k >= 0;
@@ -1217,6 +1300,7 @@ int export_go(mhnsw_index* h, int key_kind, std::vector<uint8_t>& out) {
     int r = validate(h);
     if (r) return r;
     GoWriter w;
+    w.strs = &h->l2s;
     w.varint(1);  // encodingVersion
     w.varint(h->M);
     w.f64(h->ml);
@@ -1245,7 +1329,7 @@ int export_go(mhnsw_index* h, int key_kind, std::vector<uint8_t>& out) {
         w.varint(Ly.count);
         for (int64_t i = 0; i < N; ++i) {
             if (!in_layer(h, i, l) || h->hdead[i]) continue;
-            if (!key_fits(keys[i], key_kind)) return fail(h, MHNSW_EINVAL, "key %lld does not fit the key type", (long long)keys[i]);
+            if (!key_fits(h, keys[i], key_kind)) return fail(h, MHNSW_EINVAL, "key %lld does not fit the key type", (long long)keys[i]);
             w.key(keys[i], key_kind);
             w.floats(vecs.data() + (size_t)i * h->dim, h->dim);
             const int d = std::min(std::max(deg[i], 0), Ly.cap);
@@ -1274,6 +1358,14 @@ int import_go(mhnsw_index* h, const uint8_t* buf, int64_t size, int key_kind) {
     const int L = (int)gg.layers.size();
     const int64_t N = L ? (int64_t)gg.layers[0].keys.size() : 0;
     reset_graph(h);
+    if (key_kind == KEY_STRING) {  // ordinals -> evenly spaced labels in string order
+        std::vector<int64_t> lab;
+        strkey_table(h, gg.strkeys, lab);
+        for (auto& Ly : gg.layers) {
+            for (auto& k : Ly.keys) k = lab[(size_t)k];
+            for (auto& k : Ly.nb_keys) k = lab[(size_t)k];
+        }
+    }
     if (N == 0) return 0;
     if (L > MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "more than %d layers", MH_MAXL);
     std::unordered_map<int64_t, int32_t> id;
@@ -1625,3 +1717,60 @@ int mhnsw_merge_topk_device(const int64_t* keys_in, const float* dist_in, const 
 }
 
 }  // extern "C"
+
+// ---- Go string keys (Graph[string]) ------------------------------------------
+int mhnsw_strkeys_encode(mhnsw_index* h, const char* blob, const int64_t* offs, int64_t n, int assign,
+                         int64_t* out) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    if (n < 0) return fail(h, MHNSW_EINVAL, "negative key count");
+    std::vector<std::string> ks((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        if (offs[i + 1] < offs[i]) return fail(h, MHNSW_EINVAL, "bad string offsets");
+        ks[(size_t)i].assign(blob + offs[i], (size_t)(offs[i + 1] - offs[i]));
+    }
+    int r;
+    if (assign) {
+        std::vector<const std::string*> fresh;
+        for (const auto& x : ks)
+            if (!h->s2l.count(x)) fresh.push_back(&x);
+        std::sort(fresh.begin(), fresh.end(), [](const std::string* a, const std::string* b) { return *a < *b; });
+        fresh.erase(std::unique(fresh.begin(), fresh.end(), [](const std::string* a, const std::string* b) { return *a == *b; }),
+                    fresh.end());
+        if (!fresh.empty()) {
+            if (fresh.size() * 4 > h->s2l.size()) {  // bulk: one even re-spacing
+                for (const auto* x : fresh) h->s2l.emplace(*x, INT64_MIN);
+                if ((r = strkey_relabel(h))) return r;
+            } else {
+                for (const auto* x : fresh)
+                    if ((r = strkey_insert(h, *x))) return r;
+            }
+        }
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        auto it = h->s2l.find(ks[(size_t)i]);
+        out[i] = it == h->s2l.end() ? INT64_MIN : it->second;
+    }
+    return MHNSW_OK;
+}
+
+int mhnsw_strkeys_decode(mhnsw_index* h, const int64_t* labels, int64_t n, char* blob, int64_t cap, int64_t* offs,
+                         int64_t* need) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    int64_t tot = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        auto it = h->l2s.find(labels[i]);
+        if (it != h->l2s.end()) tot += (int64_t)it->second.size();
+    }
+    if (need) *need = tot;
+    if (!blob || cap < tot) return MHNSW_OK;
+    int64_t o = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        offs[i] = o;
+        auto it = h->l2s.find(labels[i]);
+        if (it == h->l2s.end()) continue;
+        memcpy(blob + o, it->second.data(), it->second.size());
+        o += (int64_t)it->second.size();
+    }
+    offs[n] = o;
+    return MHNSW_OK;
+}

@@ -9,7 +9,7 @@
 
 namespace mh {
 
-bool key_kind_ok(int kind) { return kind >= KEY_INT && kind <= KEY_UINT32; }
+bool key_kind_ok(int kind) { return kind >= KEY_INT && kind <= KEY_STRING; }
 
 // ---- writer -----------------------------------------------------------------
 void GoWriter::varint(int64_t v) {  // binary.PutVarint
@@ -50,6 +50,12 @@ void GoWriter::key(int64_t k, int kind) {
             memcpy(b, &k, 8);
             out.insert(out.end(), b, b + 8);
             return;
+        case KEY_STRING: {
+            static const std::string empty;
+            auto it = strs ? strs->find(k) : decltype(strs->find(k)){};
+            str(strs && it != strs->end() ? it->second : empty);
+            return;
+        }
         default: {
             const uint32_t u = (uint32_t)k;
             memcpy(b, &u, 4);
@@ -64,6 +70,8 @@ namespace {
 struct Reader {
     const uint8_t* p;
     size_t n, i = 0;
+    GoGraph* g = nullptr;                           // KEY_STRING intern table
+    std::unordered_map<std::string, int64_t> sidx;
     // Go errors: io.EOF when nothing could be read, io.ErrUnexpectedEOF when a
     // value is cut short, binary's overflow error for an over-long varint.
     std::string varint(int64_t& v) {
@@ -105,6 +113,21 @@ struct Reader {
                 k = v;
                 return e;
             }
+            case KEY_STRING: {  // encode.go:35-45: varint length, then the bytes
+                int64_t ln = 0;
+                std::string e = varint(ln);
+                if (!e.empty()) return e;
+                if (ln < 0 || (size_t)ln > n - i) return "unexpected EOF";
+                std::string s((const char*)p + i, (size_t)ln);
+                i += (size_t)ln;
+                auto it = sidx.find(s);
+                if (it == sidx.end()) {
+                    it = sidx.emplace(s, (int64_t)g->strkeys.size()).first;
+                    g->strkeys.push_back(s);
+                }
+                k = it->second;
+                return "";
+            }
             default: {
                 uint32_t v;
                 std::string e = bytes(&v, 4);
@@ -116,7 +139,7 @@ struct Reader {
 };
 
 const char* key_type_name(int kind) {
-    static const char* names[] = {"*int", "*int64", "*int32", "*uint64", "*uint32"};
+    static const char* names[] = {"*int", "*int64", "*int32", "*uint64", "*uint32", "*string"};
     return names[kind];
 }
 
@@ -136,6 +159,8 @@ std::string fmt(const char* f, ...) {
 std::string go_decode(const uint8_t* buf, size_t n, int key_kind, GoGraph& g) {
     if (!key_kind_ok(key_kind)) return fmt("unsupported key kind %d", key_kind);
     Reader r{buf, n};
+    r.g = &g;
+    g.strkeys.clear();
     std::string e;
     // multiBinaryRead(r, &version, &h.M, &h.Ml, &h.EfSearch, &dist)
     if (!(e = r.varint(g.version)).empty()) return "reading *int at index 0: " + e;
@@ -178,7 +203,11 @@ std::string go_decode(const uint8_t* buf, size_t n, int key_kind, GoGraph& g) {
             if (!(e = r.varint(nnb)).empty())
                 return fmt("decoding node %lld: reading *int at index 2: %s", (long long)j, e.c_str());
             if (nnb < 0 || (size_t)nnb > n) return fmt("decoding neighbor 0 for node %lld: unexpected EOF", (long long)j);
-            if (!seen.insert(key).second) return fmt("duplicate key %lld in layer %lld", (long long)key, (long long)l);
+            if (!seen.insert(key).second) {
+                if (key_kind == KEY_STRING)
+                    return fmt("duplicate key %s in layer %lld", g.strkeys[(size_t)key].c_str(), (long long)l);
+                return fmt("duplicate key %lld in layer %lld", (long long)key, (long long)l);
+            }
             if (g.dim < 0) g.dim = (int)vl;
             if ((int)vl != g.dim) return fmt("embedding dimension mismatch: %d != %lld", g.dim, (long long)vl);
             L.keys[(size_t)j] = key;

@@ -14,7 +14,7 @@ from typing import Iterable, List, NamedTuple, Optional, Sequence
 
 import numpy as np
 
-from ._lib import (BUILD_BATCH, BUILD_COMPAT, COSINE, EUCLIDEAN, KEY_INT, MODE_BEAM, MODE_COMPAT, MODE_EXACT,
+from ._lib import (BUILD_BATCH, BUILD_COMPAT, COSINE, EUCLIDEAN, KEY_INT, KEY_STRING, MODE_BEAM, MODE_COMPAT, MODE_EXACT,
                    HnswError, check, load)
 
 Vector = np.ndarray
@@ -26,8 +26,44 @@ class Node(NamedTuple):
     Value: Vector
 
 
-def MakeNode(key: int, vec) -> Node:  # graph.go:25-27
-    return Node(int(key), np.asarray(vec, dtype=np.float32))
+def MakeNode(key, vec) -> Node:  # graph.go:25-27
+    return Node(key, np.asarray(vec, dtype=np.float32))
+
+
+# ---- K of Graph[K cmp.Ordered] ------------------------------------------------
+# The engine carries keys as int64 and only ever compares them, so every Go
+# ordered key type travels as an order-preserving int64 image:
+#   int    -> itself (Go int / int64 / int32 / uint32 ranges)
+#   float  -> the IEEE-754 total-order image of the float64 bits (NaN rejected)
+#   str    -> the engine's order labels (mhnsw_strkeys_encode: lexicographic
+#             order of the UTF-8 bytes = Go string order; labels may be
+#             re-spaced by an Add, so they are converted at every call)
+_SIGN = np.uint64(1 << 63)
+
+
+def _float_image(keys) -> np.ndarray:
+    f = np.asarray(keys, np.float64).reshape(-1)
+    if np.isnan(f).any():
+        raise HnswError(-1, "NaN keys are not ordered")
+    b = f.view(np.uint64)
+    neg = (b >> np.uint64(63)).astype(bool)
+    u = np.where(neg, ~b, b | _SIGN)
+    return (u ^ _SIGN).view(np.int64)
+
+
+def _float_key(images: np.ndarray) -> List[float]:
+    u = np.asarray(images, np.int64).view(np.uint64) ^ _SIGN
+    neg = (u >> np.uint64(63)) == 0
+    b = np.where(neg, ~u, u & ~_SIGN)
+    return b.view(np.float64).tolist()
+
+
+def _key_type(key) -> str:
+    if isinstance(key, (str, bytes)):
+        return "str"
+    if isinstance(key, (float, np.floating)):
+        return "float"
+    return "int"
 
 
 def _f32(a) -> np.ndarray:
@@ -108,7 +144,8 @@ class Graph:
         self._h = h
         self.M, self.Ml, self.EfSearch, self.Distance = M, Ml, EfSearch, Distance
         self._rng = int(Rng)
-        self._values = {}
+        self._values = {}  # original key -> value (Node.Value)
+        self._kt = None    # "int" | "float" | "str" once the first key is seen
         self.set_option("build_mode", build_mode)
         for k, v in options.items():
             self.set_option(k, v)
@@ -154,6 +191,54 @@ class Graph:
         self._sync()
         self._check(load().mhnsw_validate(self._h))
 
+    # -- keys: Go K -> the engine's int64 order image ---------------------------
+    def _bind_kt(self, key):
+        kt = _key_type(key)
+        if self._kt is None:
+            self._kt = kt
+        elif kt != self._kt and not (self._kt == "float" and kt == "int"):
+            raise HnswError(-1, f"key type {type(key).__name__} does not match the graph's {self._kt} keys")
+
+    def encode_keys(self, keys, assign: bool = False) -> np.ndarray:
+        """Go keys -> int64 engine keys (string labels: INT64_MIN when unknown
+        and not `assign`)."""
+        keys = list(keys)
+        if not keys:
+            return np.zeros(0, np.int64)
+        self._bind_kt(keys[0])
+        if self._kt == "int":
+            return np.asarray([int(k) for k in keys], np.int64)
+        if self._kt == "float":
+            return _float_image([float(k) for k in keys])
+        bs = [k.encode() if isinstance(k, str) else bytes(k) for k in keys]
+        offs = np.zeros(len(bs) + 1, np.int64)
+        offs[1:] = np.cumsum([len(b) for b in bs])
+        out = np.zeros(len(bs), np.int64)
+        self._check(load().mhnsw_strkeys_encode(self._h, b"".join(bs), _ptr(offs, C.c_int64), len(bs),
+                                                1 if assign else 0, _ptr(out, C.c_int64)))
+        return out
+
+    def decode_keys(self, images) -> list:
+        """int64 engine keys (e.g. from search_arrays) -> Go keys."""
+        images = np.ascontiguousarray(np.asarray(images, np.int64).reshape(-1))
+        if self._kt in (None, "int"):
+            return images.tolist()
+        if self._kt == "float":
+            return _float_key(images)
+        lib = load()
+        need = C.c_int64()
+        self._check(lib.mhnsw_strkeys_decode(self._h, _ptr(images, C.c_int64), len(images), None, 0, None,
+                                             C.byref(need)))
+        buf = C.create_string_buffer(max(need.value, 1))
+        offs = np.zeros(len(images) + 1, np.int64)
+        self._check(lib.mhnsw_strkeys_decode(self._h, _ptr(images, C.c_int64), len(images), buf, need.value,
+                                             _ptr(offs, C.c_int64), C.byref(need)))
+        raw = buf.raw
+        return [raw[offs[i]:offs[i + 1]].decode() for i in range(len(images))]
+
+    def _nodes(self, images) -> List[Node]:
+        return [self._node(k) for k in self.decode_keys(images)]
+
     # -- graph.go:437-531 / 942-1042 --------------------------------------------
     def Add(self, *nodes: Node):
         self.BatchAdd(list(nodes))
@@ -162,7 +247,6 @@ class Graph:
         if not nodes:
             self.Validate()
             return
-        keys = np.array([int(n.Key) for n in nodes], dtype=np.int64)
         vecs = [np.asarray(n.Value, dtype=np.float32).ravel() for n in nodes]
         dims = {v.size for v in vecs}
         if len(dims) != 1:
@@ -171,9 +255,11 @@ class Graph:
             for v in vecs:
                 if v.size != d0:
                     raise HnswError(-2, f"embedding dimension mismatch: {d0} != {v.size}")
+        self._sync()
+        keys = self.encode_keys([n.Key for n in nodes], assign=True)
         self.add_arrays(keys, np.stack(vecs), levels=levels)
         for n, v in zip(nodes, vecs):
-            self._values[int(n.Key)] = v
+            self._values[n.Key] = v
 
     def add_arrays(self, keys, vecs, levels=None):
         """Array form of BatchAdd: keys int64[n], vecs float32[n, dim] (host)."""
@@ -219,7 +305,7 @@ class Graph:
                                                C.c_void_p(keys_ptr), C.c_void_p(dist_ptr), C.c_void_p(n_ptr),
                                                C.c_void_p(stream)))
 
-    def _node(self, key: int) -> Node:
+    def _node(self, key) -> Node:
         v = self._values.get(key)
         if v is None:
             v, _ = self.Lookup(key)
@@ -227,7 +313,7 @@ class Graph:
 
     def Search(self, near, k: int, mode: int = MODE_COMPAT) -> List[Node]:
         ok, _, on = self.search_arrays(np.asarray(near, np.float32).reshape(1, -1), k, mode)
-        return [self._node(int(x)) for x in ok[0, : on[0]]]
+        return self._nodes(ok[0, : on[0]])
 
     def BatchSearch(self, queries: Iterable, k: int, mode: int = MODE_COMPAT) -> List[List[Node]]:
         qs = [np.asarray(q, np.float32).ravel() for q in queries]
@@ -242,7 +328,7 @@ class Graph:
                 if q.size != d0:
                     raise HnswError(-2, f"embedding dimension mismatch for query {i}: {d0} != {q.size}")
         ok, _, on = self.search_arrays(np.stack(qs), k, mode)
-        return [[self._node(int(x)) for x in ok[b, : on[b]]] for b in range(len(qs))]
+        return [self._nodes(ok[b, : on[b]]) for b in range(len(qs))]
 
     def ParallelSearch(self, near, k: int, mode: int = MODE_COMPAT) -> List[Node]:
         """graph.go:631-826: the reference fans distance work out to goroutines;
@@ -292,7 +378,7 @@ class Graph:
             if d0 != negative.size:
                 raise HnswError(-2, f"negative embedding dimension mismatch: {d0} != {negative.size}")
         ok, _, on = self.search_negatives_arrays(near[None], [negative[None]], k, negWeight, mode)
-        return [self._node(int(x)) for x in ok[0, : on[0]]]
+        return self._nodes(ok[0, : on[0]])
 
     def SearchWithNegatives(self, near, negatives, k: int, negWeight: float, mode: int = MODE_COMPAT,
                             flags: int = 0) -> List[Node]:
@@ -310,7 +396,7 @@ class Graph:
                 if d0 != n.size:
                     raise HnswError(-2, f"negative embedding {i} dimension mismatch: {d0} != {n.size}")
         ok, _, on = self.search_negatives_arrays(near[None], [np.stack(negs)], k, negWeight, mode, flags=flags)
-        return [self._node(int(x)) for x in ok[0, : on[0]]]
+        return self._nodes(ok[0, : on[0]])
 
     def BatchSearchWithNegatives(self, queries, negatives, k: int, negWeight: float, mode: int = MODE_COMPAT,
                                  flags: int = 0):
@@ -336,7 +422,7 @@ class Graph:
             return [None] * len(qs)
         ok, _, on = self.search_negatives_arrays(np.stack(qs), [np.stack(n) if n else np.zeros((0, qs[0].size))
                                                                 for n in negs], k, negWeight, mode, flags=flags)
-        return [[self._node(int(x)) for x in ok[b, : on[b]]] for b in range(len(qs))]
+        return [self._nodes(ok[b, : on[b]]) for b in range(len(qs))]
 
     # -- graph.go:829, 421, 898 --------------------------------------------------
     def Len(self) -> int:
@@ -347,12 +433,13 @@ class Graph:
     def Dims(self) -> int:
         return int(load().mhnsw_dims(self._h))
 
-    def Lookup(self, key: int):
-        v = self._values.get(int(key))
+    def Lookup(self, key):
+        v = self._values.get(key)
         if v is not None:
             return v, True
         out = np.zeros(max(self.Dims(), 1), np.float32)
-        found = self._check(load().mhnsw_lookup(self._h, int(key), _ptr(out, C.c_float)))
+        img = int(self.encode_keys([key])[0])
+        found = self._check(load().mhnsw_lookup(self._h, img, _ptr(out, C.c_float)))
         return (out if found else None), bool(found)
 
     def Topography(self) -> List[int]:  # analyzer.go:41-49
@@ -365,19 +452,19 @@ class Graph:
         return out[:n].tolist()
 
     # -- Delete / BatchDelete (graph.go:843-895) -------------------------------
-    def Delete(self, key: int) -> bool:
+    def Delete(self, key) -> bool:
         return self.BatchDelete([key])[0]
 
     def BatchDelete(self, keys) -> List[bool]:
-        keys = np.ascontiguousarray(np.asarray(list(keys) if not isinstance(keys, np.ndarray) else keys).reshape(-1),
-                                    np.int64)
-        out = np.zeros(max(len(keys), 1), np.uint8)
+        orig = list(np.asarray(keys).reshape(-1).tolist()) if isinstance(keys, np.ndarray) else list(keys)
         self._sync()
-        self._check(load().mhnsw_delete(self._h, _ptr(keys, C.c_int64), len(keys), _ptr(out, C.c_uint8)))
-        res = [bool(x) for x in out[:len(keys)]]
-        for key, ok in zip(keys.tolist(), res):
+        imgs = np.ascontiguousarray(self.encode_keys(orig), np.int64)
+        out = np.zeros(max(len(imgs), 1), np.uint8)
+        self._check(load().mhnsw_delete(self._h, _ptr(imgs, C.c_int64), len(imgs), _ptr(out, C.c_uint8)))
+        res = [bool(x) for x in out[:len(imgs)]]
+        for key, ok in zip(orig, res):
             if ok:
-                self._values.pop(int(key), None)
+                self._values.pop(key, None)
         return res
 
     # -- levels / stats / exchange ------------------------------------------------
@@ -418,7 +505,15 @@ class Graph:
         return dict(keys=keys, vecs=vecs, deg=deg, adj=adj, entry=entry[:L], dead=dead[:N])
 
     # -- encode.go:128-262 binary format ------------------------------------------
-    def export_bytes(self, key_kind: int = KEY_INT) -> bytes:
+    def _kind(self, key_kind):
+        if key_kind is None:
+            return KEY_STRING if self._kt == "str" else KEY_INT
+        return key_kind
+
+    def export_bytes(self, key_kind: Optional[int] = None) -> bytes:
+        """encode.go Export; key_kind = the Go key type (default: string for a
+        string-keyed graph, else Go `int`)."""
+        key_kind = self._kind(key_kind)
         self._sync()
         lib = load()
         size = C.c_int64()
@@ -427,16 +522,18 @@ class Graph:
         self._check(lib.mhnsw_export_go(self._h, key_kind, _ptr(buf, C.c_uint8), buf.size, C.byref(size)))
         return buf[: size.value].tobytes()
 
-    def import_bytes(self, data: bytes, key_kind: int = KEY_INT):
+    def import_bytes(self, data: bytes, key_kind: Optional[int] = None):
+        key_kind = self._kind(key_kind)
         buf = np.frombuffer(data, np.uint8).copy() if len(data) else np.zeros(1, np.uint8)
         self._check(load().mhnsw_import_go(self._h, _ptr(buf, C.c_uint8), len(data), key_kind))
         self._values.clear()
+        self._kt = "str" if key_kind == KEY_STRING else "int"
         self._pull_params()
 
-    def Export(self, w, key_kind: int = KEY_INT):  # encode.go:131-176 (w: has .write)
+    def Export(self, w, key_kind: Optional[int] = None):  # encode.go:131-176 (w: has .write)
         w.write(self.export_bytes(key_kind))
 
-    def Import(self, r, key_kind: int = KEY_INT):  # encode.go:181-262 (r: has .read)
+    def Import(self, r, key_kind: Optional[int] = None):  # encode.go:181-262 (r: has .read)
         self.import_bytes(r.read(), key_kind)
 
     def _pull_params(self):
@@ -465,7 +562,8 @@ class SavedGraph(Graph):
 
     Path: str = ""
 
-    def Save(self, key_kind: int = KEY_INT):
+    def Save(self, key_kind: Optional[int] = None):
+        key_kind = self._kind(key_kind)
         self._sync()
         self._check(load().mhnsw_save(self._h, os.fsencode(self.Path), key_kind))
 
@@ -477,6 +575,7 @@ def LoadSavedGraph(path: str, key_kind: int = KEY_INT) -> SavedGraph:  # encode.
     g = SavedGraph(M=16, Ml=0.25, EfSearch=20, Distance=CosineDistance, Rng=time.time_ns())
     g.Path = path
     g._check(load().mhnsw_load(g._h, os.fsencode(path), key_kind))
+    g._kt = "str" if key_kind == KEY_STRING else None
     if g.Len() or os.path.getsize(path):
         g._pull_params()
     return g

@@ -1,12 +1,15 @@
 // hnsw_amd/graph.hpp -- header-only C++17 mirror of the reference's Go API
 // (TFMV/hnsw graph.go:17-27, 305-366, 437-1110; distance.go:12-46) over the C
 // ABI in mhnsw.h.  Same names, argument meaning and error messages; Go's
-// `error` becomes hnsw::Error (empty == nil).  Keys are Go `int`-like
-// integral types (the C ABI carries int64).  Vectors are copied in (the
-// reference aliases caller slices, graph.go:447, 911 -- documented in DESIGN.md).
+// `error` becomes hnsw::Error (empty == nil).  Keys are any Go cmp.Ordered
+// type: integral (the C ABI's int64), floating (their IEEE total-order int64
+// image) or std::string (the engine's order labels, mhnsw_strkeys_encode).
+// Vectors are copied in (the reference aliases caller slices, graph.go:447,
+// 911 -- documented in DESIGN.md).
 #pragma once
 
 #include <cstdint>
+#include <cstring>
 #include <initializer_list>
 #include <map>
 #include <memory>
@@ -63,9 +66,90 @@ struct DistanceFunc {
 inline const DistanceFunc CosineDistance{MHNSW_COSINE, "cosine"};        // distance.go:15-17
 inline const DistanceFunc EuclideanDistance{MHNSW_EUCLIDEAN, "euclidean"};  // distance.go:20-23
 
+// ---- K of Graph[K cmp.Ordered] -> the engine's int64 key -------------------
+// The engine only compares keys, so each key type travels as an
+// order-preserving int64 image.  String labels can be re-spaced by an Add, so
+// they are converted at every call and never cached.
+template <class K, class = void>
+struct KeyCodec;
+
+template <class K>
+struct KeyCodec<K, std::enable_if_t<std::is_integral<K>::value>> {
+    // Go encoding of K (encode.go:72-104): C++ `int` stands for Go `int`
+    // (varint); other 64-/32-bit types for Go int64 / uint64 / uint32
+    // (pass MHNSW_KEY_INT32 explicitly for Go int32 keys)
+    static constexpr int kind = std::is_same<K, int>::value                        ? MHNSW_KEY_INT
+                                : (std::is_signed<K>::value && sizeof(K) == 8)     ? MHNSW_KEY_INT64
+                                : (std::is_unsigned<K>::value && sizeof(K) == 8)   ? MHNSW_KEY_UINT64
+                                : (std::is_unsigned<K>::value && sizeof(K) == 4)   ? MHNSW_KEY_UINT32
+                                                                                   : MHNSW_KEY_INT;
+    static std::vector<int64_t> encode(mhnsw_index*, const std::vector<K>& ks, bool) {
+        return std::vector<int64_t>(ks.begin(), ks.end());
+    }
+    static std::vector<K> decode(mhnsw_index*, const int64_t* v, size_t n) { return std::vector<K>(v, v + n); }
+};
+
+template <class K>
+struct KeyCodec<K, std::enable_if_t<std::is_floating_point<K>::value>> {
+    static constexpr int kind = MHNSW_KEY_INT;  // Go has no float-keyed encoding test; export as images
+    static int64_t image(double f) {
+        uint64_t b;
+        std::memcpy(&b, &f, 8);
+        b = (b >> 63) ? ~b : (b | (uint64_t(1) << 63));
+        return (int64_t)(b ^ (uint64_t(1) << 63));
+    }
+    static double value(int64_t i) {
+        uint64_t u = (uint64_t)i ^ (uint64_t(1) << 63);
+        u = (u >> 63) ? (u & ~(uint64_t(1) << 63)) : ~u;
+        double f;
+        std::memcpy(&f, &u, 8);
+        return f;
+    }
+    static std::vector<int64_t> encode(mhnsw_index*, const std::vector<K>& ks, bool) {
+        std::vector<int64_t> out;
+        for (K k : ks) {
+            if (k != k) throw std::invalid_argument("NaN keys are not ordered");
+            out.push_back(image((double)k));
+        }
+        return out;
+    }
+    static std::vector<K> decode(mhnsw_index*, const int64_t* v, size_t n) {
+        std::vector<K> out;
+        for (size_t i = 0; i < n; ++i) out.push_back((K)value(v[i]));
+        return out;
+    }
+};
+
+template <>
+struct KeyCodec<std::string> {
+    static constexpr int kind = MHNSW_KEY_STRING;
+    static std::vector<int64_t> encode(mhnsw_index* h, const std::vector<std::string>& ks, bool assign) {
+        std::string blob;
+        std::vector<int64_t> offs{0};
+        for (const auto& k : ks) {
+            blob += k;
+            offs.push_back((int64_t)blob.size());
+        }
+        std::vector<int64_t> out(ks.size());
+        if (mhnsw_strkeys_encode(h, blob.data(), offs.data(), (int64_t)ks.size(), assign ? 1 : 0, out.data()) < 0)
+            throw std::runtime_error(mhnsw_last_error(h));
+        return out;
+    }
+    static std::vector<std::string> decode(mhnsw_index* h, const int64_t* v, size_t n) {
+        int64_t need = 0;
+        mhnsw_strkeys_decode(h, v, (int64_t)n, nullptr, 0, nullptr, &need);
+        std::string blob((size_t)need, '\0');
+        std::vector<int64_t> offs(n + 1);
+        mhnsw_strkeys_decode(h, v, (int64_t)n, &blob[0], need, offs.data(), &need);
+        std::vector<std::string> out;
+        for (size_t i = 0; i < n; ++i) out.push_back(blob.substr((size_t)offs[i], (size_t)(offs[i + 1] - offs[i])));
+        return out;
+    }
+};
+
 template <class K>
 class Graph {  // graph.go:305-332
-    static_assert(std::is_integral<K>::value, "hnsw_amd keys are integral (Go int); see INTEGRATION.md");
+    using Codec = KeyCodec<K>;
 
    public:
     const DistanceFunc* Distance = &CosineDistance;
@@ -103,9 +187,9 @@ class Graph {  // graph.go:305-332
         sync();
         if (nodes.empty()) return make_error(mhnsw_validate(h_), h_);
         const size_t d = nodes[0].Value.size();
-        std::vector<int64_t> keys;
+        std::vector<K> ks;
         std::vector<float> flat;
-        keys.reserve(nodes.size());
+        ks.reserve(nodes.size());
         flat.reserve(nodes.size() * d);
         for (const auto& n : nodes) {
             if (n.Value.size() != d) {
@@ -114,13 +198,14 @@ class Graph {  // graph.go:305-332
                                  std::to_string(n.Value.size()),
                              MHNSW_EDIM};
             }
-            keys.push_back((int64_t)n.Key);
+            ks.push_back(n.Key);
             flat.insert(flat.end(), n.Value.begin(), n.Value.end());
         }
+        const std::vector<int64_t> keys = Codec::encode(h_, ks, /*assign=*/true);
         int rc = mhnsw_add(h_, keys.data(), flat.data(), (int64_t)nodes.size(), (int)d,
                            levels ? levels->data() : nullptr);
         if (rc < 0) return make_error(rc, h_);
-        for (const auto& n : nodes) values_[(int64_t)n.Key] = n.Value;
+        for (const auto& n : nodes) values_[n.Key] = n.Value;
         return {};
     }
 
@@ -159,11 +244,10 @@ class Graph {  // graph.go:305-332
                               n.data());
         if (rc < 0) return {{}, make_error(rc, h_)};
         std::vector<std::vector<Node<K>>> out(B);
-        for (size_t b = 0; b < B; ++b)
-            for (int j = 0; j < n[b]; ++j) {
-                const int64_t key = keys[b * kk + j];
-                out[b].push_back(Node<K>{(K)key, lookup_value(key)});
-            }
+        for (size_t b = 0; b < B; ++b) {
+            const std::vector<K> ks = Codec::decode(h_, keys.data() + b * kk, (size_t)n[b]);
+            for (int j = 0; j < n[b]; ++j) out[b].push_back(Node<K>{ks[(size_t)j], lookup_value(ks[(size_t)j])});
+        }
         return {out, {}};
     }
 
@@ -171,10 +255,10 @@ class Graph {  // graph.go:305-332
     int Dims() const { return mhnsw_dims(h_); }      // graph.go:421
 
     std::pair<Vector, bool> Lookup(K key) {  // graph.go:898
-        auto it = values_.find((int64_t)key);
+        auto it = values_.find(key);
         if (it != values_.end()) return {it->second, true};
         Vector v(Dims() > 0 ? Dims() : 1);
-        int found = mhnsw_lookup(h_, (int64_t)key, v.data());
+        int found = mhnsw_lookup(h_, Codec::encode(h_, {key}, false)[0], v.data());
         if (found <= 0) return {{}, false};
         return {v, true};
     }
@@ -193,7 +277,7 @@ class Graph {  // graph.go:305-332
     }
 
     // encode.go:131-176 Export (Go key type K: MHNSW_KEY_INT for `int`, ...)
-    std::pair<std::vector<uint8_t>, Error> Export(int key_kind = MHNSW_KEY_INT) {
+    std::pair<std::vector<uint8_t>, Error> Export(int key_kind = Codec::kind) {
         sync();
         int64_t size = 0;
         int rc = mhnsw_export_go(h_, key_kind, nullptr, 0, &size);
@@ -205,7 +289,7 @@ class Graph {  // graph.go:305-332
     }
 
     // encode.go:181-262 Import: parameters and distance come from the file
-    Error Import(const std::vector<uint8_t>& buf, int key_kind = MHNSW_KEY_INT) {
+    Error Import(const std::vector<uint8_t>& buf, int key_kind = Codec::kind) {
         int rc = mhnsw_import_go(h_, buf.data(), (int64_t)buf.size(), key_kind);
         if (rc < 0) return make_error(rc, h_);
         int metric = 0;
@@ -223,13 +307,13 @@ class Graph {  // graph.go:305-332
         std::vector<bool> res(keys.size(), false);
         if (keys.empty()) return res;
         sync();
-        std::vector<int64_t> k64(keys.begin(), keys.end());
+        std::vector<int64_t> k64 = Codec::encode(h_, keys, false);
         std::vector<uint8_t> out(keys.size());
         if (mhnsw_delete(h_, k64.data(), (int64_t)k64.size(), out.data()) < 0)
             throw std::runtime_error(mhnsw_last_error(h_));
         for (size_t i = 0; i < keys.size(); ++i) {
             res[i] = out[i] != 0;
-            if (res[i]) values_.erase(k64[i]);
+            if (res[i]) values_.erase(keys[i]);
         }
         return res;
     }
@@ -246,17 +330,17 @@ class Graph {  // graph.go:305-332
             seeded_ = Rng;
         }
     }
-    Vector lookup_value(int64_t key) {
+    Vector lookup_value(const K& key) {
         auto it = values_.find(key);
         if (it != values_.end()) return it->second;
         Vector v(Dims() > 0 ? Dims() : 1);
-        mhnsw_lookup(h_, key, v.data());
+        mhnsw_lookup(h_, Codec::encode(h_, {key}, false)[0], v.data());
         return v;
     }
 
     mhnsw_index* h_ = nullptr;
     uint64_t seeded_ = 0;
-    std::map<int64_t, Vector> values_;
+    std::map<K, Vector> values_;
 };
 
 // graph.go:340-348

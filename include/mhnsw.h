@@ -152,7 +152,8 @@ int mhnsw_import(mhnsw_index *h, int64_t N, int dim, int L, int cap, const int64
  * file) and reports the reference's errors ("unknown distance function %q",
  * "incompatible encoding version: %d", ...).  Save writes path.tmp then
  * renames; Load of a missing or empty file leaves the graph empty. */
-enum { MHNSW_KEY_INT = 0, MHNSW_KEY_INT64 = 1, MHNSW_KEY_INT32 = 2, MHNSW_KEY_UINT64 = 3, MHNSW_KEY_UINT32 = 4 };
+enum { MHNSW_KEY_INT = 0, MHNSW_KEY_INT64 = 1, MHNSW_KEY_INT32 = 2, MHNSW_KEY_UINT64 = 3, MHNSW_KEY_UINT32 = 4,
+       MHNSW_KEY_STRING = 5 /* Go string keys: the labels of mhnsw_strkeys_encode */ };
 int mhnsw_export_go(mhnsw_index *h, int key_kind, uint8_t *buf, int64_t cap, int64_t *size);
 int mhnsw_import_go(mhnsw_index *h, const uint8_t *buf, int64_t size, int key_kind);
 int mhnsw_save(mhnsw_index *h, const char *path, int key_kind);
@@ -169,6 +170,23 @@ int mhnsw_stats(const mhnsw_index *h, int64_t *out, int n);
 int mhnsw_reset_stats(mhnsw_index *h);
 /* device time of the last search's main kernel (HIP events on its stream) */
 int mhnsw_last_kernel_ms(mhnsw_index *h, float *ms);
+
+/* ---- Go string keys (Graph[string], graph.go:305 K = string) ----
+ * The engine compares keys only by order (graph.go:137 expansion order, map
+ * order stand-ins), so a string key travels as an int64 order label: every
+ * string ever added gets a label and labels follow lexicographic (Go string)
+ * order.  encode: n strings (blob + offs[n+1]) -> labels; with `assign` new
+ * strings get labels (a new string between two adjacent labels may re-space
+ * all labels: the stored keys are rewritten, so earlier labels go stale --
+ * hosts convert at every call, never cache), without it unknown strings give
+ * INT64_MIN.  decode: labels -> strings (blob + offs[n+1]); `need` = bytes;
+ * blob == NULL or cap < need only reports `need`.  Unknown labels decode to
+ * "".  Options "strkeys" / "strkey_relabels" report the table size and the
+ * number of re-spacings. */
+int mhnsw_strkeys_encode(mhnsw_index *h, const char *blob, const int64_t *offs, int64_t n, int assign,
+                         int64_t *out);
+int mhnsw_strkeys_decode(mhnsw_index *h, const int64_t *labels, int64_t n, char *blob, int64_t cap,
+                         int64_t *offs, int64_t *need);
 
 /* ---- multi-GPU: merge per-shard top-k lists (device pointers) ----
  * inputs [shards][B][k] (+ n_in [shards][B]); output best k by (dist, key). */

@@ -165,6 +165,44 @@ static void TestGraph_ExportImport() {
         REQUIRE(n1.first[i] == n2.first[i], "Search nodes");
 }
 
+// Graph[string] (examples/optimized_distance/main.go:82, vector/example/main.go:79):
+// string keys are ordered labels inside the engine; Search, Lookup, Delete and
+// the string encoding (encode.go:78-87) round-trip the caller's strings.
+static void TestGraph_StringKeys() {
+    hnsw::Graph<std::string> g(8, 0.25, 20, &hnsw::CosineDistance, 1);
+    const char* words[] = {"apple", "banana", "cherry", "date", "elderberry", "fig", "grape", "honeydew",
+                           "kiwi", "lemon", "mango", "nectarine", "orange", "papaya", "quince", "raspberry"};
+    for (int i = 0; i < 16; ++i) {
+        hnsw::Vector v(8);
+        for (int j = 0; j < 8; ++j) v[j] = (float)((i * 7 + j * 3) % 11) + 0.5f * (float)(i == j);
+        REQUIRE(!g.Add(hnsw::MakeNode(std::string(words[i]), v)), "add string key");
+    }
+    REQUIRE(g.Len() == 16, "len 16");
+    auto look = g.Lookup("kiwi");
+    REQUIRE(look.second && look.first.size() == 8, "Lookup string");
+    auto s = g.Search(look.first, 1, MHNSW_MODE_EXACT);
+    REQUIRE(!s.second && s.first.size() == 1 && s.first[0].Key == "kiwi", "Search returns the string key");
+    REQUIRE(g.Delete("kiwi") && !g.Delete("kiwi") && !g.Delete("zucchini"), "Delete string key");
+    auto ex = g.Export();
+    REQUIRE(!ex.second && !ex.first.empty(), "Export string keys");
+    hnsw::Graph<std::string> g2;
+    REQUIRE(!g2.Import(ex.first), "Import string keys");
+    REQUIRE(g2.Len() == 15 && g2.Lookup("lemon").second && !g2.Lookup("kiwi").second, "imported keys");
+    auto a = g.Search(look.first, 5, MHNSW_MODE_EXACT), b = g2.Search(look.first, 5, MHNSW_MODE_EXACT);
+    REQUIRE(!a.second && !b.second && a.first.size() == b.first.size(), "imported search");
+    for (size_t i = 0; i < a.first.size() && i < b.first.size(); ++i)
+        REQUIRE(a.first[i].Key == b.first[i].Key, "imported search keys");
+}
+
+// K = float64: ordered by value (negative, zero, positive)
+static void TestGraph_FloatKeys() {
+    hnsw::Graph<double> g(6, 0.5, 20, &hnsw::EuclideanDistance, 0);
+    for (int i = 0; i < 64; ++i) REQUIRE(!g.Add(hnsw::MakeNode(-3.25 + 0.125 * i, {(float)i})), "add float key");
+    auto s = g.Search({17.f}, 1, MHNSW_MODE_EXACT);
+    REQUIRE(!s.second && s.first.size() == 1 && s.first[0].Key == -3.25 + 0.125 * 17, "float key round trip");
+    REQUIRE(g.Delete(-3.25) && g.Len() == 63, "delete float key");
+}
+
 int main() {
     TestDistances();
     Test_layerNode_search();
@@ -175,6 +213,8 @@ int main() {
     TestBatchDelete();
     TestGraph_AddDelete();
     TestGraph_ExportImport();
+    TestGraph_StringKeys();
+    TestGraph_FloatKeys();
     std::printf("%s (%d failures)\n", failures ? "FAIL" : "PASS", failures);
     return failures;
 }

@@ -17,7 +17,7 @@ import struct
 
 import numpy as np
 
-KEY_INT, KEY_INT64, KEY_INT32, KEY_UINT64, KEY_UINT32 = 0, 1, 2, 3, 4
+KEY_INT, KEY_INT64, KEY_INT32, KEY_UINT64, KEY_UINT32, KEY_STRING = 0, 1, 2, 3, 4, 5
 _FIXED = {KEY_INT64: "<q", KEY_INT32: "<i", KEY_UINT64: "<Q", KEY_UINT32: "<I"}
 
 
@@ -57,13 +57,20 @@ def read_varint(buf: bytes, pos: int):
     raise GoError("binary: varint overflows a 64-bit integer")
 
 
-def put_key(k: int, kind: int) -> bytes:
+def put_key(k, kind: int) -> bytes:
+    if kind == KEY_STRING:  # encode.go:78-87: varint length + bytes
+        return put_string(k)
     return put_varint(k) if kind == KEY_INT else struct.pack(_FIXED[kind], k)
 
 
 def read_key(buf, pos, kind):
     if kind == KEY_INT:
         return read_varint(buf, pos)
+    if kind == KEY_STRING:  # encode.go:35-45
+        n, pos = read_varint(buf, pos)
+        if pos + n > len(buf):
+            raise GoError("unexpected EOF")
+        return buf[pos:pos + n].decode(), pos + n
     fmt = _FIXED[kind]
     n = struct.calcsize(fmt)
     if pos + n > len(buf):
@@ -93,9 +100,11 @@ def encode(M, Ml, EfSearch, dist, layers, kind=KEY_INT) -> bytes:
     return b"".join(out)
 
 
-def encode_export(ex, M, Ml, EfSearch, dist, kind=KEY_INT) -> bytes:
+def encode_export(ex, M, Ml, EfSearch, dist, kind=KEY_INT, keymap=None) -> bytes:
     """An engine/oracle CSR export in the engine's canonical order: live
-    members in id order, neighbour keys ascending."""
+    members in id order, neighbour keys ascending (`keymap`: engine key ->
+    Go key, e.g. string labels -> strings; order-preserving)."""
+    km = keymap or (lambda x: x)
     keys, vecs, deg, adj = ex["keys"], ex["vecs"], ex["deg"], ex["adj"]
     dead = ex.get("dead", np.zeros(len(keys), np.uint8))
     layers = []
@@ -105,7 +114,7 @@ def encode_export(ex, M, Ml, EfSearch, dist, kind=KEY_INT) -> bytes:
             if deg[l, i] == -2 or dead[i]:
                 continue
             d = max(int(deg[l, i]), 0)
-            nodes.append((int(keys[i]), vecs[i], sorted(int(keys[j]) for j in adj[l, i, :d])))
+            nodes.append((km(int(keys[i])), vecs[i], [km(k) for k in sorted(int(keys[j]) for j in adj[l, i, :d])]))
         layers.append(nodes)
     return encode(M, Ml, EfSearch, dist, layers, kind)
 
