@@ -5,14 +5,15 @@ as hand-written HIP kernels for gfx950 behind a C ABI (include/mhnsw.h,
 hnsw_amd/libmhnsw.so).  This package is the host-side mirror of the reference's
 Go API (Graph, Node, CosineDistance, ...).  There is no CPU fallback.
 """
-from ._lib import (BUILD_BATCH, BUILD_COMPAT, COSINE, EUCLIDEAN, KEY_INT, KEY_INT32, KEY_INT64, KEY_STRING, KEY_UINT32,
+from ._lib import (BUILD_BATCH, BUILD_COMPAT, BUILD_FLAT, COSINE, EUCLIDEAN, KEY_INT, KEY_INT32, KEY_INT64, KEY_STRING, KEY_UINT32,
                    KEY_UINT64, MODE_BEAM, MODE_COMPAT, MODE_EXACT, HnswError, LIB_PATH, SIGNATURES, load)
 from .graph import (CosineDistance, DistanceFunc, EuclideanDistance, Graph, LoadSavedGraph, MakeNode, NewGraph,
                     NewGraphWithConfig, Node, RegisterDistanceFunc, SavedGraph, Vector, distance_func_to_name,
                     merge_topk_device)
+from .adapters import ExactAdapter, ExactIndex, HNSWAdapter
 
 __all__ = [
-    "BUILD_BATCH", "BUILD_COMPAT", "COSINE", "EUCLIDEAN", "MODE_BEAM", "MODE_COMPAT", "MODE_EXACT", "HnswError",
+    "BUILD_BATCH", "BUILD_COMPAT", "BUILD_FLAT", "ExactIndex", "ExactAdapter", "HNSWAdapter", "KEY_STRING", "COSINE", "EUCLIDEAN", "MODE_BEAM", "MODE_COMPAT", "MODE_EXACT", "HnswError",
     "LIB_PATH", "SIGNATURES", "load", "CosineDistance", "DistanceFunc", "EuclideanDistance", "Graph", "MakeNode",
     "NewGraph", "NewGraphWithConfig", "Node", "RegisterDistanceFunc", "Vector", "distance_func_to_name",
     "merge_topk_device", "KEY_INT", "KEY_INT32", "KEY_INT64", "KEY_UINT32", "KEY_UINT64", "LoadSavedGraph",

@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libmhnsw.so")
 
 COSINE, EUCLIDEAN, NO_DISTANCE = 0, 1, -1
 MODE_COMPAT, MODE_BEAM, MODE_EXACT = 0, 1, 2
-BUILD_COMPAT, BUILD_BATCH = 0, 1
+BUILD_COMPAT, BUILD_BATCH, BUILD_FLAT = 0, 1, 2
 KEY_INT, KEY_INT64, KEY_INT32, KEY_UINT64, KEY_UINT32, KEY_STRING = 0, 1, 2, 3, 4, 5
 
 OK, EINVAL, EDIM, EK, ENOMEM, EDEVICE, EUNSUPPORTED, EINTERNAL = 0, -1, -2, -3, -4, -5, -6, -7

@@ -523,6 +523,7 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
             seen[keys[i]] = 1;
         }
     }
+    const bool flat = h->build_mode == MHNSW_BUILD_FLAT;  // no graph: every row in layer 0, no links
     if (h->build_mode == MHNSW_BUILD_COMPAT && h->M + 1 > 64)
         return fail(h, MHNSW_EUNSUPPORTED, "compat build supports M <= 63");
     if (m0_of(h) + 1 > 64 || h->M + 1 > 64) return fail(h, MHNSW_EUNSUPPORTED, "degree caps above 63 unsupported");
@@ -533,7 +534,9 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     std::vector<int32_t> lv(n);
     bool le = h->layers_exist;
     for (int64_t i = 0; i < n; ++i) {
-        if (levels) {
+        if (flat) {
+            lv[i] = 0;
+        } else if (levels) {
             lv[i] = levels[i];
             if (lv[i] < 0) return fail(h, MHNSW_EINVAL, "invalid level: %d", lv[i]);
         } else {
@@ -587,7 +590,9 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     }
     h->layers_exist = true;
     h->n = n1;
-    if (compat)
+    if (flat)
+        r = 0;
+    else if (compat)
         r = run_build_compat(h, n0, n1, top0);
     else
         r = run_build_batch(h, n0, n1, top_live, entry_live);
@@ -606,6 +611,8 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         return fail(h, MHNSW_EDIM, "embedding dimension mismatch for query %d: %d != %d", 0, h->dim, dim);
     }
     if (mode < 0 || mode > 2) return fail(h, MHNSW_EINVAL, "unknown search mode %d", mode);
+    if (h->build_mode == MHNSW_BUILD_FLAT && mode != MHNSW_MODE_EXACT)
+        return fail(h, MHNSW_EUNSUPPORTED, "flat index (build_mode 2) supports exact search only");
     if (B <= 0) return 0;
     if (!h->layers_exist || live_count(h) == 0) {  // graph.go:554-556: nil, nil
         if (on_device)
@@ -919,7 +926,8 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
     std::string n(name ? name : "");
     if (n == "build_mode") {
-        if (v != MHNSW_BUILD_COMPAT && v != MHNSW_BUILD_BATCH) return fail(h, MHNSW_EINVAL, "bad build_mode");
+        if (v != MHNSW_BUILD_COMPAT && v != MHNSW_BUILD_BATCH && v != MHNSW_BUILD_FLAT)
+            return fail(h, MHNSW_EINVAL, "bad build_mode");
         if (h->n > 0 && v != h->build_mode) return fail(h, MHNSW_EINVAL, "build_mode must be set before the first Add");
         h->build_mode = (int)v;
     } else if (n == "m0") {
@@ -1623,7 +1631,9 @@ int mhnsw_delete(mhnsw_index* h, const int64_t* keys, int64_t n, uint8_t* out) {
     a.stats = h->d_stats + 4;
     a.err = h->d_err;
     a.vis_log2 = h->vis_log2;
-    if (h->build_mode == MHNSW_BUILD_COMPAT) {
+    if (h->build_mode == MHNSW_BUILD_FLAT) {
+        // no links to repair: the dead flag removes the row from exact search
+    } else if (h->build_mode == MHNSW_BUILD_COMPAT) {
         if ((r = ensure_buf(h, h->cand, ids.size()))) return r;
         HIPCHK(h, hipMemcpyAsync(h->cand.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, h->stream));
         a.ids = h->cand.p;

@@ -44,6 +44,7 @@ typedef struct mhnsw_index mhnsw_index;
 /* build modes (option "build_mode") */
 #define MHNSW_BUILD_COMPAT 0 /* graph.go:437-531 sequential Add semantics */
 #define MHNSW_BUILD_BATCH 1  /* batched parallel insert (throughput)      */
+#define MHNSW_BUILD_FLAT 2   /* vector store only, exact search (hnsw-extensions/hybrid/exact.go ExactIndex) */
 
 /* error classes */
 #define MHNSW_OK 0
