@@ -359,7 +359,7 @@ void fix_entries(mhnsw_index* h) {
 
 int set_shape(mhnsw_index* h, int dim) {
     int lpr, vpl;
-    if (!pick_cfg(dim, lpr, vpl)) return fail(h, MHNSW_EUNSUPPORTED, "dimension %d not supported (1..2048)", dim);
+    if (!pick_cfg(dim, lpr, vpl)) return fail(h, MHNSW_EUNSUPPORTED, "dimension %d not supported (1..4096)", dim);
     h->dim = dim;
     h->lpr = lpr;
     h->vpl = vpl;

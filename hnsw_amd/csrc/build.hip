@@ -649,7 +649,9 @@ static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
     X(64, 3, 8)            \
     X(64, 4, 4)            \
     X(64, 6, 4)            \
-    X(64, 8, 2)
+    X(64, 8, 2)            \
+    X(64, 12, 1)           \
+    X(64, 16, 1)
 
 int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, hipStream_t s) {
     // the sequential build keeps three query rows live (search / addNeighbor /

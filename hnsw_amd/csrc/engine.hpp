@@ -22,6 +22,8 @@ inline bool pick_cfg(int dim, int& lpr, int& vpl) {
     if (dim <= 1024) { lpr = 64; vpl = 4; return true; }
     if (dim <= 1536) { lpr = 64; vpl = 6; return true; }
     if (dim <= 2048) { lpr = 64; vpl = 8; return true; }
+    if (dim <= 3072) { lpr = 64; vpl = 12; return true; }
+    if (dim <= 4096) { lpr = 64; vpl = 16; return true; }
     return false;
 }
 inline int pitch_of(int lpr, int vpl) { return lpr * 4 * vpl; }

@@ -622,7 +622,9 @@ int launch_exact_select(const ExactArgs& a, hipStream_t s) {
     X(64, 3, 8)            \
     X(64, 4, 4)            \
     X(64, 6, 4)            \
-    X(64, 8, 2)
+    X(64, 8, 2)            \
+    X(64, 12, 1)           \
+    X(64, 16, 1)
 
 int launch_rerank(const float* Q, const GraphDev& g, const uint32_t* cand, int kk, int64_t B, int lpr, int vpl, int k,
                   int64_t* out_keys, float* out_dist, int32_t* out_n, int32_t* out_ids, const CertArgs& c,

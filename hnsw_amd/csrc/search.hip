@@ -384,7 +384,9 @@ static int launch_compat_t(const SearchArgs& a, hipStream_t s) {
     X(64, 3, 8)                 \
     X(64, 4, 4)                 \
     X(64, 6, 4)                 \
-    X(64, 8, 2)
+    X(64, 8, 2)            \
+    X(64, 12, 1)           \
+    X(64, 16, 1)
 
 int launch_norms(const float* X, int64_t n0, int64_t n1, int pitch, int lpr, int vpl, float* out, hipStream_t s) {
 #define X_(L, V, G) \

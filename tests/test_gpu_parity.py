@@ -75,7 +75,8 @@ def test_distance_kats(H, ref):
             assert abs(d - c["want"]) <= c["tol"], c["src"]
 
 
-@pytest.mark.parametrize("dim", [1, 2, 3, 7, 16, 64, 100, 128, 255, 256, 500, 768, 1000, 1536, 2048])
+@pytest.mark.parametrize("dim", [1, 2, 3, 7, 16, 64, 100, 128, 255, 256, 500, 768, 1000, 1536, 2048, 2049, 3072,
+                                 4096])
 def test_distance_sweep_bitwise(H, O, dim):
     rng = np.random.default_rng(dim)
     X = rng.uniform(-1, 1, (300, dim)).astype(np.float32)
@@ -170,6 +171,8 @@ def test_fixture_build_and_search(H, name):
     (1500, 33, 1, 10, 0.3, 24),
     (800, 1536, 1, 12, 0.25, 16),
     (600, 3, 1, 6, 0.5, 20),
+    (300, 3072, 0, 8, 0.25, 16),
+    (250, 4096, 1, 6, 0.3, 16),
 ])
 def test_compat_build_parity(H, O, n, d, metric, M, ml, ef):
     rng = np.random.default_rng(n + d)
@@ -334,13 +337,13 @@ def _exact_inputs(rng, n, d, nq, metric):
 
 
 @pytest.mark.parametrize("precision", [0, 1])
-@pytest.mark.parametrize("metric,d", [(0, 24), (1, 24), (0, 768), (1, 768), (0, 1536)])
+@pytest.mark.parametrize("metric,d", [(0, 24), (1, 24), (0, 768), (1, 768), (0, 1536), (1, 4096)])
 def test_exact_precision_parity(H, O, metric, d, precision):
     """Exact mode with f32-input MFMA scores (0) and bf16x3 split scores (1):
     after the canonical re-rank and the certificate (or its fallback) the
     output is the oracle's brute force bit for bit."""
     rng = np.random.default_rng(100 + d + metric)
-    n = 3000 if d < 1536 else 1500
+    n = 3000 if d < 1536 else (1500 if d < 4096 else 600)
     X, Q = _exact_inputs(rng, n, d, 96, metric)
     g = H.Graph(M=8, Ml=0.25, EfSearch=32, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
                 ef_construction=32)
@@ -386,6 +389,13 @@ def test_exact_certificate_fallback(H, O, metric):
         o.import_graph(**g.export())
         rk, rd, rn = o.search(Q, 10, mode=O.MODE_EXACT)
         _same_results(gk, gd, gn, rk, rd, rn)
+    g.close()
+
+
+def test_dimension_limit(H):
+    g = H.Graph(M=4, Ml=0.25, EfSearch=8)
+    with pytest.raises(H.HnswError, match=r"dimension 4097 not supported \(1..4096\)"):
+        g.add_arrays(np.arange(2), np.ones((2, 4097), np.float32))
     g.close()
 
 
