@@ -110,6 +110,12 @@ struct mhnsw_index {
     DevBuf<uint8_t> xflag;
     DevBuf<int32_t> xflagged, xnflag;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // cross-stream ordering: a *_device search returns once enqueued on the
+    // caller's stream; the next call on another stream (or a mutation) must
+    // not reuse scratch / rewrite the graph under it
+    hipEvent_t scr_ev = nullptr, meta_ev = nullptr;
+    hipStream_t scr_stream = nullptr;
+    bool scr_valid = false;
     bool have_timing = false;
     // host mirrors
     std::unordered_map<int64_t, int32_t> key2id;  // live keys only
@@ -600,9 +606,43 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     return r;
 }
 
+// Mutations (Add / Delete / Reserve / Import) first let every enqueued
+// search finish: they rewrite or reallocate what those kernels read.
+int drain(mhnsw_index* h) {
+    if (h->scr_valid) HIPCHK(h, hipEventSynchronize(h->scr_ev));
+    h->scr_valid = false;
+    return 0;
+}
+
+int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B, int dim, int k, int mode, int ef,
+                const int64_t* entry_key, int64_t* okeys, float* odist, int32_t* on, hipStream_t s, bool timing,
+                int32_t* out_ids);
+
+// every search: order after the previous scratch user (another stream), and
+// after the metadata copies this call makes on the handle's stream
 int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B, int dim, int k, int mode, int ef,
                 const int64_t* entry_key, int64_t* okeys, float* odist, int32_t* on, hipStream_t s, bool timing,
                 int32_t* out_ids = nullptr) {
+    if (h->scr_valid && h->scr_stream != s) HIPCHK(h, hipStreamWaitEvent(s, h->scr_ev, 0));
+    const int r = search_body(h, queries, on_device, B, dim, k, mode, ef, entry_key, okeys, odist, on, s, timing,
+                              out_ids);
+    HIPCHK(h, hipEventRecord(h->scr_ev, s));
+    h->scr_stream = s;
+    h->scr_valid = true;
+    return r;
+}
+
+// the search kernels run on the caller's stream; metadata goes up on the handle's
+int order_meta(mhnsw_index* h, hipStream_t s) {
+    if (s == h->stream) return 0;
+    HIPCHK(h, hipEventRecord(h->meta_ev, h->stream));
+    HIPCHK(h, hipStreamWaitEvent(s, h->meta_ev, 0));
+    return 0;
+}
+
+int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B, int dim, int k, int mode, int ef,
+                const int64_t* entry_key, int64_t* okeys, float* odist, int32_t* on, hipStream_t s, bool timing,
+                int32_t* out_ids) {
     int r = validate(h);
     if (r) return r;
     if (k <= 0) return fail(h, MHNSW_EK, "k must be greater than 0, got %d", k);  // graph.go:542-544
@@ -673,7 +713,7 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             if ((r = ensure_buf(h, h->qsplit, (size_t)qc * h->pitch * 2))) return r;
         }
         LCHK(h, launch_norms(h->qpad.p, 0, B, h->pitch, h->lpr, h->vpl, h->qnorm.p, s));
-        if ((r = sync_layer_table(h))) return r;
+        if ((r = sync_layer_table(h)) || (r = order_meta(h, s))) return r;
         GraphDev g = graph_view(h);
         // certificate constants (u = 2^-24; gamma_n = n u / (1 - n u) bounds any
         // order of n-term f32 summation relative to the sum of magnitudes)
@@ -756,7 +796,7 @@ int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));
     } else {
         if ((r = sync_layer_entries(h))) return r;
-        if ((r = sync_layer_table(h))) return r;
+        if ((r = sync_layer_table(h)) || (r = order_meta(h, s))) return r;
         SearchArgs a;
         a.g = graph_view(h);
         a.q = h->qpad.p;
@@ -832,7 +872,8 @@ int mhnsw_create(int metric, int M, double ml, int ef_search, uint64_t seed, mhn
         hipMalloc(&h->d_err, sizeof(int)) != hipSuccess || hipMalloc(&h->touched_cnt, 16) != hipSuccess ||
         hipMalloc(&h->d_layer_entry, MH_MAXL * 4) != hipSuccess ||
         hipMalloc(&h->d_layers, MH_MAXL * sizeof(LayerDev)) != hipSuccess || hipEventCreate(&h->ev0) != hipSuccess ||
-        hipEventCreate(&h->ev1) != hipSuccess || hipMemset(h->d_stats, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
+        hipEventCreate(&h->ev1) != hipSuccess || hipEventCreateWithFlags(&h->scr_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->meta_ev, hipEventDisableTiming) != hipSuccess || hipMemset(h->d_stats, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
         mhnsw_destroy(h);
         return fail(nullptr, MHNSW_EDEVICE, "device initialisation failed");
     }
@@ -842,6 +883,7 @@ int mhnsw_create(int metric, int M, double ml, int ef_search, uint64_t seed, mhn
 
 void mhnsw_destroy(mhnsw_index* h) {
     if (!h) return;
+    if (h->scr_valid) (void)hipEventSynchronize(h->scr_ev);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     auto F = [](void* p) {
         if (p) (void)hipFree(p);
@@ -891,6 +933,8 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->xflag.p);
     F(h->xflagged.p);
     F(h->xnflag.p);
+    if (h->scr_ev) (void)hipEventDestroy(h->scr_ev);
+    if (h->meta_ev) (void)hipEventDestroy(h->meta_ev);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -995,7 +1039,8 @@ int mhnsw_validate(mhnsw_index* h) {
 
 int mhnsw_reserve(mhnsw_index* h, int64_t n, int dim) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
-    int r;
+    int r = drain(h);
+    if (r) return r;
     if (!h->layers_exist) {
         if ((r = set_shape(h, dim))) return r;
     } else if (dim != h->dim) {
@@ -1008,13 +1053,16 @@ int mhnsw_reserve(mhnsw_index* h, int64_t n, int dim) {
 
 int mhnsw_add(mhnsw_index* h, const int64_t* keys, const float* vecs, int64_t n, int dim, const int32_t* levels) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
+    int r = drain(h);
+    if (r) return r;
     return add_impl(h, keys, vecs, false, n, dim, levels);
 }
 
 int mhnsw_add_device(mhnsw_index* h, const int64_t* keys, const float* d_vecs, int64_t n, int dim,
                      const int32_t* levels) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
-    HIPCHK(h, hipDeviceSynchronize());  // order after whatever produced d_vecs
+    HIPCHK(h, hipDeviceSynchronize());  // order after whatever produced d_vecs (and any enqueued search)
+    h->scr_valid = false;
     return add_impl(h, keys, d_vecs, true, n, dim, levels);
 }
 
@@ -1440,6 +1488,8 @@ extern "C" {
 int mhnsw_import(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t* keys, const float* vecs,
                  const int32_t* deg, const int32_t* adj, const int32_t* entry, const uint8_t* dead) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
+    int r = drain(h);
+    if (r) return r;
     return import_csr(h, N, dim, L, cap, keys, vecs, deg, adj, entry, dead);
 }
 
@@ -1458,6 +1508,8 @@ int mhnsw_export_go(mhnsw_index* h, int key_kind, uint8_t* buf, int64_t cap, int
 
 int mhnsw_import_go(mhnsw_index* h, const uint8_t* buf, int64_t size, int key_kind) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
+    int r = drain(h);
+    if (r) return r;
     return import_go(h, buf, size, key_kind);
 }
 
@@ -1479,6 +1531,7 @@ int mhnsw_save(mhnsw_index* h, const char* path, int key_kind) {
 // encode.go:280-299 LoadSavedGraph: a missing or empty file leaves the graph empty
 int mhnsw_load(mhnsw_index* h, const char* path, int key_kind) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
+    if (int r0 = drain(h)) return r0;
     FILE* f = fopen(path, "rb");
     if (!f) return 0;
     std::vector<uint8_t> buf;
@@ -1605,6 +1658,7 @@ int mhnsw_search_negatives(mhnsw_index* h, const float* queries, int64_t B, int 
 // graph.go:843-895 Delete / BatchDelete
 int mhnsw_delete(mhnsw_index* h, const int64_t* keys, int64_t n, uint8_t* out) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
+    if (int r0 = drain(h)) return r0;
     if (n > 0 && (!keys || !out)) return fail(h, MHNSW_EINVAL, "keys and out must be non-NULL");
     for (int64_t i = 0; i < n; ++i) out[i] = 0;
     if (n <= 0 || h->layers.empty()) return 0;
@@ -1733,6 +1787,9 @@ int mhnsw_strkeys_encode(mhnsw_index* h, const char* blob, const int64_t* offs, 
                          int64_t* out) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
     if (n < 0) return fail(h, MHNSW_EINVAL, "negative key count");
+    if (assign) {  // a re-spacing rewrites the stored keys enqueued searches read
+        if (int r0 = drain(h)) return r0;
+    }
     std::vector<std::string> ks((size_t)n);
     for (int64_t i = 0; i < n; ++i) {
         if (offs[i + 1] < offs[i]) return fail(h, MHNSW_EINVAL, "bad string offsets");

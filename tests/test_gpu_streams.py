@@ -1,0 +1,66 @@
+"""GPU: the ABI's stream contract.  A *_device search returns once enqueued on
+the caller's stream; a following search on another stream must not reuse the
+handle's scratch under it, and a mutation (Add / Delete) must not rewrite the
+graph under an enqueued search (the reference's RWMutex, graph.go:328)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _device_search(torch, H, g, Q, k, stream, mode):
+    B, d = Q.shape
+    ok = torch.empty(B, k, dtype=torch.int64, device="cuda")
+    od = torch.empty(B, k, dtype=torch.float32, device="cuda")
+    on = torch.empty(B, dtype=torch.int32, device="cuda")
+    g.search_device(Q.data_ptr(), B, d, k, ok.data_ptr(), od.data_ptr(), on.data_ptr(), mode=mode, ef=64,
+                    stream=stream.cuda_stream)
+    return ok, od, on
+
+
+@pytest.mark.parametrize("mode", [1, 2])  # beam, exact
+def test_searches_on_two_streams(H, mode):
+    import torch
+
+    rng = np.random.default_rng(3)
+    n, d, B, k = 60000, 128, 8192, 10
+    X = rng.normal(size=(n, d)).astype(np.float32)
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, build_mode=H.BUILD_BATCH, ef_construction=64)
+    g.add_arrays(np.arange(n), X)
+    QA = torch.tensor(rng.normal(size=(B, d)).astype(np.float32), device="cuda")
+    QB = torch.tensor(rng.normal(size=(B, d)).astype(np.float32), device="cuda")
+    want_a = g.search_arrays(QA.cpu().numpy(), k, mode=mode, ef=64)
+    want_b = g.search_arrays(QB.cpu().numpy(), k, mode=mode, ef=64)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        a = _device_search(torch, H, g, QA, k, sa, mode)
+        b = _device_search(torch, H, g, QB, k, sb, mode)
+        torch.cuda.synchronize()
+        for got, want in ((a, want_a), (b, want_b)):
+            assert np.array_equal(got[2].cpu().numpy(), want[2])
+            assert np.array_equal(got[0].cpu().numpy(), want[0])
+            assert np.array_equal(got[1].cpu().numpy().view(np.uint32), want[1].view(np.uint32))
+    g.close()
+
+
+def test_add_after_enqueued_search(H):
+    import torch
+
+    rng = np.random.default_rng(4)
+    n, d, B, k = 50000, 64, 8192, 10
+    X = rng.normal(size=(n + 5000, d)).astype(np.float32)
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.EuclideanDistance, build_mode=H.BUILD_BATCH,
+                ef_construction=64)
+    g.add_arrays(np.arange(n), X[:n])
+    Q = torch.tensor(rng.normal(size=(B, d)).astype(np.float32), device="cuda")
+    want = g.search_arrays(Q.cpu().numpy(), k, mode=H.MODE_EXACT)
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    got = _device_search(torch, H, g, Q, k, s, H.MODE_EXACT)
+    g.add_arrays(np.arange(n, n + 5000), X[n:])  # must wait for the enqueued search
+    g.BatchDelete(list(range(0, n, 7)))
+    torch.cuda.synchronize()
+    assert np.array_equal(got[0].cpu().numpy(), want[0])
+    assert np.array_equal(got[1].cpu().numpy().view(np.uint32), want[1].view(np.uint32))
+    g.close()
