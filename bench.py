@@ -47,7 +47,7 @@ def parse():
     p.add_argument("--mode", choices=["replica", "shard"], default="replica")
     p.add_argument("--nbase", type=int, default=1_000_000, help="vectors per index (per shard in shard mode)")
     p.add_argument("--dim", type=int, default=768)
-    p.add_argument("--batch", type=int, default=16384, help="queries per step per GPU")
+    p.add_argument("--batch", type=int, default=65536, help="queries per step per GPU")
     p.add_argument("--ef", type=int, default=64)
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--metric", choices=["cosine", "euclidean"], default="cosine")
