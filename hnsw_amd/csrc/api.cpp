@@ -64,7 +64,8 @@ struct mhnsw_index {
     int vis_log2 = 12;
     int exact_kk = 0;
     int exact_precision = 1;
-    int exact_tile = 0;       // bf16x3 GEMM tile variant (exact.hip launch_exact_scores_x3)  // 0: f32-input MFMA scores, 1: bf16x3 split MFMA scores (both certified)
+    int exact_tile = 0;       // bf16x3 GEMM tile variant (exact.hip launch_exact_scores_x3)
+    int compat_waves = 8;     // compat insert: waves scoring each distance batch (1 = the walking wave alone)  // 0: f32-input MFMA scores, 1: bf16x3 split MFMA scores (both certified)
     // shape
     int dim = 0, pitch = 0, lpr = 0, vpl = 0;
     bool layers_exist = false;
@@ -413,7 +414,7 @@ int run_build_compat(mhnsw_index* h, int64_t n0, int64_t n1, int top0) {
     a.stats = h->d_stats + 4;
     a.err = h->d_err;
     a.vis_log2 = h->vis_log2;
-    int lr = launch_build_compat(a, h->lpr, h->vpl, h->stream);
+    int lr = launch_build_compat(a, h->lpr, h->vpl, h->compat_waves, h->stream);
     if (lr == -2) return fail(h, MHNSW_EUNSUPPORTED, "compat build LDS budget exceeded (ef=%d, M=%d)", h->ef, h->M);
     LCHK(h, lr);
     int err = 0;
@@ -1000,6 +1001,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
         h->exact_kk = (int)v;
     } else if (n == "exact_tile") {
         h->exact_tile = (int)v;
+    } else if (n == "compat_waves") {
+        if (v != 1 && v != 8) return fail(h, MHNSW_EINVAL, "compat_waves must be 1 or 8");
+        h->compat_waves = (int)v;
     } else if (n == "exact_precision") {
         if (v != 0 && v != 1) return fail(h, MHNSW_EINVAL, "exact_precision must be 0 (f32) or 1 (bf16x3)");
         h->exact_precision = (int)v;
@@ -1024,6 +1028,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "exact_kk") *v = h->exact_kk;
     else if (n == "exact_precision") *v = h->exact_precision;
     else if (n == "exact_tile") *v = h->exact_tile;
+    else if (n == "compat_waves") *v = h->compat_waves;
     else if (n == "strkey_relabels") *v = h->relabels;
     else if (n == "strkeys") *v = (int64_t)h->s2l.size();
     else if (n == "pitch") *v = h->pitch;

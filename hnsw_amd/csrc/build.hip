@@ -26,15 +26,24 @@ __device__ __forceinline__ void build_sync() { __syncthreads(); }
 // ---------------------------------------------------------------------------
 // compat build
 // ---------------------------------------------------------------------------
+// The walks below run on ONE wave (the "master"): every graph mutation, heap
+// and visited-set operation happens there, in the reference's order.  Only
+// distance batches are delegated, through the evaluator policy `Ev`:
+// WaveEval evaluates on the master itself; MwEval (k_build_compat_mw) hands a
+// batch to all waves of the workgroup and gets the distances back in LDS, in
+// the same order.  Distances are the canonical ones whichever wave computes
+// them (eval_rows), so both evaluators give identical graphs.
 struct BuildSmem {
     CompatSmem cs;
     float* hd;  // replenish heap
     uint32_t* hi;
     int hcap;
+    uint32_t* radj;  // replenish: staged neighbour rows (hcap entries)
+    int64_t* rkey;   // ... and their keys
 };
 
-template <class C, int G>
-__device__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v) {
+template <class C, int G, class Ev>
+__device__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v, const Ev& ev) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
     int32_t* row = g.layers[l].adj + (size_t)n * capl;
@@ -45,16 +54,17 @@ __device__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v) {
     if (!m) return;
     const int pos = __ffsll((long long)m) - 1;
     const int32_t last = ld_i32<true>(row + d - 1);
-    build_sync();
+    ev.sync();
     if (lane == 0) {
         st_i32(row + pos, last);
         st_i32(g.layers[l].deg + n, d - 1);
     }
-    build_sync();
+    ev.sync();
 }
 
 // append nw to n's neighbour set if absent; returns the new degree
-__device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw) {
+template <class Ev>
+__device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw, const Ev& ev) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
     int32_t* row = g.layers[l].adj + (size_t)n * capl;
@@ -62,18 +72,24 @@ __device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw) {
     if (d < 0) d = 0;  // graph.go:46-48 allocate the map
     const bool pres = lane < d && (uint32_t)ld_i32<true>(row + lane) == nw;
     const bool present = __ballot(pres) != 0;
-    build_sync();
+    ev.sync();
     if (lane == 0) {
         if (!present) st_i32(row + d, (int32_t)nw);
         st_i32(g.layers[l].deg + n, present ? d : d + 1);
     }
-    build_sync();
+    ev.sync();
     return present ? d : d + 1;
 }
 
-// graph.go:172-219
-template <class C, int G>
-__device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err) {
+// graph.go:172-219.  The neighbours' rows and keys are staged in LDS in one
+// pass (instead of one dependent load chain per neighbour); the candidates are
+// then walked in the reference's order (neighbours, then their neighbours, both
+// in ascending key order -- the map-order stand-in), recorded in the visited
+// set and collected, and ONE distance batch scores them all; the heap sees the
+// pushes in the same order as a per-neighbour loop would produce.
+template <class C, int G, class Ev>
+__device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err,
+                          const Ev& ev) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
     int dn = ld_i32<true>(g.layers[l].deg + n);
@@ -81,7 +97,7 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
     if (dn >= m) return;
     const int vsize = 1 << S.cs.vlog2, vmask = vsize - 1;
     vis_clear(S.cs.vis, vsize);
-    build_sync();
+    ev.sync();
     if (lane == 0) vis_probe(S.cs.vis, vmask, n);  // graph.go:184
     uint32_t mine = 0xFFFFFFFFu;
     int64_t key = INT64_MAX;
@@ -91,19 +107,36 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
     }
     bitonic64(key, mine);
     if (lane < dn) vis_probe(S.cs.vis, vmask, mine);  // graph.go:187-189
-    QReg<C> q;
-    load_query(q, g.vecs + (size_t)n * g.pitch);
-    const float qn = g.norms[n];
-    GHeap h{S.hd, S.hi, 0};
+    // stage every neighbour's row (deg, entries, keys) -- rows j < dn, j-major
+    const int mydeg = lane < dn ? min(ld_i32<true>(g.layers[l].deg + mine), capl) : -1;
+    const int tot = min(dn * capl, S.hcap);
+    for (int e0 = 0; e0 < tot; e0 += 64) {  // uniform trip count: the shuffles see every lane
+        const int e = e0 + lane;
+        const int j = min(e / capl, 63), i = e % capl;
+        const uint32_t nb = shfl_u(mine, j);
+        const int dj = __shfl(mydeg, j, 64);
+        uint32_t th = 0xFFFFFFFFu;
+        int64_t tk = INT64_MAX;
+        if (e < tot && i < dj) {
+            th = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)nb * capl + i));
+            tk = g.keys[th];
+        }
+        if (e < tot) {
+            S.radj[e] = th;
+            S.rkey[e] = tk;
+        }
+    }
+    ev.sync();
+    // the reference's walk: visited bookkeeping and the candidate list, in order
+    int ncand = 0;
     for (int j = 0; j < dn; ++j) {  // graph.go:192-210
-        const uint32_t nb = rl_u(mine, j);
-        const int dnb = min(ld_i32<true>(g.layers[l].deg + nb), capl);
+        const int dnb = __shfl(mydeg, j, 64);
         if (dnb < 0) continue;
         uint32_t th = 0xFFFFFFFFu;
         int64_t tk = INT64_MAX;
-        if (lane < dnb) {
-            th = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)nb * capl + lane));
-            tk = g.keys[th];
+        if (lane < dnb && j * capl + lane < S.hcap) {
+            th = S.radj[j * capl + lane];
+            tk = S.rkey[j * capl + lane];
         }
         bitonic64(tk, th);
         int pr = 0;
@@ -111,12 +144,25 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
         if (__ballot(pr == 2)) err = 1;
         int cnt;
         const uint32_t cid = compact(th, pr == 1, cnt);
-        st.E += cnt;
-        eval_list<C, G>(g, q, qn, cid, cnt, COSINE,  // graph.go:204 hard-coded cosine
-                        [&](float d, uint32_t u) {
-                            if (h.n < S.hcap) gh_push(h, d, u);
-                            else err |= 8;
-                        });
+        if (ncand + cnt > S.hcap) {
+            err |= 8;
+            cnt = S.hcap - ncand;
+        }
+        if (lane < cnt) ev.list[ncand + lane] = cid;
+        ncand += cnt;
+    }
+    ev.sync();
+    st.E += ncand;
+    GHeap h{S.hd, S.hi, 0};
+    {
+        QReg<C> q;
+        load_query(q, g.vecs + (size_t)n * g.pitch);
+        const float qn = g.norms[n];
+        ev.template run_list<C, G>(g, q, qn, ncand, COSINE,  // graph.go:204 hard-coded cosine
+                                   [&](float d, uint32_t u) {
+                                       if (h.n < S.hcap) gh_push(h, d, u);
+                                       else err |= 8;
+                                   });
     }
     // graph.go:213-218 (len < m before every add: addNeighbor cannot evict)
     while (h.n > 0) {
@@ -126,17 +172,17 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
         float bd;
         uint32_t best;
         gh_pop(h, bd, best);
-        list_append(g, l, n, best);
+        list_append(g, l, n, best, ev);
     }
 }
 
 // graph.go:41-81
-template <class C, int G>
+template <class C, int G, class Ev>
 __device__ void add_neighbor(const GraphDev& g, int l, uint32_t n, uint32_t nw, int m, BuildSmem& S, WaveStats& st,
-                             int& err) {
+                             int& err, const Ev& ev) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
-    const int d = list_append(g, l, n, nw);
+    const int d = list_append(g, l, n, nw, ev);
     if (d <= m) return;
     uint32_t nb = 0xFFFFFFFFu;
     int64_t key = INT64_MAX;
@@ -151,42 +197,148 @@ __device__ void add_neighbor(const GraphDev& g, int l, uint32_t n, uint32_t nw, 
     float worst_d = -__int_as_float(0x7f800000);
     uint32_t worst = EMPTY_ID;
     st.E += d;
-    eval_list<C, G>(g, q, qn, nb, d, g.metric, [&](float dd, uint32_t u) {  // graph.go:60-71
+    ev.template run<C, G>(g, q, qn, nb, d, g.metric, [&](float dd, uint32_t u) {  // graph.go:60-71
         if (dd > worst_d || worst == EMPTY_ID) {
             worst_d = dd;
             worst = u;
         }
     });
     if (worst == EMPTY_ID) return;
-    list_remove<C, G>(g, l, n, worst);  // graph.go:74
-    if (ld_i32<true>(g.layers[l].deg + worst) >= 0) list_remove<C, G>(g, l, worst, n);  // graph.go:76-78
-    replenish<C, G>(g, l, worst, m, S, st, err);  // graph.go:79
+    list_remove<C, G>(g, l, n, worst, ev);  // graph.go:74
+    if (ld_i32<true>(g.layers[l].deg + worst) >= 0) list_remove<C, G>(g, l, worst, n, ev);  // graph.go:76-78
+    replenish<C, G>(g, l, worst, m, S, st, err, ev);  // graph.go:79
 }
 
+// ---- multi-wave evaluator ----------------------------------------------------
+// Protocol block in LDS.  The master posts a batch (query registers, ids,
+// metric) and hits a workgroup barrier; every wave scores its share of the
+// rows into dist[]; a second barrier hands the distances back.  Workers sit in
+// mw_worker's loop between the two barriers until the master posts EXIT.
+struct MwHdr {
+    int cmd, cnt, metric;
+    float qn;
+};
+constexpr int MW_EVAL = 0, MW_EXIT = 1;
+
+__device__ __forceinline__ void mw_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// rows [0, cnt) of ids, wave w of nw: canonical distances into dist[]
 template <class C, int G>
-__global__ __launch_bounds__(64) void k_build_compat(CompatBuildArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+__device__ __forceinline__ void mw_share(const GraphDev& g, const QReg<C>& q, float qn, const uint32_t* ids,
+                                         float* dist, int cnt, int metric, int w, int nw) {
+    using RM = RowMap<C, G>;
+    constexpr int GROUP = C::LPR >> RM::LG;
     const int lane = lane_id();
-    const int vsize = 1 << a.vis_log2;
-    BuildSmem S;
-    S.cs.vis = smem;
-    S.cs.vlog2 = a.vis_log2;
-    uint32_t* p = smem + vsize;
+    for (int base = w * RM::T; base < cnt; base += nw * RM::T) {
+        uint32_t rid[G];
+        bool valid[G];
+#pragma unroll
+        for (int gg = 0; gg < G; ++gg) {
+            const int t = base + RM::reg_row(gg, lane);
+            valid[gg] = t < cnt;
+            rid[gg] = valid[gg] ? guard_id(g, ids[t]) : 0u;
+        }
+        const float s = metric == EUCLIDEAN ? eval_rows<C, G, true>(q, g.vecs, g.pitch, rid, valid)
+                                            : eval_rows<C, G, false>(q, g.vecs, g.pitch, rid, valid);
+        const int town = base + RM::owned_row(lane);
+        if (town < cnt && (lane & (GROUP - 1)) == 0) {
+            const float xn = metric == COSINE ? g.norms[guard_id(g, ids[town])] : 1.f;
+            dist[town] = finalize(metric, s, xn, qn);
+        }
+    }
+}
+
+template <class C>
+struct MwEval {
+    MwHdr* hdr;
+    float4* qbuf;     // [VPL * 64] the master's query registers, lane-major
+    uint32_t* list;   // ids of the posted batch (also replenish's candidate list)
+    float* dist;      // [cap] distances back
+    int nw;
+    template <class C2, int G, class Sink>
+    __device__ __forceinline__ void run_list(const GraphDev& g, const QReg<C2>& q, float qn, int cnt, int metric,
+                                             Sink&& sink) const {
+        if (cnt <= 0) return;
+        const int lane = lane_id();
+#pragma unroll
+        for (int v = 0; v < C2::VPL; ++v) qbuf[v * 64 + lane] = q.v[v];
+        if (lane == 0) {
+            hdr->cmd = MW_EVAL;
+            hdr->cnt = cnt;
+            hdr->metric = metric;
+            hdr->qn = qn;
+        }
+        mw_barrier();  // post
+        mw_share<C2, G>(g, q, qn, list, dist, cnt, metric, 0, nw);
+        mw_barrier();  // collect
+        for (int t = 0; t < cnt; ++t) sink(dist[t], list[t]);
+    }
+    template <class C2, int G, class Sink>
+    __device__ __forceinline__ void run(const GraphDev& g, const QReg<C2>& q, float qn, uint32_t cid, int cnt,
+                                        int metric, Sink&& sink) const {
+        if (cnt <= 0) return;
+        if (lane_id() < cnt) list[lane_id()] = cid;
+        run_list<C2, G>(g, q, qn, cnt, metric, sink);
+    }
+    // the master's own lanes only (workers never touch graph state)
+    __device__ __forceinline__ void sync() const {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
+};
+
+template <class C, int G>
+__device__ void mw_worker(const GraphDev& g, const MwEval<C>& ev, int w) {
+    for (;;) {
+        mw_barrier();
+        if (ev.hdr->cmd == MW_EXIT) break;
+        QReg<C> q;
+        const int lane = lane_id();
+#pragma unroll
+        for (int v = 0; v < C::VPL; ++v) q.v[v] = ev.qbuf[v * 64 + lane];
+        mw_share<C, G>(g, q, ev.hdr->qn, ev.list, ev.dist, ev.hdr->cnt, ev.hdr->metric, w, ev.nw);
+        mw_barrier();
+    }
+}
+
+// LDS of the compat walks: visited set, compat heaps, replenish heap + staging
+__device__ __forceinline__ uint32_t* build_smem(uint32_t* p, int vis_log2, int M, int ef, BuildSmem& S) {
+    S.cs.vis = p;
+    S.cs.vlog2 = vis_log2;
+    p += 1 << vis_log2;
     S.cs.cd = reinterpret_cast<float*>(p);
-    p += a.ef + 2;
+    p += ef + 2;
     S.cs.ci = p;
-    p += a.ef + 2;
+    p += ef + 2;
     S.cs.rd = reinterpret_cast<float*>(p);
-    p += a.M + 2;
+    p += M + 2;
     S.cs.ri = p;
-    p += a.M + 2;
-    const int hcap = a.M * (a.M + 1) + 2;
+    p += M + 2;
+    const int hcap = (M + 1) * (M + 1) + 2;  // >= any neighbours-of-neighbours list
+    S.hcap = hcap;
     S.hd = reinterpret_cast<float*>(p);
     p += hcap;
     S.hi = p;
-    S.hcap = hcap;
-    WaveStats st;
-    int err = 0;
+    p += hcap;
+    S.radj = p;
+    p += hcap;
+    p += (reinterpret_cast<uintptr_t>(p) & 4) ? 1 : 0;  // 8-B align
+    S.rkey = reinterpret_cast<int64_t*>(p);
+    p += 2 * hcap;
+    return p;
+}
+__host__ __device__ constexpr size_t build_smem_words(int vis_log2, int M, int ef) {
+    return ((size_t)1 << vis_log2) + 2 * (size_t)(ef + 2) + 2 * (size_t)(M + 2) + 5 * (size_t)((M + 1) * (M + 1) + 2) + 1;
+}
+
+// graph.go:437-531 for inserts [n0, n1), by the master wave
+template <class C, int G, class Ev>
+__device__ void compat_inserts(const CompatBuildArgs& a, BuildSmem& S, const Ev& ev, WaveStats& st, int& err) {
+    const int lane = lane_id();
     int top = a.top0;
     for (int64_t i = a.n0; i < a.n1; ++i) {
         const uint32_t id = (uint32_t)i;
@@ -199,9 +351,9 @@ __global__ __launch_bounds__(64) void k_build_compat(CompatBuildArgs a) {
         for (int l = top; l >= 0; --l) {  // graph.go:475
             const int32_t ent = a.layer_entry[l];
             if (ent == (int32_t)id) {  // graph.go:485-488: empty layer, no search
-                build_sync();
+                ev.sync();
                 if (lane == 0) st_i32(a.g.layers[l].deg + id, -1);
-                build_sync();
+                ev.sync();
                 continue;
             }
             // graph.go:492-498: layer.nodes[*elevator] is nil once that node was deleted
@@ -213,7 +365,7 @@ __global__ __launch_bounds__(64) void k_build_compat(CompatBuildArgs a) {
                 err |= 2;
                 break;
             }
-            const int cnt = compat_layer<C, G, true>(a.g, l, sp, a.M, a.ef, q, qn, S.cs, st, err);  // :500
+            const int cnt = compat_layer<C, G, true>(a.g, l, sp, a.M, a.ef, q, qn, S.cs, st, err, ev);  // :500
             if (cnt == 0) {
                 err |= 2;
                 break;
@@ -221,32 +373,86 @@ __global__ __launch_bounds__(64) void k_build_compat(CompatBuildArgs a) {
             elevator = S.cs.ri[0];  // graph.go:508
             if (level >= l) {       // graph.go:510-521
                 const uint32_t nbh = lane < cnt ? S.cs.ri[lane] : 0u;
-                build_sync();
+                ev.sync();
                 if (lane == 0) st_i32(a.g.layers[l].deg + id, -1);
-                build_sync();
+                ev.sync();
                 for (int j = 0; j < cnt; ++j) {
                     const uint32_t c = rl_u(nbh, j);
-                    add_neighbor<C, G>(a.g, l, c, id, a.M, S, st, err);
-                    add_neighbor<C, G>(a.g, l, id, c, a.M, S, st, err);
+                    add_neighbor<C, G>(a.g, l, c, id, a.M, S, st, err, ev);
+                    add_neighbor<C, G>(a.g, l, id, c, a.M, S, st, err, ev);
                 }
             }
         }
         if (err) break;
     }
-    if (lane == 0) {
+}
+
+template <class C, int G>
+__global__ __launch_bounds__(64) void k_build_compat(CompatBuildArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    BuildSmem S;
+    uint32_t* p = build_smem(smem, a.vis_log2, a.M, a.ef, S);
+    WaveEval ev;
+    ev.list = p;
+    WaveStats st;
+    int err = 0;
+    compat_inserts<C, G>(a, S, ev, st, err);
+    if (lane_id() == 0) {
         atomicAdd(&a.stats[0], st.E);
         atomicAdd(&a.stats[1], st.X);
         if (err) atomicOr(a.err, err);
     }
 }
 
+// The same walk with distance batches spread over NW waves (the sequential
+// insert is latency-bound: one wave keeps too few rows in flight).
+template <class C, int G, int NW>
+__global__ __launch_bounds__(64 * NW) void k_build_compat_mw(CompatBuildArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    BuildSmem S;
+    uint32_t* p = build_smem(smem, a.vis_log2, a.M, a.ef, S);
+    MwEval<C> ev;
+    p += (4 - (reinterpret_cast<uintptr_t>(p) >> 2) % 4) % 4;  // 16-B align: qbuf is read/written as float4
+    ev.hdr = reinterpret_cast<MwHdr*>(p);
+    p += 4;
+    ev.qbuf = reinterpret_cast<float4*>(p);
+    p += 4 * 64 * C::VPL;
+    ev.list = p;
+    p += S.hcap;
+    ev.dist = reinterpret_cast<float*>(p);
+    ev.nw = NW;
+    const int wave = threadIdx.x >> 6;
+    if (wave != 0) {
+        mw_worker<C, G>(a.g, ev, wave);
+        return;
+    }
+    WaveStats st;
+    int err = 0;
+    compat_inserts<C, G>(a, S, ev, st, err);
+    if (lane_id() == 0) ev.hdr->cmd = MW_EXIT;
+    mw_barrier();  // releases the workers
+    if (lane_id() == 0) {
+        atomicAdd(&a.stats[0], st.E);
+        atomicAdd(&a.stats[1], st.X);
+        if (err) atomicOr(a.err, err);
+    }
+}
+
+constexpr int MW_WAVES = 8;
+
 template <class C, int G>
-static int launch_build_compat_t(const CompatBuildArgs& a, hipStream_t s) {
-    const size_t words = ((size_t)1 << a.vis_log2) + 2 * (size_t)(a.ef + 2) + 2 * (size_t)(a.M + 2) +
-                         2 * (size_t)(a.M * (a.M + 1) + 2);
-    const size_t lds = words * 4;
-    if (lds > 160 * 1024) return -2;
-    hipLaunchKernelGGL((k_build_compat<C, G>), dim3(1), dim3(64), lds, s, a);
+static int launch_build_compat_t(const CompatBuildArgs& a, int waves, hipStream_t s) {
+    const size_t base = build_smem_words(a.vis_log2, a.M, a.ef);
+    const int hcap = (a.M + 1) * (a.M + 1) + 2;
+    if (waves <= 1 || C::VPL >= 16) {  // 4096-d: the walking wave alone (register budget)
+        const size_t lds = (base + hcap) * 4;
+        if (lds > 160 * 1024) return -2;
+        hipLaunchKernelGGL((k_build_compat<C, G>), dim3(1), dim3(64), lds, s, a);
+    } else {
+        const size_t lds = (base + 3 + 4 + 4 * 64 * (size_t)C::VPL + 2 * (size_t)hcap) * 4;
+        if (lds > 160 * 1024) return -2;
+        hipLaunchKernelGGL((k_build_compat_mw<C, G, MW_WAVES>), dim3(1), dim3(64 * MW_WAVES), lds, s, a);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -453,7 +659,8 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
 // stand-in) drop their backlink and are replenished; the deleted node's own
 // row stays (the reference keeps the layerNode behind one-directional edges).
 template <class C, int G>
-__device__ void isolate(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err) {
+__device__ void isolate(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err,
+                        const WaveEval& ev) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
     const int dn = min(ld_i32<true>(g.layers[l].deg + n), capl);
@@ -468,8 +675,8 @@ __device__ void isolate(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& 
     for (int j = 0; j < dn; ++j) {
         const uint32_t x = rl_u(mine, j);
         if (ld_i32<true>(g.layers[l].deg + x) < 0) continue;  // neighbor.neighbors == nil
-        list_remove<C, G>(g, l, x, n);                         // graph.go:231
-        replenish<C, G>(g, l, x, m, S, st, err);               // graph.go:232
+        list_remove<C, G>(g, l, x, n, ev);                     // graph.go:231
+        replenish<C, G>(g, l, x, m, S, st, err, ev);           // graph.go:232
     }
 }
 
@@ -480,21 +687,16 @@ __global__ __launch_bounds__(64) void k_delete_compat(DeleteArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int lane = lane_id();
     BuildSmem S;
-    S.cs.vis = smem;
-    S.cs.vlog2 = a.vis_log2;
-    uint32_t* p = smem + (1 << a.vis_log2);
-    const int hcap = a.M * (a.M + 1) + 2;
-    S.hd = reinterpret_cast<float*>(p);
-    p += hcap;
-    S.hi = p;
-    S.hcap = hcap;
+    uint32_t* p = build_smem(smem, a.vis_log2, a.M, 0, S);
+    WaveEval ev;
+    ev.list = p;
     WaveStats st;
     int err = 0;
     for (int64_t i = 0; i < a.nids; ++i) {
         const uint32_t id = a.ids[i];
         for (int l = 0; l < a.g.nlayers; ++l) {
             if (ld_i32<true>(a.g.layers[l].deg + id) == -2) continue;
-            isolate<C, G>(a.g, l, id, a.M, S, st, err);
+            isolate<C, G>(a.g, l, id, a.M, S, st, err, ev);
         }
     }
     if (lane == 0) {
@@ -626,7 +828,7 @@ __global__ __launch_bounds__(64) void k_delete_repair(DeleteArgs a) {
 
 template <class C, int G>
 static int launch_delete_compat_t(const DeleteArgs& a, hipStream_t s) {
-    const size_t words = ((size_t)1 << a.vis_log2) + 2 * (size_t)(a.M * (a.M + 1) + 2);
+    const size_t words = build_smem_words(a.vis_log2, a.M, 0) + (size_t)((a.M + 1) * (a.M + 1) + 2);
     if (words * 4 > 160 * 1024) return -2;
     hipLaunchKernelGGL((k_delete_compat<C, G>), dim3(1), dim3(64), words * 4, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -653,11 +855,11 @@ static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
     X(64, 12, 1)           \
     X(64, 16, 1)
 
-int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, hipStream_t s) {
+int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, int waves, hipStream_t s) {
     // the sequential build keeps three query rows live (search / addNeighbor /
     // replenish): two rows in flight per group keeps it spill-free
 #define X_(L, V, G) \
-    if (lpr == L && vpl == V) return launch_build_compat_t<Cfg<L, V>, (G < 2 ? G : 2)>(a, s);
+    if (lpr == L && vpl == V) return launch_build_compat_t<Cfg<L, V>, (G < 2 ? G : 2)>(a, waves, s);
     MH_FOR_EACH_CFG(X_)
 #undef X_
     return -3;

@@ -78,6 +78,31 @@ struct WaveStats {
     unsigned long long E = 0, X = 0, resets = 0;
 };
 
+// How the sequential (compat) walks evaluate distances and order their own
+// lanes.  WaveEval: everything on the calling wave (a 64-thread workgroup, so
+// __syncthreads only orders this wave).  The multi-wave build evaluator
+// (build.hip MwEval) has the same interface and spreads each batch of rows
+// over the workgroup's other waves.
+struct WaveEval {
+    uint32_t* list = nullptr;  // LDS candidate list (run_list)
+    template <class C, int G, class Sink>
+    __device__ __forceinline__ void run(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int cnt,
+                                        int metric, Sink&& sink) const {
+        eval_list<C, G>(g, q, qn, cid, cnt, metric, sink);
+    }
+    // rows list[0, cnt), sink called in list order
+    template <class C, int G, class Sink>
+    __device__ __forceinline__ void run_list(const GraphDev& g, const QReg<C>& q, float qn, int cnt, int metric,
+                                             Sink&& sink) const {
+        for (int b = 0; b < cnt; b += 64) {
+            const int c = min(64, cnt - b);
+            const uint32_t cid = lane_id() < c ? list[b + lane_id()] : 0u;
+            eval_list<C, G>(g, q, qn, cid, c, metric, sink);
+        }
+    }
+    __device__ __forceinline__ void sync() const { __syncthreads(); }
+};
+
 // ---------------------------------------------------------------------------
 // beam: sorted list of <= ef entries; stop when every entry is expanded
 // ---------------------------------------------------------------------------
@@ -139,17 +164,17 @@ struct CompatSmem {
     uint32_t* ri;  // result heap [k+2]
 };
 
-template <class C, int G, bool COH = false>
+template <class C, int G, bool COH = false, class Ev = WaveEval>
 __device__ __forceinline__ int compat_layer(const GraphDev& g, int layer, uint32_t entry, int k, int ef, const QReg<C>& q, float qn,
-                            CompatSmem& S, WaveStats& st, int& err) {
+                            CompatSmem& S, WaveStats& st, int& err, const Ev& ev = Ev()) {
     const int lane = lane_id();
     if (entry == EMPTY_ID) return 0;
     const int vsize = 1 << S.vlog2, vmask = vsize - 1;
     vis_clear(S.vis, vsize);
-    __syncthreads();
+    ev.sync();
     GHeap cand{S.cd, S.ci, 0}, res{S.rd, S.ri, 0};
     float d0 = 0.f;
-    eval_list<C, G>(g, q, qn, entry, 1, g.metric, [&](float d, uint32_t) { d0 = d; });  // graph.go:112
+    ev.template run<C, G>(g, q, qn, entry, 1, g.metric, [&](float d, uint32_t) { d0 = d; });  // graph.go:112
     st.E += 1;
     if (lane == 0) vis_probe(S.vis, vmask, entry);  // graph.go:123
     gh_push(cand, d0, entry);                        // graph.go:109-114
@@ -179,7 +204,7 @@ __device__ __forceinline__ int compat_layer(const GraphDev& g, int layer, uint32
         int cnt;
         const uint32_t cid = compact(nb, pr == 1, cnt);
         st.E += cnt;
-        eval_list<C, G>(g, q, qn, cid, cnt, g.metric, [&](float dist, uint32_t u) {  // graph.go:146-159
+        ev.template run<C, G>(g, q, qn, cid, cnt, g.metric, [&](float dist, uint32_t u) {  // graph.go:146-159
             improved = improved || (res.n > 0 && dist < res.d[0]);
             if (res.n < k) {
                 gh_push(res, dist, u);

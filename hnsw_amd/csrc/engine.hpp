@@ -83,7 +83,7 @@ struct CompatBuildArgs {
     int* err;
     int vis_log2;
 };
-int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, hipStream_t s);
+int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, int waves, hipStream_t s);  // waves: 1 or 8
 
 // ---- delete (graph.go:843-895) ----
 struct DeleteArgs {
