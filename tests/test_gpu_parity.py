@@ -203,6 +203,23 @@ def test_compat_build_parity(H, O, n, d, metric, M, ml, ef):
     assert np.all(np.abs(gd[fin, 0] - rd[fin, 0]) <= TOL * np.maximum(1.0, np.abs(rd[fin, 0])))
 
 
+@pytest.mark.parametrize("metric,d", [(0, 48), (1, 768)])
+def test_compat_build_waves_identical(H, O, metric, d):
+    """The compat insert scored by the walking wave alone or by 8 waves builds
+    the same graph as the oracle."""
+    rng = np.random.default_rng(d)
+    n, M = 700, 10
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    lv = _levels(O, metric, M, 0.3, 20, 5, n)
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=0.3, EfSearch=20)
+    o.add(np.arange(n), X, lv)
+    for waves in (1, 8):
+        g = H.Graph(M=M, Ml=0.3, EfSearch=20, Distance=_metric_fn(H, metric), compat_waves=waves)
+        g.add_arrays(np.arange(n), X, levels=lv)
+        _same_graph(g.export(), o.export())
+        g.close()
+
+
 def test_entry_injection_and_incremental_adds(H, O):
     rng = np.random.default_rng(3)
     n, d = 900, 24
