@@ -64,3 +64,62 @@ def test_add_after_enqueued_search(H):
     assert np.array_equal(got[0].cpu().numpy(), want[0])
     assert np.array_equal(got[1].cpu().numpy().view(np.uint32), want[1].view(np.uint32))
     g.close()
+
+
+def test_thread_safety(H):
+    """graph_test.go:461-527 TestThreadSafety: 1000 concurrent operations (20 %
+    Add, 20 % Delete, 60 % Search) on one graph from 16 threads; the handle's
+    RWMutex serialises mutations.  As in the reference, an Add that descends
+    through a node deleted meanwhile fails with "no nodes found in neighborhood
+    search" (graph.go:489-505; the Go test only logs Add
+    errors); Deletes and Searches never fail.  Afterwards the graph validates
+    and searches."""
+    import threading
+
+    rng = np.random.default_rng(0)
+    dims, num_nodes, num_ops = 3, 100, 1000
+    g = H.NewGraphWithConfig(16, 0.25, 20, H.EuclideanDistance)
+    for i in range(num_nodes):
+        g.Add(H.MakeNode(i, rng.random(dims).astype(np.float32)))
+    vecs = rng.random((num_ops, dims)).astype(np.float32)
+    errors, deleted, add_errors, added = [], [], [], []
+    lock = threading.Lock()
+
+    def op(i):
+        try:
+            if i % 5 == 0:
+                try:
+                    g.Add(H.MakeNode(num_nodes + i, vecs[i]))
+                    with lock:
+                        added.append(i)
+                except H.HnswError as e:
+                    with lock:
+                        add_errors.append(str(e))
+            elif i % 5 == 1:
+                if g.Delete(i % num_nodes):
+                    with lock:
+                        deleted.append(i % num_nodes)
+            else:
+                res = g.Search(vecs[i], 3)
+                assert len(res) <= 3
+        except Exception as e:  # noqa: BLE001 -- collected and reported below
+            with lock:
+                errors.append(repr(e))
+
+    def worker(t):
+        for i in range(t, num_ops, 16):
+            op(i)
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors[:5]
+    assert set(add_errors) <= {"no nodes found in neighborhood search"}, set(add_errors)
+    assert len(added) + len(add_errors) == num_ops // 5
+    g.Validate()
+    assert len(g.Search(rng.random(dims).astype(np.float32), 3)) == 3
+    live = num_nodes + len(added) - len(set(deleted))
+    assert live <= g.Len() <= live + len(add_errors)  # a failed Add may leave its node (Q18)
+    g.close()
