@@ -107,7 +107,8 @@ struct mhnsw_index {
     // immutable once added; import resets), per-chunk query planes, certificate state
     DevBuf<uint16_t> xsplit, qsplit;
     int64_t xsplit_rows = 0, xsplit_plane = 0;  // rows converted; plane stride they were written with
-    DevBuf<float> xbound, xmaxn;
+    DevBuf<float> xbound, xmaxn, xsegd;
+    DevBuf<uint32_t> xsegi;
     DevBuf<uint8_t> xflag;
     DevBuf<int32_t> xflagged, xnflag;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -704,6 +705,12 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             (r = ensure_buf(h, h->xflag, (size_t)qc)) || (r = ensure_buf(h, h->xflagged, (size_t)qc)) ||
             (r = ensure_buf(h, h->xnflag, 1)) || (r = ensure_buf(h, h->xmaxn, 1)))
             return r;
+        // selection: enough (query, row-segment) waves to stream the score rows at full rate
+        int nseg = (int)std::min<int64_t>(16, std::max<int64_t>(1, (16384 + qc - 1) / qc));
+        nseg = (int)std::max<int64_t>(1, std::min<int64_t>(nseg, (h->n + 4095) / 4096));
+        const int64_t seglen = ((h->n + nseg - 1) / nseg + 1023) / 1024 * 1024;
+        if ((r = ensure_buf(h, h->xsegd, (size_t)qc * nseg * kk)) || (r = ensure_buf(h, h->xsegi, (size_t)qc * nseg * kk)))
+            return r;
         if (split) {
             const int64_t plane = h->capn * h->pitch;
             if (h->xsplit.n < (size_t)plane * 2 || h->xsplit_plane != plane) {
@@ -762,6 +769,10 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             a.kk = kk;
             a.cand = h->cand.p;
             a.bound = h->xbound.p;
+            a.nseg = nseg;
+            a.seglen = seglen;
+            a.seg_d = h->xsegd.p;
+            a.seg_i = h->xsegi.p;
             int64_t* ok_ = dk + q0 * k;
             float* od_ = dd + q0 * k;
             int32_t* on_ = dn + q0;
@@ -930,6 +941,8 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->xsplit.p);
     F(h->qsplit.p);
     F(h->xbound.p);
+    F(h->xsegd.p);
+    F(h->xsegi.p);
     F(h->xmaxn.p);
     F(h->xflag.p);
     F(h->xflagged.p);

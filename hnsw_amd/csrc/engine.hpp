@@ -145,6 +145,10 @@ struct ExactArgs {
     int kk;               // preselect width (<= 64)
     uint32_t* cand;       // [B * kk]
     float* bound;         // [B] k_select: kk-th preselected score (+inf when fewer)
+    int nseg;             // k_select: row segments per query (<= 16), each seglen rows (multiple of 1024)
+    int64_t seglen;
+    float* seg_d;         // [B * nseg * kk] per-segment best scores / ids
+    uint32_t* seg_i;
     const uint8_t* only;  // k_select: skip rows b with only[b] == 0 (nullable)
     const uint16_t* Xh;   // split mode: bf16 hi / lo planes of X, K-blocked (k_split_rows)
     const uint16_t* Xl;

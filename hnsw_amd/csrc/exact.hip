@@ -405,8 +405,12 @@ int launch_exact_scores_x3(const ExactArgs& a, int tile, hipStream_t s) {
 // ---------------------------------------------------------------------------
 // top-kk preselect per query row (one wave per query)
 // ---------------------------------------------------------------------------
+// One wave per (query, row segment): the segment's best kk (score, id).  With
+// nseg segments per query the score matrix is streamed by B * nseg waves
+// instead of B (a 1024-query batch is only 4 waves per CU).
 __global__ __launch_bounds__(64) void k_select(ExactArgs a) {
-    const int64_t b = blockIdx.x;
+    const int64_t b = blockIdx.x / a.nseg;
+    const int sg = (int)(blockIdx.x % a.nseg);
     if (b >= a.B) return;
     if (a.only && !a.only[b]) return;
     const int lane = lane_id();
@@ -417,7 +421,9 @@ __global__ __launch_bounds__(64) void k_select(ExactArgs a) {
     const int kk = a.kk;
     float worst = inf;
     constexpr int U = 4;
-    for (int64_t base = 0; base < a.N; base += 256 * U) {
+    const int64_t seg = a.seglen;  // multiple of 256 * U
+    const int64_t lo = (int64_t)sg * seg, hi = min(lo + seg, a.N);
+    for (int64_t base = lo; base < hi; base += 256 * U) {
         float4 v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -430,7 +436,7 @@ __global__ __launch_bounds__(64) void k_select(ExactArgs a) {
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const int64_t e = base + u * 256 + lane * 4 + c;
-                const float x = e < a.N ? vv[c] : inf;
+                const float x = e < hi ? vv[c] : inf;
                 unsigned long long m = __ballot(x < worst);
                 while (m) {
                     const int src = __ffsll((long long)m) - 1;
@@ -447,8 +453,44 @@ __global__ __launch_bounds__(64) void k_select(ExactArgs a) {
             }
         }
     }
-    if (lane < kk) a.cand[b * kk + lane] = (L.i[0] == EMPTY_ID) ? EMPTY_ID : (L.i[0] & ID_MASK);
-    if (lane == 0 && a.bound) a.bound[b] = worst;
+    if (lane < kk) {
+        const size_t o = ((size_t)b * a.nseg + sg) * kk + lane;
+        a.seg_d[o] = L.d[0];
+        a.seg_i[o] = L.i[0] == EMPTY_ID ? EMPTY_ID : (L.i[0] & ID_MASK);
+    }
+}
+
+// Merge a query's nseg segment lists: the best kk by (score, id) and the
+// kk-th score (the certificate's bound; +inf when fewer than kk rows scored).
+__global__ __launch_bounds__(64) void k_select_merge(ExactArgs a) {
+    __shared__ float sd[16 * 64];
+    __shared__ uint32_t si[16 * 64];
+    const int64_t b = blockIdx.x;
+    if (b >= a.B) return;
+    if (a.only && !a.only[b]) return;
+    const int lane = lane_id();
+    const int kk = a.kk, n = a.nseg * kk;
+    const float inf = __int_as_float(0x7f800000);
+    for (int e = lane; e < n; e += 64) {
+        const size_t o = (size_t)b * n + e;
+        const uint32_t id = a.seg_i[o];
+        sd[e] = id == EMPTY_ID ? inf : a.seg_d[o];
+        si[e] = id;
+    }
+    __syncthreads();
+    for (int e = lane; e < kk; e += 64) a.cand[b * kk + e] = EMPTY_ID;
+    float kth = inf;
+    for (int e = lane; e < n; e += 64) {
+        const uint32_t id = si[e];
+        if (id == EMPTY_ID) continue;
+        const float d = sd[e];
+        int rank = 0;
+        for (int f = 0; f < n; ++f) rank += (si[f] != EMPTY_ID && lt_di(sd[f], si[f], d, id)) ? 1 : 0;
+        if (rank < kk) a.cand[b * kk + rank] = id;
+        if (rank == kk - 1) kth = d;
+    }
+    for (int o = 32; o >= 1; o >>= 1) kth = fminf(kth, __shfl_xor(kth, o, 64));
+    if (lane == 0 && a.bound) a.bound[b] = kth;
 }
 
 // ---------------------------------------------------------------------------
@@ -609,8 +651,9 @@ int launch_exact_scores(const ExactArgs& a, hipStream_t s) {
 
 int launch_exact_select(const ExactArgs& a, hipStream_t s) {
     if (a.B <= 0) return 0;
-    if (a.kk < 1 || a.kk > 64) return -4;
-    hipLaunchKernelGGL(k_select, dim3((unsigned)a.B), dim3(64), 0, s, a);
+    if (a.kk < 1 || a.kk > 64 || a.nseg < 1 || a.nseg > 16 || a.seglen % 1024) return -4;
+    hipLaunchKernelGGL(k_select, dim3((unsigned)(a.B * a.nseg)), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_select_merge, dim3((unsigned)a.B), dim3(64), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
