@@ -693,8 +693,8 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
     }
     HIPCHK(h, hipMemsetAsync(h->d_err, 0, sizeof(int), s));
     if (mode == MHNSW_MODE_EXACT) {
-        if (k > 64) return fail(h, MHNSW_EUNSUPPORTED, "exact mode supports k <= 64");
-        const int kk = h->exact_kk > 0 ? std::min(64, std::max(h->exact_kk, k)) : std::min(64, std::max(2 * k, k + 16));
+        if (k > 256) return fail(h, MHNSW_EUNSUPPORTED, "exact mode supports k <= 256");
+        const int kk = h->exact_kk > 0 ? std::min(256, std::max(h->exact_kk, k)) : std::min(256, std::max(2 * k, k + 16));
         const bool split = h->exact_precision == 1;
         const int64_t ldS = (h->n + 255) / 256 * 256;
         const int64_t budget = (int64_t)4 << 30;  // score workspace bytes
@@ -708,6 +708,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         // selection: enough (query, row-segment) waves to stream the score rows at full rate
         int nseg = (int)std::min<int64_t>(16, std::max<int64_t>(1, (16384 + qc - 1) / qc));
         nseg = (int)std::max<int64_t>(1, std::min<int64_t>(nseg, (h->n + 4095) / 4096));
+        nseg = std::max(1, std::min(nseg, 1024 / kk));  // merge holds nseg * kk entries
         const int64_t seglen = ((h->n + nseg - 1) / nseg + 1023) / 1024 * 1024;
         if ((r = ensure_buf(h, h->xsegd, (size_t)qc * nseg * kk)) || (r = ensure_buf(h, h->xsegi, (size_t)qc * nseg * kk)))
             return r;

@@ -11,7 +11,7 @@
 //             16x the f32-input rate per instruction), 256x256 block tile,
 //             8 waves of 128x64, operands staged by LDS-DMA into a 4-deep
 //             ring of swizzled buffers (three K-stages in flight).
-//  k_select : per query, stream its score row and keep the best kk (<= 64)
+//  k_select : per query, stream its score row and keep the best kk (<= 256)
 //             (score, id) in a lane-per-entry sorted list (threshold filter);
 //             the kk-th score is the query's preselection bound.
 //  k_rerank : recompute the kk candidates with the canonical distance engine,
@@ -408,6 +408,7 @@ int launch_exact_scores_x3(const ExactArgs& a, int tile, hipStream_t s) {
 // One wave per (query, row segment): the segment's best kk (score, id).  With
 // nseg segments per query the score matrix is streamed by B * nseg waves
 // instead of B (a 1024-query batch is only 4 waves per CU).
+template <int R>
 __global__ __launch_bounds__(64) void k_select(ExactArgs a) {
     const int64_t b = blockIdx.x / a.nseg;
     const int sg = (int)(blockIdx.x % a.nseg);
@@ -416,7 +417,7 @@ __global__ __launch_bounds__(64) void k_select(ExactArgs a) {
     const int lane = lane_id();
     const float* row = a.scores + (size_t)b * a.ldS;
     const float inf = __int_as_float(0x7f800000);
-    BList<1> L;
+    BList<R> L;
     bl_init(L);
     const int kk = a.kk;
     float worst = inf;
@@ -453,18 +454,23 @@ __global__ __launch_bounds__(64) void k_select(ExactArgs a) {
             }
         }
     }
-    if (lane < kk) {
-        const size_t o = ((size_t)b * a.nseg + sg) * kk + lane;
-        a.seg_d[o] = L.d[0];
-        a.seg_i[o] = L.i[0] == EMPTY_ID ? EMPTY_ID : (L.i[0] & ID_MASK);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int idx = r * 64 + lane;
+        if (idx < kk) {
+            const size_t o = ((size_t)b * a.nseg + sg) * kk + idx;
+            a.seg_d[o] = L.d[r];
+            a.seg_i[o] = L.i[r] == EMPTY_ID ? EMPTY_ID : (L.i[r] & ID_MASK);
+        }
     }
 }
 
 // Merge a query's nseg segment lists: the best kk by (score, id) and the
 // kk-th score (the certificate's bound; +inf when fewer than kk rows scored).
+constexpr int SEL_MERGE_MAX = 1024;  // nseg * kk
 __global__ __launch_bounds__(64) void k_select_merge(ExactArgs a) {
-    __shared__ float sd[16 * 64];
-    __shared__ uint32_t si[16 * 64];
+    __shared__ float sd[SEL_MERGE_MAX];
+    __shared__ uint32_t si[SEL_MERGE_MAX];
     const int64_t b = blockIdx.x;
     if (b >= a.B) return;
     if (a.only && !a.only[b]) return;
@@ -496,7 +502,7 @@ __global__ __launch_bounds__(64) void k_select_merge(ExactArgs a) {
 // ---------------------------------------------------------------------------
 // canonical re-rank of the kk candidates -> best k by (distance, id)
 // ---------------------------------------------------------------------------
-template <class C, int G>
+template <class C, int G, int R>
 __global__ __launch_bounds__(64) void k_rerank(const float* __restrict__ Q, GraphDev g, const uint32_t* cand, int kk,
                                                int64_t B, int k, int64_t* out_keys, float* out_dist, int32_t* out_n,
                                                int32_t* out_ids, CertArgs c) {
@@ -507,20 +513,27 @@ __global__ __launch_bounds__(64) void k_rerank(const float* __restrict__ Q, Grap
     QReg<C> q;
     load_query(q, Q + (size_t)b * C::PITCH);
     const float qn = query_norm(q);
-    const uint32_t cc = lane < kk ? cand[b * kk + lane] : EMPTY_ID;
-    int cnt;
-    const uint32_t cid = compact(cc, cc != EMPTY_ID, cnt);
-    BList<1> L;
+    BList<R> L;
     bl_init(L);
-    eval_list<C, G>(g, q, qn, cid, cnt, g.metric, [&](float d, uint32_t u) { bl_insert(L, k, d, u); });
-    const bool ok = lane < k && L.i[0] != EMPTY_ID;
-    if (lane < k) {
-        const uint32_t id = L.i[0] & ID_MASK;
-        out_keys[b * k + lane] = ok ? g.keys[id] : (int64_t)-1;
-        out_dist[b * k + lane] = ok ? L.d[0] : __int_as_float(0x7f800000);
-        if (out_ids) out_ids[b * k + lane] = ok ? (int32_t)id : -1;
+    for (int c0 = 0; c0 < kk; c0 += 64) {
+        const uint32_t cc = c0 + lane < kk ? cand[b * kk + c0 + lane] : EMPTY_ID;
+        int cnt;
+        const uint32_t cid = compact(cc, cc != EMPTY_ID, cnt);
+        eval_list<C, G>(g, q, qn, cid, cnt, g.metric, [&](float d, uint32_t u) { bl_insert(L, k, d, u); });
     }
-    const int nv = __popcll(__ballot(ok));
+    int nv = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int idx = r * 64 + lane;
+        const bool okr = idx < k && L.i[r] != EMPTY_ID;
+        if (idx < k) {
+            const uint32_t id = L.i[r] & ID_MASK;
+            out_keys[b * k + idx] = okr ? g.keys[id] : (int64_t)-1;
+            out_dist[b * k + idx] = okr ? L.d[r] : __int_as_float(0x7f800000);
+            if (out_ids) out_ids[b * k + idx] = okr ? (int32_t)id : -1;
+        }
+        nv += __popcll(__ballot(okr));
+    }
     if (lane == 0) out_n[b] = nv;
     if (c.bound) {
         const float t = c.bound[b];
@@ -651,8 +664,14 @@ int launch_exact_scores(const ExactArgs& a, hipStream_t s) {
 
 int launch_exact_select(const ExactArgs& a, hipStream_t s) {
     if (a.B <= 0) return 0;
-    if (a.kk < 1 || a.kk > 64 || a.nseg < 1 || a.nseg > 16 || a.seglen % 1024) return -4;
-    hipLaunchKernelGGL(k_select, dim3((unsigned)(a.B * a.nseg)), dim3(64), 0, s, a);
+    if (a.kk < 1 || a.kk > 256 || a.nseg < 1 || a.nseg * a.kk > SEL_MERGE_MAX || a.seglen % 1024) return -4;
+    const dim3 grid((unsigned)(a.B * a.nseg));
+    if (a.kk <= 64)
+        hipLaunchKernelGGL(k_select<1>, grid, dim3(64), 0, s, a);
+    else if (a.kk <= 128)
+        hipLaunchKernelGGL(k_select<2>, grid, dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_select<4>, grid, dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_select_merge, dim3((unsigned)a.B), dim3(64), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -673,12 +692,16 @@ int launch_rerank(const float* Q, const GraphDev& g, const uint32_t* cand, int k
                   int64_t* out_keys, float* out_dist, int32_t* out_n, int32_t* out_ids, const CertArgs& c,
                   hipStream_t s) {
     if (B <= 0) return 0;
-    if (k > 64 || kk > 64) return -4;
-#define X_(L, V, G)                                                                                           \
-    if (lpr == L && vpl == V) {                                                                               \
-        hipLaunchKernelGGL((k_rerank<Cfg<L, V>, G>), dim3((unsigned)B), dim3(64), 0, s, Q, g, cand, kk, B, k, \
-                           out_keys, out_dist, out_n, out_ids, c);                                            \
-        return hipGetLastError() == hipSuccess ? 0 : -1;                                                      \
+    if (k > 256 || kk > 256 || k > kk) return -4;
+#define X_(L, V, G)                                                                                              \
+    if (lpr == L && vpl == V) {                                                                                  \
+        if (k <= 64)                                                                                             \
+            hipLaunchKernelGGL((k_rerank<Cfg<L, V>, G, 1>), dim3((unsigned)B), dim3(64), 0, s, Q, g, cand, kk, B, k, \
+                               out_keys, out_dist, out_n, out_ids, c);                                           \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_rerank<Cfg<L, V>, G, 4>), dim3((unsigned)B), dim3(64), 0, s, Q, g, cand, kk, B, k, \
+                               out_keys, out_dist, out_n, out_ids, c);                                           \
+        return hipGetLastError() == hipSuccess ? 0 : -1;                                                         \
     }
     MH_FOR_EACH_CFG(X_)
 #undef X_

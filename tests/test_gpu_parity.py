@@ -384,6 +384,26 @@ def test_exact_precision_parity(H, O, metric, d, precision):
     g.close()
 
 
+@pytest.mark.parametrize("k", [65, 200, 256])
+def test_exact_large_k(H, O, k):
+    """k up to 256 (multi-row preselection / re-rank lists), both precisions."""
+    rng = np.random.default_rng(k)
+    n, d = 3000, 48
+    X, Q = _exact_inputs(rng, n, d, 40, 0)
+    g = H.Graph(M=8, Ml=0.25, EfSearch=32, Distance=H.CosineDistance, build_mode=H.BUILD_BATCH, ef_construction=32)
+    g.add_arrays(np.arange(n), X)
+    o = O.Graph(metric=0, order=O.ORDER_DEV, M=8, M0=16, Ml=0.25, EfSearch=32)
+    o.import_graph(**g.export())
+    rk, rd, rn = o.search(Q, k, mode=O.MODE_EXACT)
+    for precision in (1, 0):
+        g.set_option("exact_precision", precision)
+        gk, gd, gn = g.search_arrays(Q, k, mode=H.MODE_EXACT)
+        _same_results(gk, gd, gn, rk, rd, rn)
+    with pytest.raises(H.HnswError, match="k <= 256"):
+        g.search_arrays(Q[:1], 257, mode=H.MODE_EXACT)
+    g.close()
+
+
 @pytest.mark.parametrize("metric", [0, 1])
 def test_exact_certificate_fallback(H, O, metric):
     """Preselection width kk = k leaves no margin, so the certificate fails for
