@@ -65,7 +65,8 @@ struct mhnsw_index {
     int exact_kk = 0;
     int exact_precision = 1;
     int exact_tile = 0;       // bf16x3 GEMM tile variant (exact.hip launch_exact_scores_x3)
-    int compat_waves = 8;     // compat insert: waves scoring each distance batch (1 = the walking wave alone)  // 0: f32-input MFMA scores, 1: bf16x3 split MFMA scores (both certified)
+    int compat_waves = 8;
+    int upper_ef = 1;         // beam search: upper-layer descent width     // compat insert: waves scoring each distance batch (1 = the walking wave alone)  // 0: f32-input MFMA scores, 1: bf16x3 split MFMA scores (both certified)
     // shape
     int dim = 0, pitch = 0, lpr = 0, vpl = 0;
     bool layers_exist = false;
@@ -826,6 +827,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         a.stats = h->d_stats;
         a.err = h->d_err;
         a.vis_log2 = h->vis_log2;
+        a.upper_ef = h->upper_ef;
         if (mode == MHNSW_MODE_BEAM) {
             if (std::max(ef, k) > 512) return fail(h, MHNSW_EUNSUPPORTED, "beam mode supports max(ef,k) <= 512");
             if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
@@ -1015,6 +1017,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
         h->exact_kk = (int)v;
     } else if (n == "exact_tile") {
         h->exact_tile = (int)v;
+    } else if (n == "upper_ef") {
+        if (v < 1 || v > 64) return fail(h, MHNSW_EINVAL, "upper_ef must be in [1, 64]");
+        h->upper_ef = (int)v;
     } else if (n == "compat_waves") {
         if (v != 1 && v != 8) return fail(h, MHNSW_EINVAL, "compat_waves must be 1 or 8");
         h->compat_waves = (int)v;
@@ -1043,6 +1048,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "exact_precision") *v = h->exact_precision;
     else if (n == "exact_tile") *v = h->exact_tile;
     else if (n == "compat_waves") *v = h->compat_waves;
+    else if (n == "upper_ef") *v = h->upper_ef;
     else if (n == "strkey_relabels") *v = h->relabels;
     else if (n == "strkeys") *v = (int64_t)h->s2l.size();
     else if (n == "pitch") *v = h->pitch;

@@ -42,6 +42,7 @@ struct SearchArgs {
     unsigned long long* stats;    // [0]=dist evals [1]=expansions [2]=visited resets
     int* err;                     // set to nonzero on visited overflow (compat)
     int vis_log2;
+    int upper_ef;                 // beam: width of the upper-layer descent (1 = greedy, the reference's k = 1)
 };
 
 // negative-example re-ranking epilogue (graph.go:1116-1537)

@@ -188,7 +188,7 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
                 if (e < 0) continue;
                 ep = (uint32_t)e;
             }
-            beam_layer<C, 1, G>(a.g, l, ep, 1, q, qn, L1, smem, a.vis_log2, st);
+            beam_layer<C, 1, G>(a.g, l, ep, a.upper_ef, q, qn, L1, smem, a.vis_log2, st);
             float d;
             uint32_t id;
             bl_at(L1, 0, d, id);

@@ -74,7 +74,10 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * (heuristic slack x100: c is dropped when alpha*d(c,kept) < d(u,c); 100 = HNSW
  * Alg. 4), "batch_min", "batch_max", "batch_ratio_pct", "vis_log2", "exact_kk",
  * "exact_precision" (exact-mode scoring: 0 f32-input MFMA, 1 bf16x3 split MFMA;
- * both preselect, re-rank canonically and certify, so results are identical) */
+ * both preselect, re-rank canonically and certify, so results are identical),
+ * "exact_tile", "compat_waves" (1 or 8 waves scoring the compat insert's
+ * distance batches), "upper_ef" (beam mode: upper-layer descent width, 1 =
+ * greedy); read-only: "pitch", "capacity", "strkeys", "strkey_relabels" */
 int mhnsw_set_option(mhnsw_index *h, const char *name, int64_t value);
 int mhnsw_get_option(const mhnsw_index *h, const char *name, int64_t *value);
 /* Graph.Validate (graph.go:916-937) */

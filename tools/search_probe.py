@@ -24,9 +24,11 @@ del X
 G = Searcher(g, 4096, 10, d, dev)
 tk, td, tn = (x.clone() for x in G.run(Q[:4096], H.MODE_EXACT, 0))
 S = Searcher(g, B, 10, d, dev)
-for vl in (12, 11, 13):
-    g.set_option("vis_log2", vl)
-    for ef in (64,):
+knobs = [("vis_log2", 12), ("upper_ef", 1), ("upper_ef", 4), ("upper_ef", 16)]
+for name, val in knobs:
+    g.set_option(name, val)
+    vl = f"{name}={val}"
+    for ef in (56, 64):
         S.run(Q, H.MODE_BEAM, ef)
         g.reset_stats()
         torch.cuda.synchronize()
@@ -37,5 +39,5 @@ for vl in (12, 11, 13):
         dt = (time.perf_counter() - t0) / 5
         st = g.stats()
         r = recall_at_k(k_[:4096], n_[:4096], tk, tn, 10)
-        print(f"vis_log2={vl} ef={ef} qps={B / dt / 1e6:.3f}M recall={r:.4f} E={st['search_dist_evals'] / 5 / B:.1f} "
+        print(f"{vl} ef={ef} qps={B / dt / 1e6:.3f}M recall={r:.4f} E={st['search_dist_evals'] / 5 / B:.1f} "
               f"resets/q={st['visited_resets'] / 5 / B:.3f}", flush=True)
