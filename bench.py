@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--efc", type=int, default=400)
     p.add_argument("--keep-pruned", type=int, default=1)
     p.add_argument("--alpha", type=int, default=115, help="heuristic slack x100 (prune_alpha_pct; 100 = HNSW Alg. 4)")
+    p.add_argument("--screen", type=int, default=1,
+                   help="fp16 screening copy (1) or plain f32 evaluation of every candidate (0); same results")
     p.add_argument("--ef-sweep", default="32,48,64,72,80,96,128,256",
                    help="extra operating points (ef values) reported at N=1; '' disables")
     p.add_argument("--seed", type=int, default=1234)
@@ -170,7 +172,7 @@ def main():
     X = gen_vectors(a.nbase, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=base_off)
     g = H.Graph(M=a.M, Ml=0.25, EfSearch=a.ef, Distance=metric, Rng=a.seed + (rank if shard else 0),
                 build_mode=H.BUILD_BATCH, m0=a.M0, ef_construction=a.efc, heuristic=2, keep_pruned=a.keep_pruned,
-                prune_alpha_pct=a.alpha)
+                prune_alpha_pct=a.alpha, screen=a.screen)
     g.reserve(a.nbase, a.dim)
     keys = np.arange(base_off, base_off + a.nbase, dtype=np.int64)
     torch.cuda.synchronize()
@@ -236,11 +238,15 @@ def main():
     cap0 = a.M0 + 1
 
     def alg_bytes_of(stats, launches):
+        # f32 row + norm per f32 evaluation, fp16 row + norm + unscale per
+        # screened candidate, one adjacency row per expansion, the query
         E = stats["search_dist_evals"] / launches
+        Sc = stats["search_screened"] / launches
+        F = stats["search_f32_evals"] / launches
         Xp = stats["search_expansions"] / launches
-        return E * 4 * a.dim + Xp * 4 * cap0 + a.batch * 4 * a.dim, E, Xp
+        return F * (4 * a.dim + 4) + Sc * (2 * a.dim + 8) + Xp * 4 * cap0 + a.batch * 4 * a.dim, E, Xp, Sc, F
 
-    alg_bytes, E, Xp = alg_bytes_of(st, a.steps)
+    alg_bytes, E, Xp, Sc, F = alg_bytes_of(st, a.steps)
     kms = float(np.mean(kernel_ms))
     achieved = alg_bytes / (kms * 1e-3) / 1e9
 
@@ -259,7 +265,7 @@ def main():
                 ms.append(g.last_kernel_ms())
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t1) / 3
-            ab, e_, _ = alg_bytes_of(g.stats(), 3)
+            ab, e_, _, _, _ = alg_bytes_of(g.stats(), 3)
             km = float(np.mean(ms))
             points.append({"ef": ef, "recall_at_10": round(r, 4), "qps": round(a.batch / dt, 1),
                            "kernel_ms": round(km, 4), "dist_evals_per_query": round(e_ / a.batch, 1),
@@ -270,7 +276,7 @@ def main():
         try:
             pm = json.load(open(a.pmc_json))
             want = dict(n=a.nbase, dim=a.dim, batch=a.batch, ef=a.ef, efc=a.efc, m0=a.M0, keep_pruned=a.keep_pruned,
-                        alpha=a.alpha)
+                        alpha=a.alpha, screen=a.screen)
             if all(pm.get(k) == v for k, v in want.items()):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
@@ -297,6 +303,8 @@ def main():
             "n_base": a.nbase * (world if shard else 1), "dim": a.dim, "batch_per_gpu": a.batch, "ef": a.ef,
             "k": a.k, "M": a.M, "M0": a.M0, "ef_construction": a.efc, "keep_pruned": a.keep_pruned,
             "prune_alpha": a.alpha / 100,
+            "screen": ("fp16 row copy rejects candidates whose f32 distance provably exceeds the list's worst; "
+                       "every reported distance is f32, results identical to screen=0") if a.screen else "off",
             "parallelism": f"{'shard' if shard else 'replica'}{world}",
         },
         "recall_at_10": round(recall, 4),
@@ -306,6 +314,7 @@ def main():
             "kernel": "k_search_beam", "kernel_ms": round(kms, 4),
             "alg_bytes_per_launch": int(alg_bytes),
             "dist_evals_per_query": round(E / a.batch, 1), "expansions_per_query": round(Xp / a.batch, 1),
+            "screened_per_query": round(Sc / a.batch, 1), "f32_evals_per_query": round(F / a.batch, 1),
         },
         "build": {"inserts_per_s": round(a.nbase / build_s, 1), "seconds": round(build_s, 2),
                   "dist_evals_per_insert": round(bstats["build_dist_evals"] / a.nbase, 1),

@@ -63,10 +63,11 @@ struct mhnsw_index {
     int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
     int vis_log2 = 12;
     int exact_kk = 0;
-    int exact_precision = 1;
+    int exact_precision = 1;  // 0: f32-input MFMA scores, 1: bf16x3 split MFMA scores (both certified)
     int exact_tile = 0;       // bf16x3 GEMM tile variant (exact.hip launch_exact_scores_x3)
-    int compat_waves = 8;
-    int upper_ef = 1;         // beam search: upper-layer descent width     // compat insert: waves scoring each distance batch (1 = the walking wave alone)  // 0: f32-input MFMA scores, 1: bf16x3 split MFMA scores (both certified)
+    int compat_waves = 8;     // compat insert: waves scoring each distance batch (1 = the walking wave alone)
+    int upper_ef = 1;         // beam search: upper-layer descent width
+    int screen = 1;           // beam search: fp16 screening copy of the rows (results unchanged)
     // shape
     int dim = 0, pitch = 0, lpr = 0, vpl = 0;
     bool layers_exist = false;
@@ -76,6 +77,8 @@ struct mhnsw_index {
     // device state
     float* vecs = nullptr;
     float* norms = nullptr;
+    uint16_t* h16 = nullptr;  // fp16 screening copy [capn * pitch] (screen = 1)
+    float* h16inv = nullptr;  // [capn] per-row unscale (NaN: never screened)
     int64_t* keys = nullptr;
     int32_t* levels = nullptr;
     uint8_t* dead = nullptr;  // [capn] deleted rows (graph.go:843-864)
@@ -288,6 +291,10 @@ int ensure_capacity(mhnsw_index* h, int64_t need) {
     int r;
     if ((r = grow(h, h->vecs, oc * h->pitch, nc * h->pitch, 0))) return r;
     if ((r = grow(h, h->norms, oc, nc, 0))) return r;
+    if (h->screen) {
+        if ((r = grow(h, h->h16, oc * h->pitch, nc * h->pitch, 0))) return r;
+        if ((r = grow(h, h->h16inv, oc, nc, 0xFF))) return r;
+    }
     if ((r = grow(h, h->keys, oc, nc, 0))) return r;
     if ((r = grow(h, h->levels, oc, nc, 0))) return r;
     if ((r = grow(h, h->dead, oc, nc, 0))) return r;
@@ -337,6 +344,8 @@ GraphDev graph_view(const mhnsw_index* h) {
     g.capn = (uint32_t)std::max<int64_t>(h->capn, 1);
     g.err = h->d_err;
     g.dead = h->any_dead ? h->dead : nullptr;
+    g.h16 = h->screen ? h->h16 : nullptr;
+    g.h16inv = h->screen ? h->h16inv : nullptr;
     return g;
 }
 
@@ -576,6 +585,7 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     }
     LCHK(h, launch_pad_rows(src, n, dim, h->vecs + (size_t)n0 * h->pitch, h->pitch, h->stream));
     LCHK(h, launch_norms(h->vecs, n0, n1, h->pitch, h->lpr, h->vpl, h->norms, h->stream));
+    if (h->screen) LCHK(h, launch_h16_rows(h->vecs, n0, n1, h->pitch, h->h16, h->h16inv, h->stream));
     // host bookkeeping: layer membership, counts, entries
     const bool compat = h->build_mode == MHNSW_BUILD_COMPAT;
     h->hmask.resize(n1, 0u);
@@ -883,12 +893,12 @@ int mhnsw_create(int metric, int M, double ml, int ef_search, uint64_t seed, mhn
         delete h;
         return fail(nullptr, MHNSW_EDEVICE, "no HIP device available");
     }
-    if (hipMalloc(&h->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(&h->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&h->d_err, sizeof(int)) != hipSuccess || hipMalloc(&h->touched_cnt, 16) != hipSuccess ||
         hipMalloc(&h->d_layer_entry, MH_MAXL * 4) != hipSuccess ||
         hipMalloc(&h->d_layers, MH_MAXL * sizeof(LayerDev)) != hipSuccess || hipEventCreate(&h->ev0) != hipSuccess ||
         hipEventCreate(&h->ev1) != hipSuccess || hipEventCreateWithFlags(&h->scr_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->meta_ev, hipEventDisableTiming) != hipSuccess || hipMemset(h->d_stats, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
+        hipEventCreateWithFlags(&h->meta_ev, hipEventDisableTiming) != hipSuccess || hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
         mhnsw_destroy(h);
         return fail(nullptr, MHNSW_EDEVICE, "device initialisation failed");
     }
@@ -905,6 +915,8 @@ void mhnsw_destroy(mhnsw_index* h) {
     };
     F(h->vecs);
     F(h->norms);
+    F(h->h16);
+    F(h->h16inv);
     F(h->keys);
     F(h->levels);
     F(h->dead);
@@ -1020,6 +1032,23 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "upper_ef") {
         if (v < 1 || v > 64) return fail(h, MHNSW_EINVAL, "upper_ef must be in [1, 64]");
         h->upper_ef = (int)v;
+    } else if (n == "screen") {
+        if (v != 0 && v != 1) return fail(h, MHNSW_EINVAL, "screen must be 0 or 1");
+        if ((int)v == h->screen) return MHNSW_OK;
+        int r = drain(h);
+        if (r) return r;
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        if (!v) {
+            (void)hipFree(h->h16);
+            (void)hipFree(h->h16inv);
+            h->h16 = nullptr;
+            h->h16inv = nullptr;
+        } else if (h->capn > 0) {
+            if ((r = grow(h, h->h16, 0, h->capn * h->pitch, 0)) || (r = grow(h, h->h16inv, 0, h->capn, 0xFF))) return r;
+            LCHK(h, launch_h16_rows(h->vecs, 0, h->n, h->pitch, h->h16, h->h16inv, h->stream));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+        }
+        h->screen = (int)v;
     } else if (n == "compat_waves") {
         if (v != 1 && v != 8) return fail(h, MHNSW_EINVAL, "compat_waves must be 1 or 8");
         h->compat_waves = (int)v;
@@ -1049,6 +1078,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "exact_tile") *v = h->exact_tile;
     else if (n == "compat_waves") *v = h->compat_waves;
     else if (n == "upper_ef") *v = h->upper_ef;
+    else if (n == "screen") *v = h->screen;
     else if (n == "strkey_relabels") *v = h->relabels;
     else if (n == "strkeys") *v = (int64_t)h->s2l.size();
     else if (n == "pitch") *v = h->pitch;
@@ -1201,6 +1231,8 @@ void reset_graph(mhnsw_index* h) {
     };
     F(h->vecs);
     F(h->norms);
+    F(h->h16);
+    F(h->h16inv);
     F(h->keys);
     F(h->levels);
     F(h->dead);
@@ -1253,6 +1285,7 @@ int import_csr(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t
     HIPCHK(h, hipMemcpy(h->tmp.p, vecs, (size_t)N * dim * 4, hipMemcpyHostToDevice));
     LCHK(h, launch_pad_rows(h->tmp.p, N, dim, h->vecs, h->pitch, h->stream));
     LCHK(h, launch_norms(h->vecs, 0, N, h->pitch, h->lpr, h->vpl, h->norms, h->stream));
+    if (h->screen) LCHK(h, launch_h16_rows(h->vecs, 0, N, h->pitch, h->h16, h->h16inv, h->stream));
     h->xsplit_rows = 0;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     std::vector<int32_t> row;
@@ -1772,21 +1805,21 @@ int mhnsw_preview_levels(mhnsw_index* h, int64_t n, int32_t* out) {
 
 int mhnsw_stats(const mhnsw_index* h, int64_t* out, int n) {
     mhnsw_index* hh = const_cast<mhnsw_index*>(h);
-    unsigned long long d[8];
+    unsigned long long d[16];
     HIPCHK(hh, hipDeviceSynchronize());
     HIPCHK(hh, hipMemcpy(d, h->d_stats, sizeof(d), hipMemcpyDeviceToHost));
     int err = 0;
     HIPCHK(hh, hipMemcpy(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (err & 4) return fail(hh, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
-    const int64_t v[8] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4],
-                          (int64_t)d[5], (int64_t)d[6], h->stats_host[6], (int64_t)d[3]};
-    for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
+    const int64_t v[10] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4], (int64_t)d[5],
+                           (int64_t)d[6], h->stats_host[6], (int64_t)d[3], (int64_t)d[8], (int64_t)d[9]};
+    for (int i = 0; i < n && i < 10; ++i) out[i] = v[i];
     return 0;
 }
 
 int mhnsw_reset_stats(mhnsw_index* h) {
     HIPCHK(h, hipDeviceSynchronize());
-    HIPCHK(h, hipMemset(h->d_stats, 0, 8 * sizeof(unsigned long long)));
+    HIPCHK(h, hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)));
     for (auto& v : h->stats_host) v = 0;
     return 0;
 }

@@ -50,6 +50,12 @@ struct GraphDev {
     uint32_t capn;  // rows allocated: every gathered id is checked against it
     int* err;       // bit 4: out-of-range id seen (load clamped, no fault)
     const uint8_t* dead;  // [cap_nodes] 1 = deleted (nullptr until the first Delete)
+    // fp16 screening copy (nullptr = off): row r scaled by a power of two into
+    // [2^14, 2^15) and rounded to fp16; h16inv[r] undoes the scale (NaN marks a
+    // row the screen must never reject).  Only ever used to skip candidates
+    // that the f32 distance provably rejects.
+    const uint16_t* h16;      // [cap_nodes * pitch]
+    const float* h16inv;      // [cap_nodes]
 };
 
 __device__ __forceinline__ bool is_dead(const GraphDev& g, uint32_t id) { return g.dead && g.dead[id]; }
@@ -241,6 +247,79 @@ __device__ __forceinline__ float eval_rows(const QReg<C>& q, const float* __rest
         p[g] = acc;
     }
     return reduce_rows<G, C::LPR>(p);
+}
+
+// Approximate sums from the fp16 screening copy, same lane/row mapping as
+// eval_rows.  Dot: sum q_i * h_i (the caller applies the row's h16inv).
+// L2: sum (q_i - h_i * inv_g)^2 with inv[g] the row's h16inv.
+template <class C, int G, bool L2>
+__device__ __forceinline__ float eval_rows_h16(const QReg<C>& q, const uint16_t* __restrict__ H, int pitch,
+                                               const uint32_t (&ids)[G], const bool (&valid)[G],
+                                               const float (&inv)[G]) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const int sub = lane_id() & (C::LPR - 1);
+    h4 x[G][C::VPL];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint16_t* rp = H + (size_t)ids[g] * (size_t)pitch + sub * 4;
+#pragma unroll
+        for (int v = 0; v < C::VPL; ++v) {
+            if (valid[g])
+                x[g][v] = *reinterpret_cast<const h4*>(rp + v * C::LPR * 4);
+            else
+                x[g][v] = h4{0, 0, 0, 0};
+        }
+    }
+    float p[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        float acc = 0.f;
+#pragma unroll
+        for (int v = 0; v < C::VPL; ++v) {
+            const float x0 = (float)x[g][v].x, x1 = (float)x[g][v].y, x2 = (float)x[g][v].z, x3 = (float)x[g][v].w;
+            if (L2) {
+                const float t0 = fmaf(x0, inv[g], -q.v[v].x), t1 = fmaf(x1, inv[g], -q.v[v].y);
+                const float t2 = fmaf(x2, inv[g], -q.v[v].z), t3 = fmaf(x3, inv[g], -q.v[v].w);
+                acc = fmaf(t0, t0, acc);
+                acc = fmaf(t1, t1, acc);
+                acc = fmaf(t2, t2, acc);
+                acc = fmaf(t3, t3, acc);
+            } else {
+                acc = fmaf(x0, q.v[v].x, acc);
+                acc = fmaf(x1, q.v[v].y, acc);
+                acc = fmaf(x2, q.v[v].z, acc);
+                acc = fmaf(x3, q.v[v].w, acc);
+            }
+        }
+        p[g] = acc;
+    }
+    return reduce_rows<G, C::LPR>(p);
+}
+
+// Screening bounds.  With x' the fp16 copy of row x
+// (|x' - x| <= 2^-11 |x| componentwise, plus a subnormal term far below 2^-30 |x|):
+//   cosine: |approx - f32| <= 2^-11 (Cauchy-Schwarz on sum q_i (x'_i - x_i))
+//           + accumulation / finalize rounding (< 2^-17 for dim <= 4096)
+//   L2:     | |q - x'| - |q - x| | <= |x' - x| <= 2^-11 |x|  (triangle inequality)
+//           + relative rounding of both computed distances (< 2^-16)
+// Valid while no intermediate over/underflows: rows are screened only when
+// 2^-50 <= max|x_i| <= 2^50 (else h16inv = NaN) and queries when
+// 2^-40 <= |q| <= 2^40.
+constexpr float H16_DELTA_COS = 0.00048828125f + 0.0000152587890625f;  // 2^-11 + 2^-16
+constexpr float H16_REL_L2 = 1.0f - 0.000030517578125f;                // 1 - 2^-15
+constexpr float H16_ABS_L2 = 0.00048828125f * 1.000030517578125f;      // 2^-11 (1 + 2^-15)
+constexpr float H16_MIN_L2 = 8.881784197001252e-16f;                   // 2^-50
+__device__ __forceinline__ bool h16_query_ok(float qn) {
+    return qn >= 9.094947017729282e-13f && qn <= 1.099511627776e12f;  // [2^-40, 2^40]; false for NaN
+}
+// true when the f32 distance of this row is certainly > wd
+__device__ __forceinline__ bool h16_rejects(int metric, float s, float inv, float xn, float qn, float wd) {
+    if (metric == COSINE) {
+        const float da = 1.0f - (s * inv) / (xn * qn);
+        return da > wd + H16_DELTA_COS;
+    }
+    const float da = sqrtf(s);
+    return da >= H16_MIN_L2 && da * H16_REL_L2 - H16_ABS_L2 * xn > wd;
 }
 
 // finalize a canonical sum into a distance (distance.go:15-23 semantics)

@@ -74,8 +74,66 @@ __device__ __forceinline__ uint32_t compact(uint32_t v, bool keep, int& cnt) {
     return push_to(v, dst);
 }
 
+// Screened evaluation for the sorted-list searches: candidates whose fp16
+// screening distance proves the f32 distance exceeds `wd` (the list's worst
+// entry before this batch, which only decreases) are dropped; the rest go
+// through eval_list, so every distance that reaches the sink is the canonical
+// f32 one and the list evolves exactly as without the screen.
+// Returns the number of rows evaluated in f32.
+template <class C, int G, class Sink>
+__device__ __forceinline__ int eval_screened(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int cnt,
+                                             int metric, float wd, Sink&& sink) {
+    constexpr int GH = (2 * G <= C::LPR) ? 2 * G : G;
+    using RM = RowMap<C, GH>;
+    const int lane = lane_id();
+    bool rej = false;  // lane t: candidate t is rejected
+    for (int base = 0; base < cnt; base += RM::T) {
+        uint32_t ids[GH];
+        bool valid[GH];
+        float inv[GH];
+#pragma unroll
+        for (int gg = 0; gg < GH; ++gg) {
+            const int t = base + RM::reg_row(gg, lane);
+            valid[gg] = t < cnt;
+            if constexpr (C::RPI == 1)
+                ids[gg] = rl_u(cid, (base + gg) & 63);
+            else
+                ids[gg] = shfl_u(cid, t & 63);
+            ids[gg] = valid[gg] ? guard_id(g, ids[gg]) : 0u;
+        }
+        float s;
+        if (metric == EUCLIDEAN) {
+#pragma unroll
+            for (int gg = 0; gg < GH; ++gg) inv[gg] = g.h16inv[ids[gg]];
+            s = eval_rows_h16<C, GH, true>(q, g.h16, g.pitch, ids, valid, inv);
+        } else {
+#pragma unroll
+            for (int gg = 0; gg < GH; ++gg) inv[gg] = 1.f;
+            s = eval_rows_h16<C, GH, false>(q, g.h16, g.pitch, ids, valid, inv);
+        }
+        const int town = base + RM::owned_row(lane);
+        const uint32_t idown = shfl_u(cid, town & 63);  // all lanes: a permute reads inactive lanes as 0
+        bool r = false;
+        if (town < cnt) {
+            const uint32_t id = guard_id(g, idown);
+            r = h16_rejects(metric, s, g.h16inv[id], g.norms[id], qn, wd);
+        }
+        // hand row t's verdict from its owner lane to lane t
+        const int t = lane - base;
+        const int src = (t >= 0 && t < RM::T) ? RM::owner(t) : lane;
+        const bool rt = __shfl((int)r, src, 64) != 0;
+        if (t >= 0 && t < RM::T) rej = rt;
+    }
+    int cnt2;
+    const uint32_t cid2 = compact(cid, lane < cnt && !rej, cnt2);
+    if (cnt2 > 0) eval_list<C, G>(g, q, qn, cid2, cnt2, metric, sink);
+    return cnt2;
+}
+
+
 struct WaveStats {
     unsigned long long E = 0, X = 0, resets = 0;
+    unsigned long long S = 0, F = 0;  // screened rows (fp16) / rows evaluated in f32
 };
 
 // How the sequential (compat) walks evaluate distances and order their own
@@ -106,7 +164,7 @@ struct WaveEval {
 // ---------------------------------------------------------------------------
 // beam: sorted list of <= ef entries; stop when every entry is expanded
 // ---------------------------------------------------------------------------
-template <class C, int R, int G, bool COH = false>
+template <class C, int R, int G, bool COH = false, bool SCREEN = false>
 __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_t entry, int ef, const QReg<C>& q, float qn,
                            BList<R>& L, uint32_t* vis, int vlog2, WaveStats& st) {
     const int lane = lane_id();
@@ -119,6 +177,8 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
     int vcount = 1;
     eval_list<C, G>(g, q, qn, entry, 1, g.metric, [&](float d, uint32_t u) { bl_insert(L, ef, d, u); });
     st.E += 1;
+    st.F += 1;
+    const bool screen = SCREEN && h16_query_ok(qn);
     const int32_t* degp = g.layers[layer].deg;
     const int32_t* adjp = g.layers[layer].adj;
     const int capl = g.layers[layer].cap;
@@ -141,7 +201,19 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
         const uint32_t cid = compact(nb, pr != 0, cnt);
         if (cnt == 0) continue;
         st.E += cnt;
-        eval_list<C, G>(g, q, qn, cid, cnt, g.metric, [&](float d, uint32_t u) { bl_insert(L, ef, d, u); });
+        auto sink = [&](float d, uint32_t u) { bl_insert(L, ef, d, u); };
+        float wd = __int_as_float(0x7f800000);
+        if constexpr (SCREEN) {
+            uint32_t wi;
+            bl_at(L, ef - 1, wd, wi);
+        }
+        if (SCREEN && screen && wd < __int_as_float(0x7f800000)) {
+            st.S += cnt;
+            st.F += eval_screened<C, G>(g, q, qn, cid, cnt, g.metric, wd, sink);
+        } else {
+            st.F += cnt;
+            eval_list<C, G>(g, q, qn, cid, cnt, g.metric, sink);
+        }
         if (vcount > (vsize >> 1) + (vsize >> 2)) {  // forget: results unchanged
             __syncthreads();
             vis_clear(vis, vsize);

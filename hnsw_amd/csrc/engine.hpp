@@ -40,6 +40,7 @@ struct SearchArgs {
     int32_t* out_n;               // [B]
     int32_t* out_ids;             // [B*k] internal ids (nullable)
     unsigned long long* stats;    // [0]=dist evals [1]=expansions [2]=visited resets
+                                  // [8]=rows screened in fp16 [9]=rows evaluated in f32 (beam)
     int* err;                     // set to nonzero on visited overflow (compat)
     int vis_log2;
     int upper_ef;                 // beam: width of the upper-layer descent (1 = greedy, the reference's k = 1)
@@ -65,6 +66,7 @@ constexpr int NEG_MAX_CAND = 256;
 int launch_negatives(const NegArgs& a, int lpr, int vpl, hipStream_t s);
 
 int launch_pad_rows(const float* src, int64_t n, int dim, float* dst, int pitch, hipStream_t s);
+int launch_h16_rows(const float* X, int64_t n0, int64_t n1, int pitch, uint16_t* H, float* inv, hipStream_t s);
 int launch_norms(const float* X, int64_t n0, int64_t n1, int pitch, int lpr, int vpl, float* out, hipStream_t s);
 int launch_sweep(const float* q, const float* X, int64_t n, int pitch, int lpr, int vpl, int metric, float* out,
                  hipStream_t s);

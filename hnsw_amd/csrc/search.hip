@@ -167,9 +167,54 @@ static int launch_sweep_t(const float* q, const float* X, int64_t n, int pitch, 
 }
 
 // ---------------------------------------------------------------------------
+// fp16 screening copy of rows [n0, n1): one wave per row.  The row is scaled by
+// 2^e so that max|x_i| * 2^e lies in [2^14, 2^15) (exact: a power of two) and
+// rounded to nearest fp16; inv[r] = 2^-e.  Rows outside the screen's validity
+// range (max|x_i| not in [2^-50, 2^50], or any non-finite value) get inv = NaN,
+// which makes every screening test on them false.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_h16_rows(const float* __restrict__ X, int64_t n0, int64_t n1, int pitch,
+                                                  uint16_t* __restrict__ H, float* __restrict__ inv) {
+    const int lane = lane_id();
+    const int64_t r = n0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n1) return;
+    const float* xp = X + (size_t)r * pitch;
+    float m = 0.f;
+    bool fin = true;
+    for (int e = lane * 4; e < pitch; e += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(xp + e);
+        fin = fin && isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    fin = __ballot(!fin) == 0ull;
+    const bool ok = fin && m >= 8.881784197001252e-16f && m <= 1.125899906842624e15f;  // [2^-50, 2^50]
+    int k = 0;
+    if (ok) (void)frexpf(m, &k);  // m = f * 2^k, f in [0.5, 1)
+    const int ex = 15 - k;        // m * 2^ex in [2^14, 2^15)
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    for (int e = lane * 4; e < pitch; e += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(xp + e);
+        h4 o = h4{0, 0, 0, 0};
+        if (ok) o = h4{(_Float16)ldexpf(v.x, ex), (_Float16)ldexpf(v.y, ex), (_Float16)ldexpf(v.z, ex),
+                       (_Float16)ldexpf(v.w, ex)};
+        *reinterpret_cast<h4*>(H + (size_t)r * pitch + e) = o;
+    }
+    if (lane == 0) inv[r] = ok ? ldexpf(1.f, -ex) : __int_as_float(0x7fc00000);
+}
+
+int launch_h16_rows(const float* X, int64_t n0, int64_t n1, int pitch, uint16_t* H, float* inv, hipStream_t s) {
+    const int64_t rows = n1 - n0;
+    if (rows <= 0) return 0;
+    hipLaunchKernelGGL(k_h16_rows, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, X, n0, n1, pitch, H, inv);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------
 // batched search: one wave per query
 // ---------------------------------------------------------------------------
-template <class C, int R, int G>
+template <class C, int R, int G, bool SCREEN>
 __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int64_t b = blockIdx.x;
@@ -188,7 +233,7 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
                 if (e < 0) continue;
                 ep = (uint32_t)e;
             }
-            beam_layer<C, 1, G>(a.g, l, ep, a.upper_ef, q, qn, L1, smem, a.vis_log2, st);
+            beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, a.upper_ef, q, qn, L1, smem, a.vis_log2, st);
             float d;
             uint32_t id;
             bl_at(L1, 0, d, id);
@@ -198,7 +243,7 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
     BList<R> L;
     const int efl = a.ef > a.k ? a.ef : a.k;
     if (a.g.layers[0].deg[ep] == -2) ep = (uint32_t)a.layer_entry[0];
-    beam_layer<C, R, G>(a.g, 0, ep, efl, q, qn, L, smem, a.vis_log2, st);
+    beam_layer<C, R, G, false, SCREEN>(a.g, 0, ep, efl, q, qn, L, smem, a.vis_log2, st);
     // compact the sorted list into the first k live entries (deleted rows
     // route the search but are never returned)
     int nvalid = 0;
@@ -227,6 +272,8 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
         atomicAdd(&a.stats[0], st.E);
         atomicAdd(&a.stats[1], st.X);
         if (st.resets) atomicAdd(&a.stats[2], st.resets);
+        atomicAdd(&a.stats[8], st.S);
+        atomicAdd(&a.stats[9], st.F);
     }
 }
 
@@ -363,7 +410,10 @@ __global__ __launch_bounds__(64) void k_negatives(NegArgs a) {
 template <class C, int R, int G>
 static int launch_beam_t(const SearchArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 << a.vis_log2;
-    hipLaunchKernelGGL((k_search_beam<C, R, G>), dim3((unsigned)a.B), dim3(64), lds, s, a);
+    if (a.g.h16)
+        hipLaunchKernelGGL((k_search_beam<C, R, G, true>), dim3((unsigned)a.B), dim3(64), lds, s, a);
+    else
+        hipLaunchKernelGGL((k_search_beam<C, R, G, false>), dim3((unsigned)a.B), dim3(64), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -475,10 +475,11 @@ class Graph:
         return out
 
     def stats(self) -> dict:
-        o = np.zeros(8, np.int64)
-        self._check(load().mhnsw_stats(self._h, _ptr(o, C.c_int64), 8))
+        o = np.zeros(10, np.int64)
+        self._check(load().mhnsw_stats(self._h, _ptr(o, C.c_int64), 10))
         names = ["search_dist_evals", "search_expansions", "visited_resets", "build_dist_evals",
-                 "build_expansions", "dropped_proposals", "searches", "exact_uncertified"]
+                 "build_expansions", "dropped_proposals", "searches", "exact_uncertified",
+                 "search_screened", "search_f32_evals"]
         return dict(zip(names, o.tolist()))
 
     def reset_stats(self):

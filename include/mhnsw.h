@@ -77,7 +77,9 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * both preselect, re-rank canonically and certify, so results are identical),
  * "exact_tile", "compat_waves" (1 or 8 waves scoring the compat insert's
  * distance batches), "upper_ef" (beam mode: upper-layer descent width, 1 =
- * greedy); read-only: "pitch", "capacity", "strkeys", "strkey_relabels" */
+ * greedy), "screen" (beam mode, default 1: keep an fp16 copy of the rows and
+ * skip candidates it proves the f32 distance rejects; results unchanged);
+ * read-only: "pitch", "capacity", "strkeys", "strkey_relabels" */
 int mhnsw_set_option(mhnsw_index *h, const char *name, int64_t value);
 int mhnsw_get_option(const mhnsw_index *h, const char *name, int64_t *value);
 /* Graph.Validate (graph.go:916-937) */
@@ -169,7 +171,8 @@ int mhnsw_preview_levels(mhnsw_index *h, int64_t n, int32_t *out);
 /* counters: [0] search distance evals, [1] search expansions, [2] visited-set
  * resets, [3] build distance evals, [4] build expansions, [5] dropped reverse
  * proposals, [6] searches issued, [7] exact-mode queries whose preselection
- * could not be certified and were redone by a full canonical sweep */
+ * could not be certified and were redone by a full canonical sweep, [8] beam
+ * candidates screened on the fp16 copy, [9] beam candidates evaluated in f32 */
 int mhnsw_stats(const mhnsw_index *h, int64_t *out, int n);
 int mhnsw_reset_stats(mhnsw_index *h);
 /* device time of the last search's main kernel (HIP events on its stream) */

@@ -1,0 +1,88 @@
+"""GPU: the fp16 screening copy (option "screen") never changes
+a beam search.  Every result (keys, f32 distance bits, counts) with the screen
+on must equal the screen-off search and the oracle's beam search, on data built
+to sit at the screen's edges: exact distance ties (integer-valued rows),
+duplicates, rows and queries outside the screen's validity range (huge, tiny,
+zero), and queries equal to stored rows."""
+import numpy as np
+import pytest
+
+from tests.test_gpu_parity import _clustered, _metric_fn, _same_results
+
+pytestmark = pytest.mark.gpu
+
+
+def _adversarial(rng, n, d, metric):
+    X = _clustered(rng, n, d)
+    X[1] = X[2]                                   # duplicates
+    X[3] = X[2]
+    X[4] = np.nextafter(X[2], np.float32(np.inf))  # 1-ulp neighbour of a duplicate
+    X[10] *= np.float32(1e20)                     # outside [2^-50, 2^50]: never screened
+    X[11] *= np.float32(1e-20)
+    X[12] *= np.float32(2.0 ** 49)                # inside the range, near its edges
+    X[13] *= np.float32(2.0 ** -49)
+    X[20:40] = rng.integers(-1, 2, size=(20, d)).astype(np.float32)  # many exact ties
+    if metric == 0:
+        X[14] = 0.0                               # zero row: NaN cosine
+    Q = _clustered(rng, 96, d)
+    Q[0] = X[2]
+    Q[1] = X[25]
+    Q[2] = 0.0
+    Q[3] *= np.float32(1e30)                      # |q| > 2^40: query not screened
+    Q[4] *= np.float32(1e-30)
+    Q[5:9] = rng.integers(-1, 2, size=(4, d)).astype(np.float32)
+    return X, Q
+
+
+def _search(g, Q, ef, H):
+    return g.search_arrays(Q, 10, mode=H.MODE_BEAM, ef=ef)
+
+
+@pytest.mark.parametrize("metric,d,n", [(0, 64, 20000), (1, 64, 20000), (0, 768, 6000), (1, 200, 8000)])
+def test_screen_identical_to_f32(H, O, metric, d, n):
+    rng = np.random.default_rng(100 + metric + d)
+    X, Q = _adversarial(rng, n, d, metric)
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=_metric_fn(H, metric), Rng=5, build_mode=H.BUILD_BATCH,
+                ef_construction=100, heuristic=2, keep_pruned=1)
+    g.add_arrays(np.arange(n), X)
+    assert g.get_option("screen") == 1
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=16, M0=32, Ml=0.25, EfSearch=64)
+    o.import_graph(**g.export())
+    for ef in (10, 64, 200):
+        g.set_option("screen", 1)
+        g.reset_stats()
+        on = _search(g, Q, ef, H)
+        st = g.stats()
+        assert st["search_screened"] > 0
+        assert st["search_f32_evals"] < st["search_dist_evals"]
+        g.set_option("screen", 0)
+        g.reset_stats()
+        off = _search(g, Q, ef, H)
+        st = g.stats()
+        assert st["search_screened"] == 0 and st["search_f32_evals"] == st["search_dist_evals"]
+        _same_results(*on, *off)
+        _same_results(*on, *o.search(Q, 10, mode=O.MODE_BEAM, ef=ef))
+    g.close()
+
+
+def test_screen_follows_adds_and_import(H, O):
+    rng = np.random.default_rng(7)
+    n, d = 6000, 96
+    X, Q = _adversarial(rng, n, d, 0)
+    g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=H.CosineDistance, Rng=3, build_mode=H.BUILD_BATCH,
+                ef_construction=64, heuristic=2)
+    g.set_option("screen", 0)
+    g.add_arrays(np.arange(n // 2), X[: n // 2])
+    g.set_option("screen", 1)                     # enabling converts the rows already held
+    g.add_arrays(np.arange(n // 2, n), X[n // 2:])  # later adds convert their own rows
+    on = _search(g, Q, 48, H)
+    g.set_option("screen", 0)
+    _same_results(*on, *_search(g, Q, 48, H))
+    # a graph rebuilt by Import screens the imported rows
+    g2 = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=H.CosineDistance, Rng=3, build_mode=H.BUILD_BATCH)
+    g2.import_graph(**g.export())
+    g2.reset_stats()
+    _same_results(*on, *_search(g2, Q, 48, H))
+    assert g2.stats()["search_screened"] > 0
+    g.close()
+    g2.close()

@@ -119,7 +119,12 @@ def test_thread_safety(H):
     assert set(add_errors) <= {"no nodes found in neighborhood search"}, set(add_errors)
     assert len(added) + len(add_errors) == num_ops // 5
     g.Validate()
-    assert len(g.Search(rng.random(dims).astype(np.float32), 3)) == 3
+    # graph_test.go:522-523 only requires the final Search not to fail: the
+    # compat walk (the reference's semantics) may come back short after some
+    # interleavings of deletes; the exact path must find 3
+    q = rng.random(dims).astype(np.float32)
+    assert len(g.Search(q, 3)) <= 3
+    assert len(g.Search(q, 3, mode=H.MODE_EXACT)) == 3
     live = num_nodes + len(added) - len(set(deleted))
     assert live <= g.Len() <= live + len(add_errors)  # a failed Add may leave its node (Q18)
     g.close()
