@@ -238,13 +238,14 @@ def main():
     cap0 = a.M0 + 1
 
     def alg_bytes_of(stats, launches):
-        # f32 row + norm per f32 evaluation, fp16 row + norm + unscale per
-        # screened candidate, one adjacency row per expansion, the query
+        # f32 row + norm per f32 evaluation, fp16 row per screened candidate,
+        # one adjacency row per expansion, the query
         E = stats["search_dist_evals"] / launches
         Sc = stats["search_screened"] / launches
         F = stats["search_f32_evals"] / launches
         Xp = stats["search_expansions"] / launches
-        return F * (4 * a.dim + 4) + Sc * (2 * a.dim + 8) + Xp * 4 * cap0 + a.batch * 4 * a.dim, E, Xp, Sc, F
+        aux = 8 if a.metric == "euclidean" else 0  # L2 screening reads {unscale, |x|} per row
+        return F * (4 * a.dim + 4) + Sc * (2 * a.dim + aux) + Xp * 4 * cap0 + a.batch * 4 * a.dim, E, Xp, Sc, F
 
     alg_bytes, E, Xp, Sc, F = alg_bytes_of(st, a.steps)
     kms = float(np.mean(kernel_ms))

@@ -78,7 +78,8 @@ struct mhnsw_index {
     float* vecs = nullptr;
     float* norms = nullptr;
     uint16_t* h16 = nullptr;  // fp16 screening copy [capn * pitch] (screen = 1)
-    float* h16inv = nullptr;  // [capn] per-row unscale (NaN: never screened)
+    float2* h16aux = nullptr;  // [capn] L2 screening {unscale, |x|}
+    int h16_metric = -1;       // metric the copy was written for
     int64_t* keys = nullptr;
     int32_t* levels = nullptr;
     uint8_t* dead = nullptr;  // [capn] deleted rows (graph.go:843-864)
@@ -293,7 +294,7 @@ int ensure_capacity(mhnsw_index* h, int64_t need) {
     if ((r = grow(h, h->norms, oc, nc, 0))) return r;
     if (h->screen) {
         if ((r = grow(h, h->h16, oc * h->pitch, nc * h->pitch, 0))) return r;
-        if ((r = grow(h, h->h16inv, oc, nc, 0xFF))) return r;
+        if ((r = grow(h, h->h16aux, oc, nc, 0xFF))) return r;
     }
     if ((r = grow(h, h->keys, oc, nc, 0))) return r;
     if ((r = grow(h, h->levels, oc, nc, 0))) return r;
@@ -345,7 +346,8 @@ GraphDev graph_view(const mhnsw_index* h) {
     g.err = h->d_err;
     g.dead = h->any_dead ? h->dead : nullptr;
     g.h16 = h->screen ? h->h16 : nullptr;
-    g.h16inv = h->screen ? h->h16inv : nullptr;
+    g.h16aux = h->h16aux;
+    if (h->h16_metric != h->metric) g.h16 = nullptr;  // stale format: no screening
     return g;
 }
 
@@ -523,6 +525,15 @@ int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1, int top, uint32_t en
     return 0;
 }
 
+// (re)write the fp16 screening copy of rows [r0, r1) for the current metric
+int h16_rows(mhnsw_index* h, int64_t r0, int64_t r1) {
+    if (!h->screen || !h->h16) return 0;
+    if (h->h16_metric != h->metric && r0 > 0) r0 = 0;  // format change: every row
+    LCHK(h, launch_h16_rows(h->vecs, h->norms, r0, r1, h->pitch, h->metric, h->h16, h->h16aux, h->stream));
+    h->h16_metric = h->metric;
+    return 0;
+}
+
 int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_on_device, int64_t n, int dim,
              const int32_t* levels) {
     int r = validate(h);
@@ -585,7 +596,7 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     }
     LCHK(h, launch_pad_rows(src, n, dim, h->vecs + (size_t)n0 * h->pitch, h->pitch, h->stream));
     LCHK(h, launch_norms(h->vecs, n0, n1, h->pitch, h->lpr, h->vpl, h->norms, h->stream));
-    if (h->screen) LCHK(h, launch_h16_rows(h->vecs, n0, n1, h->pitch, h->h16, h->h16inv, h->stream));
+    if ((r = h16_rows(h, n0, n1))) return r;
     // host bookkeeping: layer membership, counts, entries
     const bool compat = h->build_mode == MHNSW_BUILD_COMPAT;
     h->hmask.resize(n1, 0u);
@@ -916,7 +927,7 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->vecs);
     F(h->norms);
     F(h->h16);
-    F(h->h16inv);
+    F(h->h16aux);
     F(h->keys);
     F(h->levels);
     F(h->dead);
@@ -974,6 +985,13 @@ const char* mhnsw_last_error(const mhnsw_index* h) { return h ? h->err.c_str() :
 
 int mhnsw_set_params(mhnsw_index* h, int metric, int M, double ml, int ef_search) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
+    if (metric != h->metric && h->screen && h->n > 0) {  // the screening copy's format follows the metric
+        int r = drain(h);
+        if (r) return r;
+        h->metric = metric;
+        if ((r = h16_rows(h, 0, h->n))) return r;
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
     h->metric = metric;
     h->M = M;
     h->ml = ml;
@@ -1038,17 +1056,18 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
         int r = drain(h);
         if (r) return r;
         HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->screen = (int)v;
         if (!v) {
             (void)hipFree(h->h16);
-            (void)hipFree(h->h16inv);
+            (void)hipFree(h->h16aux);
             h->h16 = nullptr;
-            h->h16inv = nullptr;
+            h->h16aux = nullptr;
+            h->h16_metric = -1;
         } else if (h->capn > 0) {
-            if ((r = grow(h, h->h16, 0, h->capn * h->pitch, 0)) || (r = grow(h, h->h16inv, 0, h->capn, 0xFF))) return r;
-            LCHK(h, launch_h16_rows(h->vecs, 0, h->n, h->pitch, h->h16, h->h16inv, h->stream));
+            if ((r = grow(h, h->h16, 0, h->capn * h->pitch, 0)) || (r = grow(h, h->h16aux, 0, h->capn, 0xFF))) return r;
+            if ((r = h16_rows(h, 0, h->n))) return r;
             HIPCHK(h, hipStreamSynchronize(h->stream));
         }
-        h->screen = (int)v;
     } else if (n == "compat_waves") {
         if (v != 1 && v != 8) return fail(h, MHNSW_EINVAL, "compat_waves must be 1 or 8");
         h->compat_waves = (int)v;
@@ -1232,7 +1251,7 @@ void reset_graph(mhnsw_index* h) {
     F(h->vecs);
     F(h->norms);
     F(h->h16);
-    F(h->h16inv);
+    F(h->h16aux);
     F(h->keys);
     F(h->levels);
     F(h->dead);
@@ -1285,7 +1304,7 @@ int import_csr(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t
     HIPCHK(h, hipMemcpy(h->tmp.p, vecs, (size_t)N * dim * 4, hipMemcpyHostToDevice));
     LCHK(h, launch_pad_rows(h->tmp.p, N, dim, h->vecs, h->pitch, h->stream));
     LCHK(h, launch_norms(h->vecs, 0, N, h->pitch, h->lpr, h->vpl, h->norms, h->stream));
-    if (h->screen) LCHK(h, launch_h16_rows(h->vecs, 0, N, h->pitch, h->h16, h->h16inv, h->stream));
+    if ((r = h16_rows(h, 0, N))) return r;
     h->xsplit_rows = 0;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     std::vector<int32_t> row;

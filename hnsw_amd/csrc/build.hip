@@ -459,7 +459,7 @@ static int launch_build_compat_t(const CompatBuildArgs& a, int waves, hipStream_
 // ---------------------------------------------------------------------------
 // batched build
 // ---------------------------------------------------------------------------
-template <class C, int R, int G>
+template <class C, int R, int G, bool SCREEN>
 __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int64_t u64 = a.n0 + blockIdx.x;
@@ -474,14 +474,14 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
     const uint32_t ep = a.cur_entry[u];
     if (a.levels[u] < l) {  // above the node's level: greedy descent only
         BList<1> L1;
-        beam_layer<C, 1, G>(a.g, l, ep, 1, q, qn, L1, smem, a.vis_log2, st);
+        beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, 1, q, qn, L1, smem, a.vis_log2, st);
         float d;
         uint32_t id;
         bl_at(L1, 0, d, id);
         if (lane == 0 && id != EMPTY_ID) a.cur_entry[u] = id & ID_MASK;
     } else {
         BList<R> L;
-        beam_layer<C, R, G>(a.g, l, ep, a.ef, q, qn, L, smem, a.vis_log2, st);
+        beam_layer<C, R, G, false, SCREEN>(a.g, l, ep, a.ef, q, qn, L, smem, a.vis_log2, st);
         float d0;
         uint32_t i0;
         bl_at(L, 0, d0, i0);
@@ -839,7 +839,10 @@ static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 << a.vis_log2;
     const int64_t n = a.n1 - a.n0;
     if (n <= 0) return 0;
-    hipLaunchKernelGGL((k_batch_search<C, R, G>), dim3((unsigned)n), dim3(64), lds, s, a);
+    if (a.g.h16)  // fp16 screening: same graph, fewer bytes per candidate
+        hipLaunchKernelGGL((k_batch_search<C, R, G, true>), dim3((unsigned)n), dim3(64), lds, s, a);
+    else
+        hipLaunchKernelGGL((k_batch_search<C, R, G, false>), dim3((unsigned)n), dim3(64), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -50,12 +50,14 @@ struct GraphDev {
     uint32_t capn;  // rows allocated: every gathered id is checked against it
     int* err;       // bit 4: out-of-range id seen (load clamped, no fault)
     const uint8_t* dead;  // [cap_nodes] 1 = deleted (nullptr until the first Delete)
-    // fp16 screening copy (nullptr = off): row r scaled by a power of two into
-    // [2^14, 2^15) and rounded to fp16; h16inv[r] undoes the scale (NaN marks a
-    // row the screen must never reject).  Only ever used to skip candidates
-    // that the f32 distance provably rejects.
+    // fp16 screening copy (nullptr = off), only ever used to skip candidates
+    // whose f32 distance provably exceeds the list's worst.
+    //   cosine: row r is fp16(x / |x| * 2^14) (no per-row value needed);
+    //           NaN halves mark a row the screen must never reject
+    //   L2:     row r is fp16(x * 2^e) with max|x_i| 2^e in [2^14, 2^15);
+    //           h16aux[r] = {2^-e, |x|}, NaN 2^-e marks a never-rejected row
     const uint16_t* h16;      // [cap_nodes * pitch]
-    const float* h16inv;      // [cap_nodes]
+    const float2* h16aux;     // [cap_nodes] (L2)
 };
 
 __device__ __forceinline__ bool is_dead(const GraphDev& g, uint32_t id) { return g.dead && g.dead[id]; }
@@ -250,8 +252,8 @@ __device__ __forceinline__ float eval_rows(const QReg<C>& q, const float* __rest
 }
 
 // Approximate sums from the fp16 screening copy, same lane/row mapping as
-// eval_rows.  Dot: sum q_i * h_i (the caller applies the row's h16inv).
-// L2: sum (q_i - h_i * inv_g)^2 with inv[g] the row's h16inv.
+// eval_rows.  Dot: sum q_i * h_i.  L2: sum (q_i - h_i * inv_g)^2 with inv[g]
+// the row's unscale.
 template <class C, int G, bool L2>
 __device__ __forceinline__ float eval_rows_h16(const QReg<C>& q, const uint16_t* __restrict__ H, int pitch,
                                                const uint32_t (&ids)[G], const bool (&valid)[G],
@@ -296,15 +298,17 @@ __device__ __forceinline__ float eval_rows_h16(const QReg<C>& q, const uint16_t*
     return reduce_rows<G, C::LPR>(p);
 }
 
-// Screening bounds.  With x' the fp16 copy of row x
-// (|x' - x| <= 2^-11 |x| componentwise, plus a subnormal term far below 2^-30 |x|):
-//   cosine: |approx - f32| <= 2^-11 (Cauchy-Schwarz on sum q_i (x'_i - x_i))
-//           + accumulation / finalize rounding (< 2^-17 for dim <= 4096)
+// Screening bounds, with y the row the fp16 copy stands for
+// (x / |x|_f32 for cosine, x for L2) and |y' - y| <= 2^-11 |y| (+ 2u from the
+// cosine normalisation, + a subnormal term far below 2^-30 |y|):
+//   cosine: |S / |q|_f32 - (the f32 cosine term)| <= 2^-11 + 2 gamma + 8u
+//           (Cauchy-Schwarz; gamma = accumulation bound of one f32 dot,
+//           < 2^-18 for dim <= 4096), so approx > wd + 2^-11 + 2^-16 => f32 > wd
 //   L2:     | |q - x'| - |q - x| | <= |x' - x| <= 2^-11 |x|  (triangle inequality)
 //           + relative rounding of both computed distances (< 2^-16)
 // Valid while no intermediate over/underflows: rows are screened only when
-// 2^-50 <= max|x_i| <= 2^50 (else h16inv = NaN) and queries when
-// 2^-40 <= |q| <= 2^40.
+// 2^-50 <= max|x_i| <= 2^50 and queries when 2^-40 <= |q| <= 2^40.
+constexpr float H16_COS_SCALE = 6.103515625e-05f;                      // 2^-14
 constexpr float H16_DELTA_COS = 0.00048828125f + 0.0000152587890625f;  // 2^-11 + 2^-16
 constexpr float H16_REL_L2 = 1.0f - 0.000030517578125f;                // 1 - 2^-15
 constexpr float H16_ABS_L2 = 0.00048828125f * 1.000030517578125f;      // 2^-11 (1 + 2^-15)
@@ -312,12 +316,12 @@ constexpr float H16_MIN_L2 = 8.881784197001252e-16f;                   // 2^-50
 __device__ __forceinline__ bool h16_query_ok(float qn) {
     return qn >= 9.094947017729282e-13f && qn <= 1.099511627776e12f;  // [2^-40, 2^40]; false for NaN
 }
-// true when the f32 distance of this row is certainly > wd
-__device__ __forceinline__ bool h16_rejects(int metric, float s, float inv, float xn, float qn, float wd) {
-    if (metric == COSINE) {
-        const float da = 1.0f - (s * inv) / (xn * qn);
-        return da > wd + H16_DELTA_COS;
-    }
+// true when the f32 distance of this row is certainly > wd (s: eval_rows_h16 sum)
+__device__ __forceinline__ bool h16_rejects_cos(float s, float qn, float wd) {
+    const float da = 1.0f - (s * H16_COS_SCALE) / qn;
+    return da > wd + H16_DELTA_COS;
+}
+__device__ __forceinline__ bool h16_rejects_l2(float s, float xn, float wd) {
     const float da = sqrtf(s);
     return da >= H16_MIN_L2 && da * H16_REL_L2 - H16_ABS_L2 * xn > wd;
 }

@@ -101,22 +101,28 @@ __device__ __forceinline__ int eval_screened(const GraphDev& g, const QReg<C>& q
                 ids[gg] = shfl_u(cid, t & 63);
             ids[gg] = valid[gg] ? guard_id(g, ids[gg]) : 0u;
         }
-        float s;
+        const int town = base + RM::owned_row(lane);
+        bool r = false;
         if (metric == EUCLIDEAN) {
+            float xn[GH];
 #pragma unroll
-            for (int gg = 0; gg < GH; ++gg) inv[gg] = g.h16inv[ids[gg]];
-            s = eval_rows_h16<C, GH, true>(q, g.h16, g.pitch, ids, valid, inv);
+            for (int gg = 0; gg < GH; ++gg) {
+                const float2 ax = g.h16aux[ids[gg]];
+                inv[gg] = ax.x;
+                xn[gg] = ax.y;
+            }
+            const float s = eval_rows_h16<C, GH, true>(q, g.h16, g.pitch, ids, valid, inv);
+            // the owner of row town computed it in register (town - base) / RPI
+            float xo = xn[0];
+#pragma unroll
+            for (int gg = 1; gg < GH; ++gg)
+                if (RM::reg_row(gg, lane) == town - base) xo = xn[gg];
+            if (town < cnt) r = h16_rejects_l2(s, xo, wd);
         } else {
 #pragma unroll
             for (int gg = 0; gg < GH; ++gg) inv[gg] = 1.f;
-            s = eval_rows_h16<C, GH, false>(q, g.h16, g.pitch, ids, valid, inv);
-        }
-        const int town = base + RM::owned_row(lane);
-        const uint32_t idown = shfl_u(cid, town & 63);  // all lanes: a permute reads inactive lanes as 0
-        bool r = false;
-        if (town < cnt) {
-            const uint32_t id = guard_id(g, idown);
-            r = h16_rejects(metric, s, g.h16inv[id], g.norms[id], qn, wd);
+            const float s = eval_rows_h16<C, GH, false>(q, g.h16, g.pitch, ids, valid, inv);
+            if (town < cnt) r = h16_rejects_cos(s, qn, wd);
         }
         // hand row t's verdict from its owner lane to lane t
         const int t = lane - base;

@@ -167,14 +167,18 @@ static int launch_sweep_t(const float* q, const float* X, int64_t n, int pitch, 
 }
 
 // ---------------------------------------------------------------------------
-// fp16 screening copy of rows [n0, n1): one wave per row.  The row is scaled by
-// 2^e so that max|x_i| * 2^e lies in [2^14, 2^15) (exact: a power of two) and
-// rounded to nearest fp16; inv[r] = 2^-e.  Rows outside the screen's validity
-// range (max|x_i| not in [2^-50, 2^50], or any non-finite value) get inv = NaN,
-// which makes every screening test on them false.
+// fp16 screening copy of rows [n0, n1) (device_common.hpp GraphDev::h16), one
+// wave per row; norms[r] (canonical |x|) must already be written.
+//   cosine: fp16(x_i * (1/|x|) * 2^14); rows outside the screen's validity
+//           range (max|x_i| not in [2^-50, 2^50], any non-finite value) get
+//           NaN halves, which make every screening test on them false
+//   L2:     fp16(x_i * 2^e), max|x_i| 2^e in [2^14, 2^15) (exact power of two);
+//           aux[r] = {2^-e, |x|}, 2^-e = NaN outside the validity range
+// Rounding is to nearest; the bounds are in device_common.hpp (H16_*).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_h16_rows(const float* __restrict__ X, int64_t n0, int64_t n1, int pitch,
-                                                  uint16_t* __restrict__ H, float* __restrict__ inv) {
+__global__ __launch_bounds__(256) void k_h16_rows(const float* __restrict__ X, const float* __restrict__ norms,
+                                                  int64_t n0, int64_t n1, int pitch, int metric,
+                                                  uint16_t* __restrict__ H, float2* __restrict__ aux) {
     const int lane = lane_id();
     const int64_t r = n0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n1) return;
@@ -189,25 +193,36 @@ __global__ __launch_bounds__(256) void k_h16_rows(const float* __restrict__ X, i
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
     fin = __ballot(!fin) == 0ull;
-    const bool ok = fin && m >= 8.881784197001252e-16f && m <= 1.125899906842624e15f;  // [2^-50, 2^50]
+    const float xn = norms[r];
+    const bool ok = fin && m >= 8.881784197001252e-16f && m <= 1.125899906842624e15f &&  // [2^-50, 2^50]
+                    xn > 0.f && isfinite(xn);
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const _Float16 hnan = __builtin_bit_cast(_Float16, (uint16_t)0x7E00);
     int k = 0;
     if (ok) (void)frexpf(m, &k);  // m = f * 2^k, f in [0.5, 1)
     const int ex = 15 - k;        // m * 2^ex in [2^14, 2^15)
-    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const float rx = ok ? 16384.0f / xn : 0.f;
     for (int e = lane * 4; e < pitch; e += 256) {
         const float4 v = *reinterpret_cast<const float4*>(xp + e);
-        h4 o = h4{0, 0, 0, 0};
-        if (ok) o = h4{(_Float16)ldexpf(v.x, ex), (_Float16)ldexpf(v.y, ex), (_Float16)ldexpf(v.z, ex),
-                       (_Float16)ldexpf(v.w, ex)};
+        h4 o;
+        if (!ok)
+            o = metric == COSINE ? h4{hnan, hnan, hnan, hnan} : h4{0, 0, 0, 0};
+        else if (metric == COSINE)
+            o = h4{(_Float16)(v.x * rx), (_Float16)(v.y * rx), (_Float16)(v.z * rx), (_Float16)(v.w * rx)};
+        else
+            o = h4{(_Float16)ldexpf(v.x, ex), (_Float16)ldexpf(v.y, ex), (_Float16)ldexpf(v.z, ex),
+                   (_Float16)ldexpf(v.w, ex)};
         *reinterpret_cast<h4*>(H + (size_t)r * pitch + e) = o;
     }
-    if (lane == 0) inv[r] = ok ? ldexpf(1.f, -ex) : __int_as_float(0x7fc00000);
+    if (lane == 0) aux[r] = make_float2(ok ? ldexpf(1.f, -ex) : __int_as_float(0x7fc00000), xn);
 }
 
-int launch_h16_rows(const float* X, int64_t n0, int64_t n1, int pitch, uint16_t* H, float* inv, hipStream_t s) {
+int launch_h16_rows(const float* X, const float* norms, int64_t n0, int64_t n1, int pitch, int metric, uint16_t* H,
+                    float2* aux, hipStream_t s) {
     const int64_t rows = n1 - n0;
     if (rows <= 0) return 0;
-    hipLaunchKernelGGL(k_h16_rows, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, X, n0, n1, pitch, H, inv);
+    hipLaunchKernelGGL(k_h16_rows, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, X, norms, n0, n1, pitch, metric,
+                       H, aux);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -86,3 +86,44 @@ def test_screen_follows_adds_and_import(H, O):
     assert g2.stats()["search_screened"] > 0
     g.close()
     g2.close()
+
+
+def test_screen_follows_metric_change(H, O):
+    """Distance is a public field (graph.go:309): switching it rewrites the
+    screening copy in the new metric's format."""
+    rng = np.random.default_rng(8)
+    n, d = 5000, 128
+    X, Q = _adversarial(rng, n, d, 1)
+    g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=H.CosineDistance, Rng=3, build_mode=H.BUILD_BATCH,
+                ef_construction=64, heuristic=2)
+    g.add_arrays(np.arange(n), X)
+    for dist, metric in ((H.EuclideanDistance, 1), (H.CosineDistance, 0)):
+        g.Distance = dist
+        g.reset_stats()
+        on = _search(g, Q, 48, H)
+        assert g.stats()["search_screened"] > 0
+        o = O.Graph(metric=metric, order=O.ORDER_DEV, M=12, M0=24, Ml=0.3, EfSearch=48)
+        o.import_graph(**g.export())
+        _same_results(*on, *o.search(Q, 10, mode=O.MODE_BEAM, ef=48))
+        g.set_option("screen", 0)
+        _same_results(*on, *_search(g, Q, 48, H))
+        g.set_option("screen", 1)
+    g.close()
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_screened_batch_build_identical(H, metric):
+    """The batched insert's searches screen too: the graph is the same."""
+    rng = np.random.default_rng(21 + metric)
+    n, d = 12000, 96
+    X, _ = _adversarial(rng, n, d, metric)
+    ex = []
+    for screen in (0, 1):
+        g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
+                    ef_construction=80, heuristic=2, keep_pruned=1, screen=screen)
+        g.add_arrays(np.arange(n), X)
+        assert g.stats()["dropped_proposals"] == 0
+        ex.append(g.export())
+        g.close()
+    from tests.test_gpu_parity import _same_graph
+    _same_graph(ex[0], ex[1])
