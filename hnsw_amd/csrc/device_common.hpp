@@ -51,7 +51,7 @@ struct GraphDev {
     int* err;       // bit 4: out-of-range id seen (load clamped, no fault)
     const uint8_t* dead;  // [cap_nodes] 1 = deleted (nullptr until the first Delete)
     // fp16 screening copy (nullptr = off), only ever used to skip candidates
-    // whose f32 distance provably exceeds the list's worst.
+    // whose f32 distance provably exceeds the list's worst ("The fp16 screening copy").
     //   cosine: row r is fp16(x / |x| * 2^14) (no per-row value needed);
     //           NaN halves mark a row the screen must never reject
     //   L2:     row r is fp16(x * 2^e) with max|x_i| 2^e in [2^14, 2^15);
@@ -298,7 +298,7 @@ __device__ __forceinline__ float eval_rows_h16(const QReg<C>& q, const uint16_t*
     return reduce_rows<G, C::LPR>(p);
 }
 
-// Screening bounds, with y the row the fp16 copy stands for
+// Screening bounds ("The fp16 screening copy"), with y the row the fp16 copy stands for
 // (x / |x|_f32 for cosine, x for L2) and |y' - y| <= 2^-11 |y| (+ 2u from the
 // cosine normalisation, + a subnormal term far below 2^-30 |y|):
 //   cosine: |S / |q|_f32 - (the f32 cosine term)| <= 2^-11 + 2 gamma + 8u

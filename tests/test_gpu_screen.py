@@ -1,4 +1,4 @@
-"""GPU: the fp16 screening copy (option "screen") never changes
+"""GPU: the fp16 screening copy (option "screen", DESIGN.md §6, "The fp16 screening copy") never changes
 a beam search.  Every result (keys, f32 distance bits, counts) with the screen
 on must equal the screen-off search and the oracle's beam search, on data built
 to sit at the screen's edges: exact distance ties (integer-valued rows),
