@@ -11,7 +11,12 @@
   4m      : the same 10M vectors as ONE index on one GPU (replica layout).
   compat  : the reference's Search() semantics on the GPU vs the oracle on the
             host, same graph.
-Usage: python tools/bench_configs.py [3] [5] [4] [4m] [compat]"""
+  config 1: 10k x 128 U[-1,1) cosine, M=16 Ml=0.25 ef=20 k=10:
+            compat build (the reference's Add) and compat Search on the GPU
+            vs the oracle on one host core, recall of compat and beam search.
+  2b      : the headline graph (bench.py defaults) searched at batch 1, 1024,
+            10000 and 65536 (SURVEY 8(d) C2 batch sizes): latency and QPS.
+Usage: python tools/bench_configs.py [1] [2b] [3] [5] [4] [4m] [compat]"""
 import json
 import os
 import sys
@@ -211,3 +216,67 @@ if "compat" in which:
     print(json.dumps({"config": "compat Search() semantics, 200k x 768 cosine, M=16 ef=20 k=10",
                       "gpu_queries_per_s": round(4096 / dt, 1), "cpu_oracle_queries_per_s_1thread": round(512 / ct, 1),
                       "identical_results_first_512": same}), flush=True)
+
+
+if "1" in which:
+    import oracle as O  # CPU baseline and ground truth only
+
+    rng = np.random.default_rng(42)  # X ~ U[-1,1), seed 42, then the 1000 queries
+    n, d, nq = 10_000, 128, 1000
+    Xh = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    Qh = rng.uniform(-1, 1, (nq, d)).astype(np.float32)
+    keys = np.arange(n, dtype=np.int64)
+    g = H.Graph(M=16, Ml=0.25, EfSearch=20, Distance=H.CosineDistance, Rng=42)  # compat build = reference Add
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g.add_arrays(keys, Xh)
+    gbuild = time.perf_counter() - t0
+    o = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=16, Ml=0.25, EfSearch=20)
+    o.import_graph(**g.export())
+    ek, _, en = o.search(Qh, 10, mode=O.MODE_EXACT)
+    Qd = torch.from_numpy(Qh).to(dev)
+    S = Searcher(g, nq, 10, d, dev)
+    out = {}
+    for name, mode in (("compat", H.MODE_COMPAT), ("beam", H.MODE_BEAM)):
+        S.run(Qd, mode, 20)
+        dt, res = timed(lambda: S.run(Qd, mode, 20), reps=5)
+        k_, n_ = res[0].cpu().numpy(), res[2].cpu().numpy()
+        rec = float(np.mean([len(set(k_[b, : n_[b]]) & set(ek[b, : en[b]])) / 10 for b in range(nq)]))
+        out[name] = (nq / dt, rec, k_)
+    t0 = time.perf_counter()
+    ok, _, _ = o.search(Qh, 10, mode=O.MODE_COMPAT, ef=20)
+    ct = time.perf_counter() - t0
+    # the reference's own build on one core (oracle compat insert, same levels)
+    lv = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=16, Ml=0.25, EfSearch=20, seed=42).preview_levels(2000)
+    oc = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=16, Ml=0.25, EfSearch=20, seed=42)
+    t0 = time.perf_counter()
+    oc.add(keys[:2000], Xh[:2000], lv)
+    cbuild = 2000 / (time.perf_counter() - t0)
+    print(json.dumps({"config": "configs[0] 10k x 128 U[-1,1) cosine, M=16 Ml=0.25 ef=20 k=10, 1000 queries",
+                      "gpu_compat_build_inserts_per_s": round(n / gbuild, 1),
+                      "cpu_oracle_compat_build_inserts_per_s_1thread_2k_prefix": round(cbuild, 1),
+                      "gpu_compat_search_qps": round(out["compat"][0], 1), "compat_recall_at_10": round(out["compat"][1], 4),
+                      "cpu_oracle_compat_search_qps_1thread": round(nq / ct, 1),
+                      "gpu_compat_identical_to_oracle": bool(np.array_equal(ok, out["compat"][2])),
+                      "gpu_beam_ef20_qps": round(out["beam"][0], 1), "beam_ef20_recall_at_10": round(out["beam"][1], 4),
+                      "note": "compat recall is the reference algorithm's own (SURVEY A.3 simulated 0.022); "
+                              "beam = standard HNSW search on the same graph"}), flush=True)
+    g.close()
+
+if "2b" in which:
+    n, d = 1_000_000, 768
+    X = gen_vectors(n, d, 1234, 12, 1000, dev, "cosine")
+    Q = gen_vectors(65536, d, 1234 + 7777, 12, 1000, dev, "cosine")
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=1234, build_mode=H.BUILD_BATCH, m0=40,
+                ef_construction=400, heuristic=2, keep_pruned=1, prune_alpha_pct=115)
+    g.reserve(n, d)
+    g.add_device(np.arange(n), X.data_ptr(), n, d)
+    del X
+    for B in (1, 1024, 10000, 65536):
+        S = Searcher(g, B, 10, d, dev)
+        S.run(Q[:B], H.MODE_BEAM, 64)
+        reps = 200 if B == 1 else (20 if B <= 10000 else 5)
+        dt, _ = timed(lambda: S.run(Q[:B], H.MODE_BEAM, 64), reps=reps)
+        print(json.dumps({"config": "configs[1] 1M x 768 cosine ef=64 k=10, batch sweep", "batch": B,
+                          "ms_per_batch": round(dt * 1e3, 4), "queries_per_s": round(B / dt, 1)}), flush=True)
+    g.close()
