@@ -68,6 +68,7 @@ struct mhnsw_index {
     int compat_waves = 8;     // compat insert: waves scoring each distance batch (1 = the walking wave alone)
     int upper_ef = 1;         // beam search: upper-layer descent width
     int screen = 1;           // beam search: fp16 screening copy of the rows (results unchanged)
+    int fuse_descent = 1;     // batched insert: all greedy descents of a batch in one launch (same graph)
     // shape
     int dim = 0, pitch = 0, lpr = 0, vpl = 0;
     bool layers_exist = false;
@@ -101,6 +102,11 @@ struct mhnsw_index {
     // scratch
     DevBuf<float> qpad, qnorm, scores, tmp;
     DevBuf<uint32_t> cand;
+    DevBuf<uint32_t> border;           // batched insert: batch nodes by level, descending
+    uint32_t* ord_pin = nullptr;       // ... staged in pinned memory
+    int64_t ord_cap = 0;
+    hipEvent_t ord_ev = nullptr;       // the staging copy has been consumed
+    bool ord_pending = false;
     DevBuf<int64_t> okeys;
     DevBuf<float> odist;
     DevBuf<int32_t> on;
@@ -440,6 +446,12 @@ int run_build_compat(mhnsw_index* h, int64_t n0, int64_t n1, int top0) {
     return 0;
 }
 
+// One batch of the batched insert.  fuse_descent (default): one launch walks
+// every node's greedy descent through the layers above its level, then layer
+// l's search launch covers only the nodes with level >= l (a prefix of the
+// batch sorted by level); otherwise every layer's launch covers the whole
+// batch and descends the others itself.  Both read each layer before its
+// commit, so they build the same graph.
 int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t entry) {
     if (a1 <= a0) return 0;
     HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(h->cur_entry + a0), (int)entry, (size_t)(a1 - a0), h->stream));
@@ -448,9 +460,34 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
     int r;
     if ((r = sync_layer_table(h))) return r;
     const int efc = h->efc > 0 ? h->efc : h->ef;
+    const int64_t nb = a1 - a0;
+    std::vector<int64_t> count(MH_MAXL + 1, 0);  // nodes with level >= l
+    const bool fuse = h->fuse_descent != 0;
+    if (fuse) {
+        if (h->ord_cap < nb) {
+            if (h->ord_pin) (void)hipHostFree(h->ord_pin);
+            h->ord_pin = nullptr;
+            h->ord_cap = 0;
+            if (hipHostMalloc((void**)&h->ord_pin, (size_t)nb * 4, hipHostMallocDefault) != hipSuccess)
+                return fail(h, MHNSW_ENOMEM, "pinned allocation failed");
+            h->ord_cap = nb;
+        }
+        if ((r = ensure_buf(h, h->border, (size_t)nb))) return r;
+        if (h->ord_pending) HIPCHK(h, hipEventSynchronize(h->ord_ev));  // the previous batch's copy has read ord_pin
+        for (int64_t i = a0; i < a1; ++i) count[std::min(h->hlevels[i], MH_MAXL)]++;
+        for (int l = MH_MAXL - 1; l >= 0; --l) count[l] += count[l + 1];
+        std::vector<int64_t> pos(MH_MAXL + 1, 0);  // level-descending, stable within a level
+        for (int l = 0; l <= MH_MAXL; ++l) pos[l] = l < MH_MAXL ? count[l + 1] : 0;
+        for (int64_t i = a0; i < a1; ++i) h->ord_pin[pos[std::min(h->hlevels[i], MH_MAXL)]++] = (uint32_t)i;
+        HIPCHK(h, hipMemcpyAsync(h->border.p, h->ord_pin, (size_t)nb * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipEventRecord(h->ord_ev, h->stream));
+        h->ord_pending = true;
+    }
     for (int l = top; l >= 0; --l) {
         const int mcap = l == 0 ? m0_of(h) : h->M;
         BatchBuildArgs a;
+        a.order = nullptr;
+        a.count = 0;
         a.g = graph_view(h);
         a.layer = l;
         a.n0 = a0;
@@ -470,6 +507,12 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         a.touched_cnt = h->touched_cnt;
         a.stats = h->d_stats + 4;
         a.vis_log2 = h->vis_log2;
+        if (fuse) {
+            if (l == top) LCHK(h, launch_build_batch_descend(a, h->lpr, h->vpl, h->stream));  // a.layer = top
+            if (l > maxlvl) continue;
+            a.order = h->border.p;
+            a.count = count[std::min(l, MH_MAXL)];
+        }
         HIPCHK(h, hipMemsetAsync(h->touched_cnt, 0, 4, h->stream));
         LCHK(h, launch_build_batch_search(a, h->lpr, h->vpl, h->stream));
         if (maxlvl >= l) LCHK(h, launch_build_batch_commit(a, h->lpr, h->vpl, (a1 - a0) * mcap, h->stream));
@@ -909,7 +952,8 @@ int mhnsw_create(int metric, int M, double ml, int ef_search, uint64_t seed, mhn
         hipMalloc(&h->d_layer_entry, MH_MAXL * 4) != hipSuccess ||
         hipMalloc(&h->d_layers, MH_MAXL * sizeof(LayerDev)) != hipSuccess || hipEventCreate(&h->ev0) != hipSuccess ||
         hipEventCreate(&h->ev1) != hipSuccess || hipEventCreateWithFlags(&h->scr_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->meta_ev, hipEventDisableTiming) != hipSuccess || hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
+        hipEventCreateWithFlags(&h->meta_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ord_ev, hipEventDisableTiming) != hipSuccess || hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
         mhnsw_destroy(h);
         return fail(nullptr, MHNSW_EDEVICE, "device initialisation failed");
     }
@@ -951,6 +995,7 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->scores.p);
     F(h->tmp.p);
     F(h->cand.p);
+    F(h->border.p);
     F(h->okeys.p);
     F(h->odist.p);
     F(h->on.p);
@@ -975,6 +1020,8 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->xnflag.p);
     if (h->scr_ev) (void)hipEventDestroy(h->scr_ev);
     if (h->meta_ev) (void)hipEventDestroy(h->meta_ev);
+    if (h->ord_ev) (void)hipEventDestroy(h->ord_ev);
+    if (h->ord_pin) (void)hipHostFree(h->ord_pin);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1050,6 +1097,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "upper_ef") {
         if (v < 1 || v > 64) return fail(h, MHNSW_EINVAL, "upper_ef must be in [1, 64]");
         h->upper_ef = (int)v;
+    } else if (n == "fuse_descent") {
+        if (v != 0 && v != 1) return fail(h, MHNSW_EINVAL, "fuse_descent must be 0 or 1");
+        h->fuse_descent = (int)v;
     } else if (n == "screen") {
         if (v != 0 && v != 1) return fail(h, MHNSW_EINVAL, "screen must be 0 or 1");
         if ((int)v == h->screen) return MHNSW_OK;
@@ -1098,6 +1148,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "compat_waves") *v = h->compat_waves;
     else if (n == "upper_ef") *v = h->upper_ef;
     else if (n == "screen") *v = h->screen;
+    else if (n == "fuse_descent") *v = h->fuse_descent;
     else if (n == "strkey_relabels") *v = h->relabels;
     else if (n == "strkeys") *v = (int64_t)h->s2l.size();
     else if (n == "pitch") *v = h->pitch;

@@ -459,12 +459,50 @@ static int launch_build_compat_t(const CompatBuildArgs& a, int waves, hipStream_
 // ---------------------------------------------------------------------------
 // batched build
 // ---------------------------------------------------------------------------
-template <class C, int R, int G, bool SCREEN>
-__global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
+// Greedy descent (ef = 1) of every new node through the layers above its own
+// level, all layers in one launch.  Every layer l is read before its commit
+// (run_batch_layers commits layer l only after this kernel), exactly what the
+// per-layer descent inside k_batch_search reads, so the graph is the same.
+template <class C, int G, bool SCREEN>
+__global__ __launch_bounds__(64) void k_batch_descend(BatchBuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int64_t u64 = a.n0 + blockIdx.x;
     if (u64 >= a.n1) return;
     const uint32_t u = (uint32_t)u64;
+    const int lv = a.levels[u];
+    if (lv >= a.layer) return;
+    WaveStats st;
+    QReg<C> q;
+    load_query(q, a.g.vecs + (size_t)u * a.g.pitch);
+    const float qn = a.g.norms[u];
+    uint32_t ep = a.cur_entry[u];
+    for (int l = a.layer; l > lv; --l) {
+        BList<1> L1;
+        beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, 1, q, qn, L1, smem, a.vis_log2, st);
+        float d;
+        uint32_t id;
+        bl_at(L1, 0, d, id);
+        if (id != EMPTY_ID) ep = id & ID_MASK;
+    }
+    if (lane_id() == 0) {
+        a.cur_entry[u] = ep;
+        atomicAdd(&a.stats[0], st.E);
+        atomicAdd(&a.stats[1], st.X);
+    }
+}
+
+template <class C, int R, int G, bool SCREEN>
+__global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t u;
+    if (a.order) {
+        if (blockIdx.x >= a.count) return;
+        u = a.order[blockIdx.x];
+    } else {
+        const int64_t u64 = a.n0 + blockIdx.x;
+        if (u64 >= a.n1) return;
+        u = (uint32_t)u64;
+    }
     const int lane = lane_id();
     const int l = a.layer;
     WaveStats st;
@@ -834,10 +872,22 @@ static int launch_delete_compat_t(const DeleteArgs& a, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+template <class C, int G>
+static int launch_batch_descend_t(const BatchBuildArgs& a, hipStream_t s) {
+    const size_t lds = (size_t)4 << a.vis_log2;
+    const int64_t n = a.n1 - a.n0;
+    if (n <= 0) return 0;
+    if (a.g.h16)
+        hipLaunchKernelGGL((k_batch_descend<C, G, true>), dim3((unsigned)n), dim3(64), lds, s, a);
+    else
+        hipLaunchKernelGGL((k_batch_descend<C, G, false>), dim3((unsigned)n), dim3(64), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 template <class C, int R, int G>
 static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 << a.vis_log2;
-    const int64_t n = a.n1 - a.n0;
+    const int64_t n = a.order ? a.count : a.n1 - a.n0;
     if (n <= 0) return 0;
     if (a.g.h16)  // fp16 screening: same graph, fewer bytes per candidate
         hipLaunchKernelGGL((k_batch_search<C, R, G, true>), dim3((unsigned)n), dim3(64), lds, s, a);
@@ -863,6 +913,14 @@ int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, int waves, h
     // replenish): two rows in flight per group keeps it spill-free
 #define X_(L, V, G) \
     if (lpr == L && vpl == V) return launch_build_compat_t<Cfg<L, V>, (G < 2 ? G : 2)>(a, waves, s);
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return -3;
+}
+
+int launch_build_batch_descend(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s) {
+#define X_(L, V, G) \
+    if (lpr == L && vpl == V) return launch_batch_descend_t<Cfg<L, V>, G>(a, s);
     MH_FOR_EACH_CFG(X_)
 #undef X_
     return -3;

@@ -126,8 +126,12 @@ struct BatchBuildArgs {
     int32_t* touched_cnt;         // [1]
     unsigned long long* stats;    // [0]=dist evals [1]=expansions [2]=dropped requests
     int vis_log2;
+    const uint32_t* order;        // nullable: node of workgroup b is order[b] (b < count), nodes sorted by
+    int64_t count;                //   level descending so that level >= layer is a prefix
 };
 int launch_build_batch_search(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s);
+// greedy descent of every node u in [n0, n1) through layers a.layer .. levels[u] + 1
+int launch_build_batch_descend(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s);
 int launch_build_batch_commit(const BatchBuildArgs& a, int lpr, int vpl, int64_t n_touched, hipStream_t s);
 
 // ---- exact / merge ----

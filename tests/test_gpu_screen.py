@@ -113,17 +113,22 @@ def test_screen_follows_metric_change(H, O):
 
 @pytest.mark.parametrize("metric", [0, 1])
 def test_screened_batch_build_identical(H, metric):
-    """The batched insert's searches screen too: the graph is the same."""
+    """The batched insert's searches screen too, and its greedy descents run
+    in one launch per batch (fuse_descent): every combination builds the same
+    graph as the plain per-layer, unscreened insert."""
+    from tests.test_gpu_parity import _same_graph
+
     rng = np.random.default_rng(21 + metric)
     n, d = 12000, 96
     X, _ = _adversarial(rng, n, d, metric)
-    ex = []
-    for screen in (0, 1):
+    ex = {}
+    for screen, fuse in ((0, 0), (1, 0), (0, 1), (1, 1)):
         g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
-                    ef_construction=80, heuristic=2, keep_pruned=1, screen=screen)
-        g.add_arrays(np.arange(n), X)
+                    ef_construction=80, heuristic=2, keep_pruned=1, screen=screen, fuse_descent=fuse)
+        g.add_arrays(np.arange(n // 3), X[: n // 3])   # two calls: later batches descend a multi-layer graph
+        g.add_arrays(np.arange(n // 3, n), X[n // 3:])
         assert g.stats()["dropped_proposals"] == 0
-        ex.append(g.export())
+        ex[(screen, fuse)] = g.export()
         g.close()
-    from tests.test_gpu_parity import _same_graph
-    _same_graph(ex[0], ex[1])
+    for key in ((1, 0), (0, 1), (1, 1)):
+        _same_graph(ex[(0, 0)], ex[key])

@@ -1,0 +1,31 @@
+"""Batched-insert probe (BASELINE configs[2]: 1M x 768 Euclidean, M=16, M0=48,
+heuristic 2): inserts/s and per-insert counters for each efConstruction given.
+Usage: python tools/build_probe.py [efc ...]"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import hnsw_amd as H  # noqa: E402
+from bench import gen_vectors  # noqa: E402
+
+dev = torch.device("cuda")
+n = int(os.environ.get("BUILD_N", 1_000_000))
+X = gen_vectors(n, 768, 77, 12, 1000, dev, "euclidean")
+opts = dict(kv.split("=") for kv in os.environ.get("BUILD_OPTS", "").split(",") if kv)
+for efc in [int(a) for a in sys.argv[1:]] or [64]:
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.EuclideanDistance, Rng=5, build_mode=H.BUILD_BATCH,
+                m0=48, ef_construction=efc, heuristic=2, **{k: int(v) for k, v in opts.items()})
+    g.reserve(n, 768)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g.add_device(np.arange(n), X.data_ptr(), n, 768)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = g.stats()
+    print(f"efc={efc} {opts}: {n / dt:.0f} inserts/s ({dt:.2f} s), {st['build_dist_evals'] / n:.0f} evals/insert, "
+          f"{st['build_expansions'] / n:.0f} expansions/insert, dropped {st['dropped_proposals']}", flush=True)
+    g.close()
