@@ -105,7 +105,7 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
         mine = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane));
         key = g.keys[mine];
     }
-    bitonic64(key, mine);
+    rank_sort(key, mine, dn);
     if (lane < dn) vis_probe(S.cs.vis, vmask, mine);  // graph.go:187-189
     // stage every neighbour's row (deg, entries, keys) -- rows j < dn, j-major
     const int mydeg = lane < dn ? min(ld_i32<true>(g.layers[l].deg + mine), capl) : -1;
@@ -138,7 +138,7 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
             th = S.radj[j * capl + lane];
             tk = S.rkey[j * capl + lane];
         }
-        bitonic64(tk, th);
+        rank_sort(tk, th, max(0, min(dnb, S.hcap - j * capl)));
         int pr = 0;
         if (lane < dnb) pr = vis_probe(S.cs.vis, vmask, th);
         if (__ballot(pr == 2)) err = 1;
@@ -153,25 +153,91 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
     }
     ev.sync();
     st.E += ncand;
-    GHeap h{S.hd, S.hi, 0};
+    // distances in push order (the reference pushes each into its heap)
     {
         QReg<C> q;
         load_query(q, g.vecs + (size_t)n * g.pitch);
         const float qn = g.norms[n];
+        int t = 0;
         ev.template run_list<C, G>(g, q, qn, ncand, COSINE,  // graph.go:204 hard-coded cosine
                                    [&](float d, uint32_t u) {
-                                       if (h.n < S.hcap) gh_push(h, d, u);
-                                       else err |= 8;
+                                       if (lane == 0) {
+                                           S.hd[t] = d;
+                                           S.hi[t] = u;
+                                       }
+                                       ++t;
                                    });
     }
-    // graph.go:213-218 (len < m before every add: addNeighbor cannot evict)
-    while (h.n > 0) {
+    ev.sync();
+    // graph.go:213-218 (len < m before every add: addNeighbor cannot evict).
+    // Every Pop returns the heap's minimum.  While no distance is NaN and the
+    // minimum of what is left is unique, that is the arg-min whatever shape
+    // the heap has, so the pushes are skipped.  Otherwise the heap is built in
+    // place by replaying the pushes (element e of the push-order array is the
+    // e-th push), the pops made so far are replayed, and the walk continues on
+    // the heap exactly as the reference's.
+    bool anynan = false;
+    for (int e = lane; e < ncand; e += 64) anynan |= !(S.hd[e] == S.hd[e]);
+    bool fast = __ballot(anynan) == 0ull;
+    uint32_t popped = 0xFFFFFFFFu;  // fast path: lane j holds the index of the j-th pop
+    int npop = 0;
+    GHeap h{S.hd, S.hi, 0};
+    auto gone = [&](int e) {
+        bool r = false;
+        for (int j = 0; j < npop; ++j) r |= rl_u(popped, j) == (uint32_t)e;
+        return r;
+    };
+    auto replay = [&]() {
+        for (int e = 0; e < ncand; ++e) {
+            h.n = e + 1;
+            gh_up(h, e);
+        }
+        for (int j = 0; j < npop; ++j) {
+            float bd;
+            uint32_t bb;
+            gh_pop(h, bd, bb);
+        }
+        fast = false;
+    };
+    if (!fast) replay();
+    for (;;) {
         int cur = ld_i32<true>(g.layers[l].deg + n);
         if (cur < 0) cur = 0;
         if (cur >= m) break;
-        float bd;
         uint32_t best;
-        gh_pop(h, bd, best);
+        if (fast) {
+            if (npop >= ncand) break;
+            float mv = __int_as_float(0x7f800000);
+            int mi = -1;
+            for (int e = lane; e < ncand; e += 64) {
+                const float v = S.hd[e];
+                if (!gone(e) && (mi < 0 || v < mv)) {
+                    mv = v;
+                    mi = e;
+                }
+            }
+            float wm = mi < 0 ? __int_as_float(0x7f800000) : mv;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) wm = fminf(wm, __shfl_xor(wm, o, 64));
+            int eq = 0;
+            for (int e = lane; e < ncand; e += 64) eq += (!gone(e) && S.hd[e] == wm) ? 1 : 0;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) eq += __shfl_xor(eq, o, 64);
+            if (eq == 1 && npop < 64) {
+                const unsigned long long own = __ballot(mi >= 0 && mv == wm);
+                const int bi = __shfl(mi, __ffsll((long long)own) - 1, 64);
+                best = S.hi[bi];
+                if (lane == npop) popped = (uint32_t)bi;
+                ++npop;
+            } else {
+                replay();  // a tie at the minimum: the heap's shape decides
+            }
+        }
+        if (!fast) {
+            if (h.n <= 0) break;
+            float bd;
+            gh_pop(h, bd, best);
+        }
         list_append(g, l, n, best, ev);
     }
 }
@@ -190,7 +256,7 @@ __device__ void add_neighbor(const GraphDev& g, int l, uint32_t n, uint32_t nw, 
         nb = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane));
         key = g.keys[nb];
     }
-    bitonic64(key, nb);  // Go map order -> ascending key
+    rank_sort(key, nb, d);  // Go map order -> ascending key
     QReg<C> q;
     load_query(q, g.vecs + (size_t)n * g.pitch);
     const float qn = g.norms[n];
@@ -709,7 +775,7 @@ __device__ void isolate(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& 
         mine = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane));
         key = g.keys[mine];
     }
-    bitonic64(key, mine);
+    rank_sort(key, mine, dn);
     for (int j = 0; j < dn; ++j) {
         const uint32_t x = rl_u(mine, j);
         if (ld_i32<true>(g.layers[l].deg + x) < 0) continue;  // neighbor.neighbors == nil

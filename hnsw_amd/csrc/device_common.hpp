@@ -94,11 +94,6 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 __device__ __forceinline__ uint32_t shfl_u(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
-__device__ __forceinline__ int64_t shfl_xor_i64(int64_t v, int m) {
-    int lo = __shfl_xor((int)(uint32_t)(uint64_t)v, m, 64);
-    int hi = __shfl_xor((int)(uint32_t)((uint64_t)v >> 32), m, 64);
-    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
 // push-style permute: lane l's value lands in lane dst(l)
 __device__ __forceinline__ uint32_t push_to(uint32_t v, int dst) {
     return (uint32_t)__builtin_amdgcn_ds_permute(dst << 2, (int)v);
@@ -520,24 +515,25 @@ __device__ __forceinline__ void gh_pop(GHeap& h, float& d, uint32_t& id) {
 __device__ __forceinline__ void gh_poplast(GHeap& h) { h.n--; }
 
 // ---------------------------------------------------------------------------
-// bitonic sort of (key, id) across the 64 lanes, ascending
+// Ascending (key, id) order of lanes 0..cnt-1 (cnt uniform, <= 64; lanes >= cnt
+// keep their values): each lane counts the entries before it -- cnt uniform
+// readlanes, no cross-lane latency chain -- and one permute scatters them.
+// Equal pairs (duplicate entries) keep lane order.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void bitonic64(int64_t& key, uint32_t& id) {
+__device__ __forceinline__ void rank_sort(int64_t& key, uint32_t& id, int cnt) {
     const int lane = lane_id();
-#pragma unroll
-    for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            int64_t ok = shfl_xor_i64(key, j);
-            uint32_t oi = (uint32_t)__shfl_xor((int)id, j, 64);
-            const bool take_min = ((lane & j) == 0) == ((lane & k) == 0);
-            const bool other_less = ok < key || (ok == key && oi < id);
-            if (take_min == other_less) {
-                key = ok;
-                id = oi;
-            }
-        }
+    const uint32_t klo = (uint32_t)(uint64_t)key, khi = (uint32_t)((uint64_t)key >> 32);
+    int r = 0;
+    for (int j = 0; j < cnt; ++j) {
+        const int64_t kj = (int64_t)(((uint64_t)rl_u(khi, j) << 32) | rl_u(klo, j));
+        const uint32_t ij = rl_u(id, j);
+        r += (kj < key || (kj == key && (ij < id || (ij == id && j < lane)))) ? 1 : 0;
     }
+    const int dst = lane < cnt ? r : lane;
+    const uint32_t nlo = push_to(klo, dst), nhi = push_to(khi, dst);
+    id = push_to(id, dst);
+    key = (int64_t)(((uint64_t)nhi << 32) | nlo);
 }
+
 
 }  // namespace mh

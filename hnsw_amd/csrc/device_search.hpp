@@ -275,7 +275,7 @@ __device__ __forceinline__ int compat_layer(const GraphDev& g, int layer, uint32
             nb = guard_id(g, (uint32_t)ld_i32<COH>(adjp + (size_t)cur * capl + lane));
             key = g.keys[nb];
         }
-        bitonic64(key, nb);  // graph.go:137-138 ascending key order
+        rank_sort(key, nb, deg);  // graph.go:137-138 ascending key order
         int pr = 0;
         if (lane < deg) pr = vis_probe(S.vis, vmask, nb);  // graph.go:141-144
         if (__ballot(pr == 2)) err = 1;                   // exact visited set required here
