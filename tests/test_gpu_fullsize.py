@@ -1,0 +1,139 @@
+"""GPU parity at BASELINE.json's full sizes, through size-independent
+properties (the oracle itself only finishes small cases in seconds):
+
+  configs[1]  1M x 768 cosine graph (the bench.py index): the fp16 screen never
+              changes a result (screen on == off, bitwise); every reported
+              distance equals the oracle's canonical distance of that pair
+              (sampled); lists sorted, keys unique; self-queries find
+              themselves; beam recall against the certified exact path.
+  configs[2]  1M x 768 Euclidean batched insert (efConstruction 64): a
+              well-formed graph (ids in range, no self loops, sets, degree
+              caps) reaching recall@10 >= 0.99 at ef 64.
+  configs[4]  1M x 1536 cosine exact path, batch 1024: f32-input and bf16x3
+              scores certify to the same results, equal to the oracle's
+              canonical distances on sampled pairs, self-queries first.
+Each builds in seconds on the GPU; vectors come from bench.gen_vectors."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _gen(n, d, seed, metric):
+    from bench import gen_vectors
+
+    return gen_vectors(n, d, seed, 12, 1000, torch.device("cuda"), metric)
+
+
+def _search(g, Q, k, mode, ef):
+    from bench import Searcher
+
+    S = Searcher(g, Q.shape[0], k, Q.shape[1], torch.device("cuda"))
+    return [x.clone().cpu().numpy() for x in S.run(Q, mode, ef)]
+
+
+def _check_lists(keys, dist, n, N):
+    for b in range(len(n)):
+        kb, db = keys[b, : n[b]], dist[b, : n[b]]
+        assert len(set(kb.tolist())) == len(kb), b
+        assert ((kb >= 0) & (kb < N)).all(), b
+        assert np.all(db[1:] >= db[:-1]), b
+
+
+def _check_oracle_distances(O, metric, X, Q, keys, n, rows=128):
+    """the reported distance of (query, result) pairs == the oracle's canonical one, bitwise"""
+    sel = np.arange(0, len(n), max(1, len(n) // rows))[:rows]
+    for b in sel:
+        kb = keys[b, : n[b]]
+        xs = X[torch.from_numpy(kb).to(X.device)].cpu().numpy()
+        q = Q[b].cpu().numpy()
+        want = np.array([O.distance(metric, O.ORDER_DEV, x, q) for x in xs], np.float32)
+        yield b, want
+
+
+def test_fullsize_c2_beam(H, O):
+    n, d, B = 1_000_000, 768, 2048
+    X = _gen(n, d, 1234, "cosine")
+    Q = _gen(B, d, 1234 + 7777, "cosine")
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=1234, build_mode=H.BUILD_BATCH, m0=40,
+                ef_construction=400, heuristic=2, keep_pruned=1, prune_alpha_pct=115)
+    g.reserve(n, d)
+    g.add_device(np.arange(n), X.data_ptr(), n, d)
+    assert len(g) == n and g.stats()["dropped_proposals"] == 0
+    on = _search(g, Q, 10, H.MODE_BEAM, 64)
+    g.set_option("screen", 0)
+    off = _search(g, Q, 10, H.MODE_BEAM, 64)
+    g.set_option("screen", 1)
+    assert np.array_equal(on[2], off[2]) and np.array_equal(on[0], off[0])
+    assert np.array_equal(on[1].view(np.uint32), off[1].view(np.uint32))
+    keys, dist, cnt = on
+    assert (cnt == 10).all()
+    _check_lists(keys, dist, cnt, n)
+    for b, want in _check_oracle_distances(O, 0, X, Q, keys, cnt):
+        assert np.array_equal(dist[b, : cnt[b]].view(np.uint32), want.view(np.uint32)), b
+    ek, ed, en = _search(g, Q, 10, H.MODE_EXACT, 0)
+    _check_lists(ek, ed, en, n)
+    rec = np.mean([len(set(keys[b]) & set(ek[b, : en[b]])) / 10 for b in range(B)])
+    assert rec >= 0.98, rec
+    # self-queries: a stored row finds itself first (distance 0 or the -1.19e-7 of parallel vectors)
+    ids = np.random.default_rng(5).choice(n, 512, replace=False)
+    sk, sd, sn = _search(g, X[torch.from_numpy(ids).cuda()].contiguous(), 10, H.MODE_BEAM, 64)
+    assert (sk[:, 0] == ids).mean() >= 0.99
+    assert np.all(np.abs(sd[:, 0][sk[:, 0] == ids]) <= 2.5e-7)
+    g.close()
+
+
+def test_fullsize_c3_build(H):
+    n, d, B = 1_000_000, 768, 1024
+    X = _gen(n, d, 77, "euclidean")
+    Q = _gen(B, d, 78, "euclidean")
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.EuclideanDistance, Rng=5, build_mode=H.BUILD_BATCH, m0=48,
+                ef_construction=64, heuristic=2)
+    g.reserve(n, d)
+    g.add_device(np.arange(n), X.data_ptr(), n, d)
+    assert g.stats()["dropped_proposals"] == 0
+    ex = g.export()
+    deg, adj = ex["deg"], ex["adj"]
+    L, N, cap = adj.shape
+    assert N == n
+    for l in range(L):
+        dl = deg[l]
+        assert (dl >= -2).all() and (dl < cap).all()
+        rows = np.nonzero(dl > 0)[0]
+        for i in rows[:: max(1, len(rows) // 20000)]:  # sampled rows: ids in range, no self loops, sets
+            r = adj[l, i, : dl[i]]
+            assert ((r >= 0) & (r < n)).all() and (r != i).all() and len(set(r.tolist())) == len(r), (l, i)
+            assert (deg[l, r] != -2).all(), (l, i)  # every neighbour is a member of the layer
+    assert (deg[0] >= 1).all()
+    bk, bd, bn = _search(g, Q, 10, H.MODE_BEAM, 64)
+    ek, ed, en = _search(g, Q, 10, H.MODE_EXACT, 0)
+    _check_lists(bk, bd, bn, n)
+    rec = np.mean([len(set(bk[b, : bn[b]]) & set(ek[b, : en[b]])) / 10 for b in range(B)])
+    assert rec >= 0.99, rec
+    g.close()
+
+
+def test_fullsize_c5_exact(H, O):
+    n, d, B = 1_000_000, 1536, 1024
+    X = _gen(n, d, 55, "cosine")
+    Q = _gen(B, d, 56, "cosine")
+    ids = np.arange(0, n, n // 16)[:16]
+    Q[:16] = X[torch.from_numpy(ids).cuda()]  # self-queries
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_FLAT)
+    g.reserve(n, d)
+    g.add_device(np.arange(n), X.data_ptr(), n, d)
+    res = {}
+    for prec in (0, 1):
+        g.set_option("exact_precision", prec)
+        g.reset_stats()
+        res[prec] = _search(g, Q, 10, H.MODE_EXACT, 0)
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+    keys, dist, cnt = res[1]
+    assert (cnt == 10).all()
+    _check_lists(keys, dist, cnt, n)
+    assert (keys[:16, 0] == ids).all()
+    for b, want in _check_oracle_distances(O, 0, X, Q, keys, cnt, rows=64):
+        assert np.array_equal(dist[b, : cnt[b]].view(np.uint32), want.view(np.uint32)), b
+    g.close()
