@@ -63,7 +63,7 @@ struct mhnsw_index {
     int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
     int vis_log2 = 12;
     int exact_kk = 0;
-    int exact_precision = 1;  // 0: f32-input MFMA scores, 1: bf16x3 split MFMA scores (both certified)
+    int exact_precision = 2;  // scores: 0 f32-input MFMA, 1 bf16x3 split, 2 fp16 2-product split (all certified)
     int exact_tile = 0;       // bf16x3 GEMM tile variant (exact.hip launch_exact_scores_x3)
     int compat_waves = 8;     // compat insert: waves scoring each distance batch (1 = the walking wave alone)
     int upper_ef = 1;         // beam search: upper-layer descent width
@@ -118,6 +118,9 @@ struct mhnsw_index {
     // immutable once added; import resets), per-chunk query planes, certificate state
     DevBuf<uint16_t> xsplit, qsplit;
     int64_t xsplit_rows = 0, xsplit_plane = 0;  // rows converted; plane stride they were written with
+    int xsplit_kind = 0;                        // 1: bf16 hi/lo planes, 2: fp16 hi plane + xinv (exact_precision)
+    DevBuf<float> xinv, qinv;                   // exact_precision 2: per-row / per-query unscale
+    DevBuf<float> xerr;                         // ... and the rows' max relative fp16 rounding
     DevBuf<float> xbound, xmaxn, xsegd;
     DevBuf<uint32_t> xsegi;
     DevBuf<uint8_t> xflag;
@@ -663,8 +666,10 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     }
     h->layers_exist = true;
     h->n = n1;
-    if (flat)
-        r = 0;
+    if (flat)  // members of layer 0 without links (an empty neighbour map, not an absent node)
+        r = hipMemsetD32Async((hipDeviceptr_t)(h->layers[0].deg + n0), 0, (size_t)n, h->stream) == hipSuccess
+                ? 0
+                : fail(h, MHNSW_EDEVICE, "device memset failed");
     else if (compat)
         r = run_build_compat(h, n0, n1, top0);
     else
@@ -759,8 +764,12 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
     HIPCHK(h, hipMemsetAsync(h->d_err, 0, sizeof(int), s));
     if (mode == MHNSW_MODE_EXACT) {
         if (k > 256) return fail(h, MHNSW_EUNSUPPORTED, "exact mode supports k <= 256");
-        const int kk = h->exact_kk > 0 ? std::min(256, std::max(h->exact_kk, k)) : std::min(256, std::max(2 * k, k + 16));
-        const bool split = h->exact_precision == 1;
+        const bool split = h->exact_precision != 0;
+        const bool h2 = h->exact_precision == 2;
+        // preselect width: the fp16 2-product scores carry a ~2x larger error bound, so the
+        // kk-th score must sit further from the k-th distance for the certificate
+        const int kk = h->exact_kk > 0 ? std::min(256, std::max(h->exact_kk, k))
+                                       : std::min(256, h2 ? std::max(2 * k, 64) : std::max(2 * k, k + 16));
         const int64_t ldS = (h->n + 255) / 256 * 256;
         const int64_t budget = (int64_t)4 << 30;  // score workspace bytes
         int64_t qc = std::max<int64_t>(1, std::min<int64_t>(B, budget / (ldS * 4)));
@@ -779,12 +788,17 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             return r;
         if (split) {
             const int64_t plane = h->capn * h->pitch;
-            if (h->xsplit.n < (size_t)plane * 2 || h->xsplit_plane != plane) {
+            const int kind = h2 ? 2 : 1;
+            if (h->xsplit.n < (size_t)plane * 2 || h->xsplit_plane != plane || h->xsplit_kind != kind) {
                 if ((r = ensure_buf(h, h->xsplit, (size_t)plane * 2))) return r;
                 h->xsplit_rows = 0;
                 h->xsplit_plane = plane;
+                h->xsplit_kind = kind;
             }
             if ((r = ensure_buf(h, h->qsplit, (size_t)qc * h->pitch * 2))) return r;
+            if (h2 && ((r = ensure_buf(h, h->xinv, (size_t)h->capn)) || (r = ensure_buf(h, h->qinv, (size_t)qc)) ||
+                       (r = ensure_buf(h, h->xerr, 1))))
+                return r;
         }
         LCHK(h, launch_norms(h->qpad.p, 0, B, h->pitch, h->lpr, h->vpl, h->qnorm.p, s));
         if ((r = sync_layer_table(h)) || (r = order_meta(h, s))) return r;
@@ -793,8 +807,12 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         // order of n-term f32 summation relative to the sum of magnitudes)
         const double u = std::ldexp(1.0, -24);
         auto gam = [&](double nn) { return nn * u / (1.0 - nn * u); };
-        const double g_mfma = gam((split ? 3.0 : 1.0) * h->pitch + 1);
-        const double e_split = split ? 3.02 * std::ldexp(1.0, -16) : 0.0;
+        // products per element: f32 1, bf16x3 3, fp16 2-product 2.  Split error: bf16x3
+        // drops ql.xl and the planes' tails (3.02 * 2^-16); fp16 2-product rounds the
+        // rows to fp16 (2^-11 |x|, Cauchy-Schwarz) and the queries to hi + lo (2^-21)
+        const double g_mfma = gam((h2 ? 2.0 : split ? 3.0 : 1.0) * h->pitch + 1);
+        // (fp16: the rows' part is the measured max |x' - x| / |x| <= 2^-11, added on the device)
+        const double e_split = h2 ? std::ldexp(1.0, -21) : split ? 3.02 * std::ldexp(1.0, -16) : 0.0;
         const double g_can = gam(4.0 * h->vpl + 8);  // canonical: 4*VPL fmaf per lane + 6 butterfly levels
         CertArgs cert{};
         cert.qnorm = h->qnorm.p;
@@ -806,11 +824,18 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         cert.flagged = h->xflagged.p;
         cert.nflag = h->xnflag.p;
         cert.stats = h->d_stats + 3;
+        cert.xerr = h2 ? h->xerr.p : nullptr;
         if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
         if (split && h->xsplit_rows < h->n) {
             uint16_t* xh = h->xsplit.p;
             uint16_t* xl = h->xsplit.p + (size_t)h->capn * h->pitch;
-            LCHK(h, launch_split_rows(h->vecs, h->xsplit_rows, h->n, h->pitch, h->capn, xh, xl, s));
+            if (h2) {
+                if (h->xsplit_rows == 0) HIPCHK(h, hipMemsetAsync(h->xerr.p, 0, sizeof(float), s));
+                LCHK(h, launch_split_h16(h->vecs, h->xsplit_rows, h->n, h->pitch, h->capn, xh, nullptr, h->xinv.p,
+                                         h->xerr.p, s));
+            }
+            else
+                LCHK(h, launch_split_rows(h->vecs, h->xsplit_rows, h->n, h->pitch, h->capn, xh, xl, s));
             h->xsplit_rows = h->n;
         }
         if (h->metric == EUCLIDEAN) {
@@ -850,8 +875,17 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
                 a.Qh = h->qsplit.p;
                 a.Ql = h->qsplit.p + (size_t)qc * h->pitch;
                 a.ldQs = qc;
-                LCHK(h, launch_split_rows(a.Q, 0, nb, h->pitch, qc, h->qsplit.p, h->qsplit.p + (size_t)qc * h->pitch, s));
-                LCHK(h, launch_exact_scores_x3(a, h->exact_tile, s));
+                if (h2) {
+                    a.xinv = h->xinv.p;
+                    a.qinv = h->qinv.p;
+                    LCHK(h, launch_split_h16(a.Q, 0, nb, h->pitch, qc, h->qsplit.p, h->qsplit.p + (size_t)qc * h->pitch,
+                                             h->qinv.p, nullptr, s));
+                    LCHK(h, launch_exact_scores_x2h(a, h->exact_tile, s));
+                } else {
+                    LCHK(h, launch_split_rows(a.Q, 0, nb, h->pitch, qc, h->qsplit.p,
+                                              h->qsplit.p + (size_t)qc * h->pitch, s));
+                    LCHK(h, launch_exact_scores_x3(a, h->exact_tile, s));
+                }
             } else {
                 LCHK(h, launch_exact_scores(a, s));
             }
@@ -1010,6 +1044,9 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->non.p);
     F(h->nos.p);
     F(h->xsplit.p);
+    F(h->xinv.p);
+    F(h->qinv.p);
+    F(h->xerr.p);
     F(h->qsplit.p);
     F(h->xbound.p);
     F(h->xsegd.p);
@@ -1122,7 +1159,8 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
         if (v != 1 && v != 8) return fail(h, MHNSW_EINVAL, "compat_waves must be 1 or 8");
         h->compat_waves = (int)v;
     } else if (n == "exact_precision") {
-        if (v != 0 && v != 1) return fail(h, MHNSW_EINVAL, "exact_precision must be 0 (f32) or 1 (bf16x3)");
+        if (v < 0 || v > 2)
+            return fail(h, MHNSW_EINVAL, "exact_precision must be 0 (f32), 1 (bf16x3) or 2 (fp16 2-product)");
         h->exact_precision = (int)v;
     } else {
         return fail(h, MHNSW_EINVAL, "unknown option '%s'", n.c_str());

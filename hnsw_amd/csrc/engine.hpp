@@ -164,9 +164,16 @@ struct ExactArgs {
     const uint16_t* Qh;   // split mode: bf16 hi / lo planes of Q, K-blocked
     const uint16_t* Ql;
     int64_t ldQs;
+    const float* xinv;    // fp16 2-product mode: per-row / per-query unscale 2^-e (NaN: outside the bound)
+    const float* qinv;
 };
 int launch_exact_scores(const ExactArgs& a, hipStream_t s);     // f32-input MFMA
 int launch_exact_scores_x3(const ExactArgs& a, int tile, hipStream_t s);  // bf16x3 split MFMA
+// fp16 2-product split: (qh + ql) . xh on v_mfma_f32_32x32x16_f16 (Xl unused)
+int launch_exact_scores_x2h(const ExactArgs& a, int tile, hipStream_t s);
+// err (nullable): running max of the rows' relative fp16 rounding |x' - x| / |x|
+int launch_split_h16(const float* src, int64_t r0, int64_t r1, int pitch, int64_t rows, uint16_t* hi, uint16_t* lo,
+                     float* inv, float* err, hipStream_t s);
 int launch_exact_select(const ExactArgs& a, hipStream_t s);
 int launch_split_rows(const float* src, int64_t r0, int64_t r1, int pitch, int64_t rows, uint16_t* hi, uint16_t* lo,
                       hipStream_t s);
@@ -184,6 +191,7 @@ struct CertArgs {
     int32_t* nflag;              // [1] out: list length
     unsigned long long* stats;   // [0] += uncertified queries
     const uint8_t* only;         // re-rank only rows with only[b] != 0 (nullable)
+    const float* xerr;           // fp16 2-product scores: max relative row rounding, added to the bound (nullable)
 };
 int launch_rerank(const float* Q, const GraphDev& g, const uint32_t* cand, int kk, int64_t B, int lpr, int vpl, int k,
                   int64_t* out_keys, float* out_dist, int32_t* out_n, int32_t* out_ids, const CertArgs& c,

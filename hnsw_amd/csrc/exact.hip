@@ -181,6 +181,79 @@ int launch_split_rows(const float* src, int64_t r0, int64_t r1, int pitch, int64
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// fp16 planes for the 2-product split (exact_precision 2): row r is scaled by
+// 2^e (max|x_i| 2^e in [2^14, 2^15), a power of two, so exact) and hi =
+// fp16(x 2^e); with `lo` also lo = fp16(x 2^e - hi) (queries: hi + lo carries
+// 22 bits).  inv[r] = 2^-e.  A row the error bound does not cover (a
+// non-finite value, or max|x_i| outside [2^-40, 2^40] and not 0) gets inv =
+// NaN: the GEMM epilogue scores it -inf, so a row is always preselected (and
+// re-ranked canonically) and a query always fails its certificate (and is
+// redone by the canonical sweep).  Same K-blocked layout as k_split_rows; one
+// wave per row.
+__global__ __launch_bounds__(256) void k_split_h16(const float* __restrict__ src, int64_t r0, int64_t r1, int pitch,
+                                                   int64_t rows, uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
+                                                   float* __restrict__ inv, float* __restrict__ err) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = r0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= r1) return;
+    const float* xp = src + row * (int64_t)pitch;
+    float m = 0.f;
+    bool fin = true;
+    for (int k = lane * 4; k < pitch; k += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(xp + k);
+        fin = fin && isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    fin = __ballot(!fin) == 0ull;
+    const bool ok = fin && (m == 0.f || (m >= 9.094947017729282e-13f && m <= 1.099511627776e12f));
+    int ex = 0;
+    if (ok && m > 0.f) {
+        int kx;
+        (void)frexpf(m, &kx);
+        ex = 15 - kx;
+    }
+    double e2 = 0.0, x2 = 0.0;  // |hi 2^-e - x|^2 and |x|^2, exact enough in f64
+    for (int k = lane * 4; k < pitch; k += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(xp + k);
+        const float w[4] = {ldexpf(v.x, ex), ldexpf(v.y, ex), ldexpf(v.z, ex), ldexpf(v.w, ex)};
+        const float xv[4] = {v.x, v.y, v.z, v.w};
+        uint16_t h[4], l[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const _Float16 hh = ok ? (_Float16)w[c] : (_Float16)0.f;
+            h[c] = __builtin_bit_cast(uint16_t, hh);
+            l[c] = __builtin_bit_cast(uint16_t, ok ? (_Float16)(w[c] - (float)hh) : (_Float16)0.f);
+            const double dv = ldexp((double)(float)hh, -ex) - (double)xv[c];
+            e2 = fma(dv, dv, e2);
+            x2 = fma((double)xv[c], (double)xv[c], x2);
+        }
+        const int64_t o = ((int64_t)(k / X3K) * rows + row) * X3K + (k % X3K);
+        *reinterpret_cast<uint2*>(hi + o) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+        if (lo) *reinterpret_cast<uint2*>(lo + o) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+    }
+    if (lane == 0) inv[row] = ok ? ldexpf(1.f, -ex) : __int_as_float(0x7fc00000);
+    if (err && ok) {  // the row's relative rounding |x' - x| / |x|, rounded up, into the running max
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            e2 += __shfl_xor(e2, o, 64);
+            x2 += __shfl_xor(x2, o, 64);
+        }
+        const float rel = x2 > 0.0 ? (float)(sqrt(e2 / x2) * (1.0 + 1e-6)) : 0.f;
+        if (lane == 0) atomicMax(reinterpret_cast<unsigned int*>(err), __float_as_uint(rel));
+    }
+}
+
+int launch_split_h16(const float* src, int64_t r0, int64_t r1, int pitch, int64_t rows, uint16_t* hi, uint16_t* lo,
+                     float* inv, float* err, hipStream_t s) {
+    if (r1 <= r0) return 0;
+    if (pitch % X3K || r1 > rows) return -5;
+    hipLaunchKernelGGL(k_split_h16, dim3((unsigned)((r1 - r0 + 3) / 4)), dim3(256), 0, s, src, r0, r1, pitch, rows, hi,
+                       lo, inv, err);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // largest row norm (NaN skipped) into *out (zeroed by the caller)
 __global__ __launch_bounds__(256) void k_max_norm(const float* __restrict__ norms, int64_t n, float* out) {
     float m = 0.f;
@@ -204,11 +277,12 @@ int launch_max_norm(const float* norms, int64_t n, float* out, hipStream_t s) {
 // rows x 16 bf16 (two 16-B chunks per row); chunk c of row r sits at chunk
 // position c ^ ((r >> 3) & 1), so the 16 consecutive rows one quarter of a
 // ds_read_b128 touches land in 16 distinct 16-B slots of the 256-B bank window.
-template <int WAVES_M, int WAVES_N, int TM, int TN>
+template <int WAVES_M, int WAVES_N, int TM, int TN, bool H2 = false>
 struct X3Tile {
     static constexpr int BM = WAVES_M * TM * 32, BN = WAVES_N * TN * 32;
     static constexpr int NT = 64 * WAVES_M * WAVES_N, NW = WAVES_M * WAVES_N;
-    static constexpr int STAGE = (BM + BN) * 2 * X3K;  // bf16 elements per stage
+    static constexpr int XPLANES = H2 ? 1 : 2;                    // H2: the rows' hi plane only
+    static constexpr int STAGE = (2 * BM + XPLANES * BN) * X3K;  // 16-bit elements per stage
     static constexpr int PIECES = STAGE * 2 / 1024;     // 1-KiB LDS-DMA pieces per stage
     static_assert(PIECES % NW == 0, "DMA split");
     static constexpr int PER = PIECES / NW;
@@ -253,6 +327,35 @@ __device__ __forceinline__ void x3_stage(const uint16_t* base, f32x16 (&acc)[TM]
         }
 }
 
+// H2 (fp16): q.x 2^(eq+ex) += ql.xh + qh.xh (the rows' rounding is the error term)
+template <class T, int TM, int TN>
+__device__ __forceinline__ void x2_stage(const uint16_t* base, f32x16 (&acc)[TM][TN], int wm, int wn, int li,
+                                         int lh) {
+    typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+    const uint16_t* Ah = base;
+    const uint16_t* Al = base + T::BM * X3K;
+    const uint16_t* Bh = base + 2 * T::BM * X3K;
+    f16x8 ah[TM], al[TM], bh[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int r = wm * TM * 32 + i * 32 + li;
+        ah[i] = __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4*>(Ah + swz16(r, lh)));
+        al[i] = __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4*>(Al + swz16(r, lh)));
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int r = wn * TN * 32 + j * 32 + li;
+        bh[j] = __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4*>(Bh + swz16(r, lh)));
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+}
+
 // Staged by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave instruction
 // straight into LDS -- no staging registers, no ds_write pass) into a ring of
 // four buffers, four separate __shared__ objects so the compiler's wait
@@ -264,9 +367,9 @@ __device__ __forceinline__ void x3_stage(const uint16_t* base, f32x16 (&acc)[TM]
 // re-reads the last K-block into a buffer nobody reads) so the in-flight count
 // is the same every step.  A lane's source chunk is pre-swizzled on the global
 // side so the linear LDS-DMA image matches swz16().
-template <int WAVES_M, int WAVES_N, int TM, int TN>
+template <int WAVES_M, int WAVES_N, int TM, int TN, bool H2>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_x3(ExactArgs a) {
-    using T = X3Tile<WAVES_M, WAVES_N, TM, TN>;
+    using T = X3Tile<WAVES_M, WAVES_N, TM, TN, H2>;
     __shared__ __attribute__((aligned(16))) uint16_t B0[T::STAGE];
     __shared__ __attribute__((aligned(16))) uint16_t B1[T::STAGE];
     __shared__ __attribute__((aligned(16))) uint16_t B2[T::STAGE];
@@ -316,7 +419,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_x3(ExactArgs 
             ld = a.ldQs;
         } else {
             const int I2 = I - apieces;
-            const int plane = I2 / (T::BN / 32);
+            const int plane = I2 / (T::BN / 32);  // H2: always 0
             r = (I2 % (T::BN / 32)) * 32 + (lane >> 1);
             base = plane ? a.Xl : a.Xh;
             row0 = n0;
@@ -335,6 +438,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_x3(ExactArgs 
 #pragma unroll
         for (int j = 0; j < T::PER; ++j) x3_dma(gp[j] + kb * gks[j], buf + lofs[j]);
     };
+    auto stage = [&](const uint16_t* buf) {
+        if constexpr (H2)
+            x2_stage<T, TM, TN>(buf, acc, wm, wn, li, lh);
+        else
+            x3_stage<T, TM, TN>(buf, acc, wm, wn, li, lh);
+    };
     // vmcnt(2*PER): this wave's pieces of the two newest stages stay in flight
     constexpr int NW2 = 2 * T::PER;
     constexpr int WAIT = (NW2 & 15) | ((NW2 >> 4) << 14) | (0x7 << 4) | (0xF << 8);
@@ -345,19 +454,19 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_x3(ExactArgs 
         __builtin_amdgcn_s_waitcnt(WAIT);
         __builtin_amdgcn_s_barrier();
         issue(B3, kt + 3);
-        x3_stage<T, TM, TN>(B0, acc, wm, wn, li, lh);
+        stage(B0);
         __builtin_amdgcn_s_waitcnt(WAIT);
         __builtin_amdgcn_s_barrier();
         issue(B0, kt + 4);
-        if (kt + 1 < nk) x3_stage<T, TM, TN>(B1, acc, wm, wn, li, lh);
+        if (kt + 1 < nk) stage(B1);
         __builtin_amdgcn_s_waitcnt(WAIT);
         __builtin_amdgcn_s_barrier();
         issue(B1, kt + 5);
-        if (kt + 2 < nk) x3_stage<T, TM, TN>(B2, acc, wm, wn, li, lh);
+        if (kt + 2 < nk) stage(B2);
         __builtin_amdgcn_s_waitcnt(WAIT);
         __builtin_amdgcn_s_barrier();
         issue(B2, kt + 6);
-        if (kt + 3 < nk) x3_stage<T, TM, TN>(B3, acc, wm, wn, li, lh);
+        if (kt + 3 < nk) stage(B3);
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no DMA may land after the workgroup ends
     // epilogue: D col = lane&31 (base row), row = (r&3) + 8*(r>>2) + 4*(lane>>5) (query)
@@ -368,39 +477,46 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_x3(ExactArgs 
         if (xr >= a.N) continue;
         const bool xok = !(a.dead && a.dead[xr]);
         const float xn = a.xnorm[xr];
+        const float xi = H2 ? a.xinv[xr] : 1.f;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int64_t qr = q0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
                 if (qr >= a.B) continue;
-                const float dot = acc[i][j][r];
+                const float qi = H2 ? a.qinv[qr] : 1.f;
+                const float dot = H2 ? acc[i][j][r] * xi * qi : acc[i][j][r];
                 const float qn = a.qnorm[qr];
                 float sc = a.metric == COSINE ? 1.0f - dot / (qn * xn) : fmaf(-2.f, dot, qn * qn + xn * xn);
-                if (!xok || !(sc == sc)) sc = inf;
+                if (!(sc == sc)) sc = inf;
+                if (H2 && !(xi == xi && qi == qi)) sc = -inf;  // outside the bound: always preselected / uncertified
+                if (!xok) sc = inf;
                 a.scores[(size_t)qr * a.ldS + xr] = sc;
             }
         }
     }
 }
 
-template <int WM_, int WN_, int TM_, int TN_>
+template <int WM_, int WN_, int TM_, int TN_, bool H2>
 static int launch_x3_t(const ExactArgs& a, hipStream_t s) {
-    using T = X3Tile<WM_, WN_, TM_, TN_>;
+    using T = X3Tile<WM_, WN_, TM_, TN_, H2>;
     const int64_t nqt = (a.B + T::BM - 1) / T::BM, nnt = (a.N + T::BN - 1) / T::BN;
-    hipLaunchKernelGGL((k_scores_x3<WM_, WN_, TM_, TN_>), dim3((unsigned)(nqt * nnt)), dim3(T::NT), 0, s, a);
+    hipLaunchKernelGGL((k_scores_x3<WM_, WN_, TM_, TN_, H2>), dim3((unsigned)(nqt * nnt)), dim3(T::NT), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_exact_scores_x3(const ExactArgs& a, int tile, hipStream_t s) {
+template <bool H2>
+static int launch_split_scores(const ExactArgs& a, int tile, hipStream_t s) {
     if (a.B <= 0 || a.N <= 0) return 0;
     if (a.pitch % X3K) return -5;
     switch (tile) {
-        case 1: return launch_x3_t<2, 4, 2, 2>(a, s);  // 128 x 256, 8 waves of 64 x 64
-        case 2: return launch_x3_t<2, 2, 2, 2>(a, s);  // 128 x 128, 4 waves of 64 x 64
-        default: return launch_x3_t<2, 4, 4, 2>(a, s);  // 256 x 256, 8 waves of 128 x 64
+        case 1: return launch_x3_t<2, 4, 2, 2, H2>(a, s);  // 128 x 256, 8 waves of 64 x 64
+        case 2: return launch_x3_t<2, 2, 2, 2, H2>(a, s);  // 128 x 128, 4 waves of 64 x 64
+        default: return launch_x3_t<2, 4, 4, 2, H2>(a, s);  // 256 x 256, 8 waves of 128 x 64
     }
 }
+int launch_exact_scores_x3(const ExactArgs& a, int tile, hipStream_t s) { return launch_split_scores<false>(a, tile, s); }
+int launch_exact_scores_x2h(const ExactArgs& a, int tile, hipStream_t s) { return launch_split_scores<true>(a, tile, s); }
 
 // ---------------------------------------------------------------------------
 // top-kk preselect per query row (one wave per query)
@@ -438,7 +554,9 @@ __global__ __launch_bounds__(64) void k_select(ExactArgs a) {
             for (int c = 0; c < 4; ++c) {
                 const int64_t e = base + u * 256 + lane * 4 + c;
                 const float x = e < hi ? vv[c] : inf;
-                unsigned long long m = __ballot(x < worst);
+                // <=: a row tying the kk-th score may still win on its id (rows
+                // arrive c-interleaved, not in id order); +inf never enters
+                unsigned long long m = __ballot(x <= worst && x < inf);
                 while (m) {
                     const int src = __ffsll((long long)m) - 1;
                     m &= m - 1;
@@ -486,12 +604,29 @@ __global__ __launch_bounds__(64) void k_select_merge(ExactArgs a) {
     __syncthreads();
     for (int e = lane; e < kk; e += 64) a.cand[b * kk + e] = EMPTY_ID;
     float kth = inf;
+    // every segment list is sorted by (score, id) with its empty slots (+inf,
+    // EMPTY_ID) at the tail: an entry's rank is its position in its own list
+    // plus, per other list, the length of the prefix ordered before it
     for (int e = lane; e < n; e += 64) {
         const uint32_t id = si[e];
         if (id == EMPTY_ID) continue;
         const float d = sd[e];
-        int rank = 0;
-        for (int f = 0; f < n; ++f) rank += (si[f] != EMPTY_ID && lt_di(sd[f], si[f], d, id)) ? 1 : 0;
+        const int s0 = e / kk;
+        int rank = e - s0 * kk;
+        for (int sg = 0; sg < a.nseg; ++sg) {
+            if (sg == s0) continue;
+            const float* ld = sd + sg * kk;
+            const uint32_t* li = si + sg * kk;
+            int lo = 0, hi = kk;  // first slot not ordered before (d, id)
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (li[mid] != EMPTY_ID && lt_di(ld[mid], li[mid], d, id))
+                    lo = mid + 1;
+                else
+                    hi = mid;
+            }
+            rank += lo;
+        }
         if (rank < kk) a.cand[b * kk + rank] = id;
         if (rank == kk - 1) kth = d;
     }
@@ -545,10 +680,12 @@ __global__ __launch_bounds__(64) void k_rerank(const float* __restrict__ Q, Grap
             if (ik == EMPTY_ID) {
                 cert = false;
             } else if (g.metric == COSINE) {
-                cert = (double)dk < (double)t - (double)c.eps_cos;
+                const double ex = c.xerr ? 1.01 * (1.0 + 1e-4) * (double)*c.xerr : 0.0;
+                cert = (double)dk < (double)t - (double)c.eps_cos - ex;
             } else {
                 const double qnd = c.qnorm[b], xm = *c.xmax;
-                const double delta = 2.0 * c.eps_dot * qnd * xm + c.c_l2 * (qnd + xm) * (qnd + xm);
+                const double ed = c.eps_dot + (c.xerr ? 1.01 * (double)*c.xerr : 0.0);
+                const double delta = 2.0 * ed * qnd * xm + c.c_l2 * (qnd + xm) * (qnd + xm);
                 cert = (double)dk * (double)dk < (double)t - delta;
             }
         }

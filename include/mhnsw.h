@@ -73,8 +73,9 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * 2 also when a reverse edge overflows a row), "keep_pruned", "prune_alpha_pct"
  * (heuristic slack x100: c is dropped when alpha*d(c,kept) < d(u,c); 100 = HNSW
  * Alg. 4), "batch_min", "batch_max", "batch_ratio_pct", "vis_log2", "exact_kk",
- * "exact_precision" (exact-mode scoring: 0 f32-input MFMA, 1 bf16x3 split MFMA;
- * both preselect, re-rank canonically and certify, so results are identical),
+ * "exact_precision" (exact-mode scoring: 0 f32-input MFMA, 1 bf16x3 split MFMA,
+ * 2 fp16 2-product split MFMA (default); all preselect, re-rank canonically and
+ * certify, so results are identical),
  * "exact_tile", "compat_waves" (1 or 8 waves scoring the compat insert's
  * distance batches), "upper_ef" (beam mode: upper-layer descent width, 1 =
  * greedy), "screen" (beam mode, default 1: keep an fp16 copy of the rows and

@@ -353,10 +353,11 @@ def _exact_inputs(rng, n, d, nq, metric):
     return X, Q
 
 
-@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("precision", [0, 1, 2])
 @pytest.mark.parametrize("metric,d", [(0, 24), (1, 24), (0, 768), (1, 768), (0, 1536), (1, 4096)])
 def test_exact_precision_parity(H, O, metric, d, precision):
-    """Exact mode with f32-input MFMA scores (0) and bf16x3 split scores (1):
+    """Exact mode with f32-input MFMA scores (0), bf16x3 split scores (1) and
+    fp16 2-product scores (2):
     after the canonical re-rank and the certificate (or its fallback) the
     output is the oracle's brute force bit for bit."""
     rng = np.random.default_rng(100 + d + metric)
@@ -386,7 +387,7 @@ def test_exact_precision_parity(H, O, metric, d, precision):
 
 @pytest.mark.parametrize("k", [65, 200, 256])
 def test_exact_large_k(H, O, k):
-    """k up to 256 (multi-row preselection / re-rank lists), both precisions."""
+    """k up to 256 (multi-row preselection / re-rank lists), every precision."""
     rng = np.random.default_rng(k)
     n, d = 3000, 48
     X, Q = _exact_inputs(rng, n, d, 40, 0)
@@ -395,7 +396,7 @@ def test_exact_large_k(H, O, k):
     o = O.Graph(metric=0, order=O.ORDER_DEV, M=8, M0=16, Ml=0.25, EfSearch=32)
     o.import_graph(**g.export())
     rk, rd, rn = o.search(Q, k, mode=O.MODE_EXACT)
-    for precision in (1, 0):
+    for precision in (2, 1, 0):
         g.set_option("exact_precision", precision)
         gk, gd, gn = g.search_arrays(Q, k, mode=H.MODE_EXACT)
         _same_results(gk, gd, gn, rk, rd, rn)
@@ -417,7 +418,7 @@ def test_exact_certificate_fallback(H, O, metric):
                 ef_construction=32)
     g.add_arrays(np.arange(n), X)
     g.set_option("exact_kk", 10)
-    for precision in (1, 0):
+    for precision in (2, 1, 0):
         g.set_option("exact_precision", precision)
         g.reset_stats()
         gk, gd, gn = g.search_arrays(Q, 10, mode=H.MODE_EXACT)
@@ -425,6 +426,40 @@ def test_exact_certificate_fallback(H, O, metric):
         o = O.Graph(metric=metric, order=O.ORDER_DEV, M=8, M0=16, Ml=0.25, EfSearch=32)
         o.import_graph(**g.export())
         rk, rd, rn = o.search(Q, 10, mode=O.MODE_EXACT)
+        _same_results(gk, gd, gn, rk, rd, rn)
+    g.close()
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_exact_h16_outside_bound(H, O, metric):
+    """fp16 2-product scores: rows outside the error bound's range (|x_i| up to
+    1e15 or down to 1e-15, an infinite component) are always preselected and
+    re-ranked canonically, queries outside it fail their certificate and are
+    redone by the canonical sweep -- results still the oracle's brute force."""
+    rng = np.random.default_rng(31 + metric)
+    n, d = 2000, 64
+    X, Q = _exact_inputs(rng, n, d, 48, metric)
+    X[100] *= np.float32(1e15)
+    X[101] *= np.float32(1e-15)
+    X[102] *= np.float32(2.0 ** 39)                # inside the range, near its edges
+    X[103] *= np.float32(2.0 ** -39)
+    X[104, 3] = np.inf
+    Q[5] *= np.float32(1e15)
+    Q[6] *= np.float32(1e-15)
+    Q[7] = X[101]                                 # finds the tiny row
+    g = H.Graph(M=8, Ml=0.25, EfSearch=32, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_FLAT)
+    g.add_arrays(np.arange(n), X)
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=8, M0=16, Ml=0.25, EfSearch=32)
+    o.import_graph(**g.export())
+    rk, rd, rn = o.search(Q, 10, mode=O.MODE_EXACT)
+    # every precision; the huge query's L2 distances all tie in f32, so its top-k
+    # is decided by ids alone (the preselection must admit rows tying its bound)
+    for precision in (2, 1, 0):
+        g.set_option("exact_precision", precision)
+        g.reset_stats()
+        gk, gd, gn = g.search_arrays(Q, 10, mode=H.MODE_EXACT)
+        if precision == 2:
+            assert g.stats()["exact_uncertified"] >= 2     # the two out-of-range queries
         _same_results(gk, gd, gn, rk, rd, rn)
     g.close()
 

@@ -88,7 +88,7 @@ if "5" in which:
     S = Searcher(g, B, 10, d, dev)
     flops = 2.0 * B * n * d
     res = {}
-    for prec, name in ((0, "f32"), (1, "bf16x3")):
+    for prec, name in ((0, "f32"), (1, "bf16x3"), (2, "fp16x2")):
         g.set_option("exact_precision", prec)
         S.run(Q, H.MODE_EXACT, 0)
         g.reset_stats()
@@ -102,8 +102,8 @@ if "5" in which:
                           "fp32_equiv_tflops_end_to_end": round(flops / dt / 1e12, 1),
                           "uncertified_per_batch": unc, "mfma_f32_peak_tflops": 157.3,
                           "mfma_bf16_dense_peak_tflops": 2500.0, "recall": 1.0}), flush=True)
-    same = all(torch.equal(a_, b_) for a_, b_ in zip(res["f32"], res["bf16x3"]))
-    print(json.dumps({"config": "configs[4] exact: f32 vs bf16x3 results", "identical": same}), flush=True)
+    same = all(torch.equal(a_, b_) for other in ("bf16x3", "fp16x2") for a_, b_ in zip(res["f32"], res[other]))
+    print(json.dumps({"config": "configs[4] exact: f32 vs bf16x3 vs fp16x2 results", "identical": same}), flush=True)
     g.close()
     del X
 
