@@ -509,6 +509,8 @@ template <bool H2>
 static int launch_split_scores(const ExactArgs& a, int tile, hipStream_t s) {
     if (a.B <= 0 || a.N <= 0) return 0;
     if (a.pitch % X3K) return -5;
+    // tile 0: the measured best per split (config 5: bf16x3 256 x 256, fp16 128 x 256)
+    if (tile == 0) tile = H2 ? 1 : 3;
     switch (tile) {
         case 1: return launch_x3_t<2, 4, 2, 2, H2>(a, s);  // 128 x 256, 8 waves of 64 x 64
         case 2: return launch_x3_t<2, 2, 2, 2, H2>(a, s);  // 128 x 128, 4 waves of 64 x 64

@@ -76,7 +76,8 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * "exact_precision" (exact-mode scoring: 0 f32-input MFMA, 1 bf16x3 split MFMA,
  * 2 fp16 2-product split MFMA (default); all preselect, re-rank canonically and
  * certify, so results are identical),
- * "exact_tile", "compat_waves" (1 or 8 waves scoring the compat insert's
+ * "exact_tile" (split GEMM tile: 0 best measured per split, 1 128x256, 2 128x128,
+ * 3 256x256), "compat_waves" (1 or 8 waves scoring the compat insert's
  * distance batches), "upper_ef" (beam mode: upper-layer descent width, 1 =
  * greedy), "screen" (beam mode, default 1: keep an fp16 copy of the rows and
  * skip candidates it proves the f32 distance rejects; results unchanged);

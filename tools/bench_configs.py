@@ -117,11 +117,14 @@ if "5t" in which:  # bf16x3 GEMM tile variants (exact_tile option), same workloa
     g.reserve(n, d)
     g.add_device(np.arange(n), X.data_ptr(), n, d)
     S = Searcher(g, B, 10, d, dev)
-    for tile in (1, 2):
-        g.set_option("exact_tile", tile)
-        S.run(Q, H.MODE_EXACT, 0)
-        dt, _ = timed(lambda: S.run(Q, H.MODE_EXACT, 0), reps=5)
-        print(json.dumps({"exact_tile": tile, "ms_per_batch": round(dt * 1e3, 3)}), flush=True)
+    for prec in (1, 2):
+        g.set_option("exact_precision", prec)
+        for tile in (1, 2, 3):
+            g.set_option("exact_tile", tile)
+            S.run(Q, H.MODE_EXACT, 0)
+            dt, _ = timed(lambda: S.run(Q, H.MODE_EXACT, 0), reps=5)
+            print(json.dumps({"exact_precision": prec, "exact_tile": tile, "ms_per_batch": round(dt * 1e3, 3)}),
+                  flush=True)
     g.close()
     del X
 
