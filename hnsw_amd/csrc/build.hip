@@ -83,9 +83,9 @@ __device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw, co
 
 // graph.go:172-219.  The neighbours' rows and keys are staged in LDS in one
 // pass (instead of one dependent load chain per neighbour); the candidates are
-// then walked in the reference's order (neighbours, then their neighbours, both
-// in ascending key order -- the map-order stand-in), recorded in the visited
-// set and collected, and ONE distance batch scores them all; the heap sees the
+// then collected in the reference's walk order (neighbours, then their
+// neighbours, both in ascending key order -- the map-order stand-in) for all
+// rows at once, and ONE distance batch scores them all; the heap sees the
 // pushes in the same order as a per-neighbour loop would produce.
 template <class C, int G, class Ev>
 __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err,
@@ -95,10 +95,6 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
     int dn = ld_i32<true>(g.layers[l].deg + n);
     if (dn < 0) dn = 0;
     if (dn >= m) return;
-    const int vsize = 1 << S.cs.vlog2, vmask = vsize - 1;
-    vis_clear(S.cs.vis, vsize);
-    ev.sync();
-    if (lane == 0) vis_probe(S.cs.vis, vmask, n);  // graph.go:184
     uint32_t mine = 0xFFFFFFFFu;
     int64_t key = INT64_MAX;
     if (lane < dn) {
@@ -106,7 +102,6 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
         key = g.keys[mine];
     }
     rank_sort(key, mine, dn);
-    if (lane < dn) vis_probe(S.cs.vis, vmask, mine);  // graph.go:187-189
     // stage every neighbour's row (deg, entries, keys) -- rows j < dn, j-major
     const int mydeg = lane < dn ? min(ld_i32<true>(g.layers[l].deg + mine), capl) : -1;
     const int tot = min(dn * capl, S.hcap);
@@ -127,23 +122,52 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
         }
     }
     ev.sync();
-    // the reference's walk: visited bookkeeping and the candidate list, in order
-    int ncand = 0;
-    for (int j = 0; j < dn; ++j) {  // graph.go:192-210
-        const int dnb = __shfl(mydeg, j, 64);
-        if (dnb < 0) continue;
-        uint32_t th = 0xFFFFFFFFu;
-        int64_t tk = INT64_MAX;
-        if (lane < dnb && j * capl + lane < S.hcap) {
-            th = S.radj[j * capl + lane];
-            tk = S.rkey[j * capl + lane];
+    // The reference's walk (graph.go:184-210): visited = {n} + n's neighbours;
+    // then each neighbour j in key order, each of its neighbours in key order,
+    // collecting the ones not yet visited.  All rows at once: (1) every entry's
+    // rank in its row's key order gives its walk position j*capl + rank in
+    // S.hi (EMPTY past the row's degree); (2) a walk entry is collected when it
+    // is not n, not one of n's neighbours and not seen at an earlier position.
+    uint32_t* W = S.hi;
+    for (int e0 = 0; e0 < tot; e0 += 64) {  // uniform trip count for the shuffle
+        const int e = e0 + lane;
+        const int j = min(e / capl, 63), i = e % capl;
+        const int dj = __shfl(mydeg, j, 64);
+        if (e < tot) {
+            const uint32_t v = S.radj[e];
+            const int64_t kv = S.rkey[e];
+            const int row = j * capl;
+            if (i < dj) {
+                int r = 0;
+                for (int i2 = 0; i2 < dj && row + i2 < tot; ++i2) {
+                    const int64_t k2 = S.rkey[row + i2];
+                    const uint32_t v2 = S.radj[row + i2];
+                    r += (k2 < kv || (k2 == kv && (v2 < v || (v2 == v && i2 < i)))) ? 1 : 0;
+                }
+                W[row + r] = v;
+            } else {
+                W[e] = EMPTY_ID;
+            }
         }
-        rank_sort(tk, th, max(0, min(dnb, S.hcap - j * capl)));
+    }
+    ev.sync();
+    const int vsize = 1 << S.cs.vlog2, vmask = vsize - 1;
+    vis_clear(S.cs.vis, vsize);
+    ev.sync();
+    if (lane == 0) vis_probe(S.cs.vis, vmask, n);     // graph.go:184
+    if (lane < dn) vis_probe(S.cs.vis, vmask, mine);  // graph.go:187-189
+    ev.sync();
+    int ncand = 0;
+    for (int e0 = 0; e0 < tot; e0 += 64) {  // 64 walk positions at a time, in order
+        const int e = e0 + lane;
+        const uint32_t v = e < tot ? W[e] : EMPTY_ID;
+        bool first = v != EMPTY_ID;  // not repeated at a lower lane of this chunk
+        for (int l2 = 0; l2 < 63; ++l2) first = first && !(l2 < lane && rl_u(v, l2) == v);
         int pr = 0;
-        if (lane < dnb) pr = vis_probe(S.cs.vis, vmask, th);
+        if (first) pr = vis_probe(S.cs.vis, vmask, v);  // earlier chunks and the pre-visited set
         if (__ballot(pr == 2)) err = 1;
         int cnt;
-        const uint32_t cid = compact(th, pr == 1, cnt);
+        const uint32_t cid = compact(v, pr == 1, cnt);
         if (ncand + cnt > S.hcap) {
             err |= 8;
             cnt = S.hcap - ncand;
