@@ -42,18 +42,21 @@ struct BuildSmem {
     int64_t* rkey;   // ... and their keys
 };
 
+// Rows are loaded together with their degree (one round trip; entries past
+// the degree are ignored): the sequential walk is bound by dependent loads.
 template <class C, int G, class Ev>
 __device__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v, const Ev& ev) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
     int32_t* row = g.layers[l].adj + (size_t)n * capl;
+    const int32_t rv = lane < capl ? ld_i32<true>(row + lane) : -1;
     const int d = ld_i32<true>(g.layers[l].deg + n);
     if (d <= 0) return;
-    const bool hit = lane < d && (uint32_t)ld_i32<true>(row + lane) == v;
+    const bool hit = lane < d && (uint32_t)rv == v;
     const unsigned long long m = __ballot(hit);
     if (!m) return;
     const int pos = __ffsll((long long)m) - 1;
-    const int32_t last = ld_i32<true>(row + d - 1);
+    const int32_t last = __shfl(rv, d - 1, 64);
     ev.sync();
     if (lane == 0) {
         st_i32(row + pos, last);
@@ -62,15 +65,18 @@ __device__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v, co
     ev.sync();
 }
 
-// append nw to n's neighbour set if absent; returns the new degree
+// append nw to n's neighbour set if absent; returns the new degree and, in
+// *rowout (nullable), the row after the append (lane i: entry i)
 template <class Ev>
-__device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw, const Ev& ev) {
+__device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw, const Ev& ev,
+                           int32_t* rowout = nullptr) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
     int32_t* row = g.layers[l].adj + (size_t)n * capl;
+    const int32_t rv = lane < capl ? ld_i32<true>(row + lane) : -1;
     int d = ld_i32<true>(g.layers[l].deg + n);
     if (d < 0) d = 0;  // graph.go:46-48 allocate the map
-    const bool pres = lane < d && (uint32_t)ld_i32<true>(row + lane) == nw;
+    const bool pres = lane < d && (uint32_t)rv == nw;
     const bool present = __ballot(pres) != 0;
     ev.sync();
     if (lane == 0) {
@@ -78,6 +84,7 @@ __device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw, co
         st_i32(g.layers[l].deg + n, present ? d : d + 1);
     }
     ev.sync();
+    if (rowout) *rowout = (!present && lane == d) ? (int32_t)nw : rv;
     return present ? d : d + 1;
 }
 
@@ -92,13 +99,14 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
                           const Ev& ev) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
+    const int32_t rv = lane < capl ? ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane) : -1;
     int dn = ld_i32<true>(g.layers[l].deg + n);
     if (dn < 0) dn = 0;
     if (dn >= m) return;
     uint32_t mine = 0xFFFFFFFFu;
     int64_t key = INT64_MAX;
     if (lane < dn) {
-        mine = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane));
+        mine = guard_id(g, (uint32_t)rv);
         key = g.keys[mine];
     }
     rank_sort(key, mine, dn);
@@ -109,11 +117,13 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
         const int e = e0 + lane;
         const int j = min(e / capl, 63), i = e % capl;
         const uint32_t nb = shfl_u(mine, j);
+        // the entry load goes out before the degree is needed (masked below)
+        const int32_t ev_ = e < tot && j < dn ? ld_i32<true>(g.layers[l].adj + (size_t)nb * capl + i) : -1;
         const int dj = __shfl(mydeg, j, 64);
         uint32_t th = 0xFFFFFFFFu;
         int64_t tk = INT64_MAX;
         if (e < tot && i < dj) {
-            th = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)nb * capl + i));
+            th = guard_id(g, (uint32_t)ev_);
             tk = g.keys[th];
         }
         if (e < tot) {
@@ -271,13 +281,13 @@ template <class C, int G, class Ev>
 __device__ void add_neighbor(const GraphDev& g, int l, uint32_t n, uint32_t nw, int m, BuildSmem& S, WaveStats& st,
                              int& err, const Ev& ev) {
     const int lane = lane_id();
-    const int capl = g.layers[l].cap;
-    const int d = list_append(g, l, n, nw, ev);
+    int32_t rv;
+    const int d = list_append(g, l, n, nw, ev, &rv);
     if (d <= m) return;
     uint32_t nb = 0xFFFFFFFFu;
     int64_t key = INT64_MAX;
     if (lane < d) {
-        nb = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane));
+        nb = guard_id(g, (uint32_t)rv);
         key = g.keys[nb];
     }
     rank_sort(key, nb, d);  // Go map order -> ascending key

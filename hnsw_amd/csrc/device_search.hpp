@@ -265,14 +265,17 @@ __device__ __forceinline__ int compat_layer(const GraphDev& g, int layer, uint32
         uint32_t cur;
         gh_pop(cand, cdist, cur);  // graph.go:127
         bool improved = false;
-        const int deg = min(ld_i32<COH>(degp + guard_id(g, cur)), capl);
+        const uint32_t cg = guard_id(g, cur);
+        // the row is loaded with its degree (one round trip, entries past deg ignored)
+        const int32_t rowv = lane < capl ? ld_i32<COH>(adjp + (size_t)cg * capl + lane) : -1;
+        const int deg = min(ld_i32<COH>(degp + cg), capl);
         if (deg < 0) continue;  // graph.go:131-133 (nil neighbor map)
         st.X += 1;
         const bool have = lane < deg;
         uint32_t nb = 0xFFFFFFFFu;
         int64_t key = INT64_MAX;
         if (have) {
-            nb = guard_id(g, (uint32_t)ld_i32<COH>(adjp + (size_t)cur * capl + lane));
+            nb = guard_id(g, (uint32_t)rowv);
             key = g.keys[nb];
         }
         rank_sort(key, nb, deg);  // graph.go:137-138 ascending key order
