@@ -16,7 +16,9 @@
             vs the oracle on one host core, recall of compat and beam search.
   2b      : the headline graph (bench.py defaults) searched at batch 1, 1024,
             10000 and 65536 (SURVEY 8(d) C2 batch sizes): latency and QPS.
-Usage: python tools/bench_configs.py [1] [2b] [3] [5] [4] [4m] [compat]"""
+  2u      : SURVEY 8(d) C2 stress set: 1M x 768 U[-1,1) cosine, same build
+            parameters, recall@10 and QPS per ef in {32, 64, 128, 256}.
+Usage: python tools/bench_configs.py [1] [2b] [2u] [3] [5] [4] [4m] [compat]"""
 import json
 import os
 import sys
@@ -292,4 +294,25 @@ if "2b" in which:
         dt, _ = timed(lambda: S.run(Q[:B], H.MODE_BEAM, 64), reps=reps)
         print(json.dumps({"config": "configs[1] 1M x 768 cosine ef=64 k=10, batch sweep", "batch": B,
                           "ms_per_batch": round(dt * 1e3, 4), "queries_per_s": round(B / dt, 1)}), flush=True)
+    g.close()
+
+if "2u" in which:
+    n, d, B, NGT = 1_000_000, 768, 65536, 4096
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(42)
+    X = (torch.rand(n, d, generator=gen, device=dev) * 2 - 1).contiguous()
+    Q = (torch.rand(B, d, generator=gen, device=dev) * 2 - 1).contiguous()
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=1234, build_mode=H.BUILD_BATCH, m0=40,
+                ef_construction=400, heuristic=2, keep_pruned=1, prune_alpha_pct=115)
+    g.reserve(n, d)
+    bt, _ = timed(lambda: g.add_device(np.arange(n), X.data_ptr(), n, d))
+    del X
+    tk, td, tn = (x.clone() for x in Searcher(g, NGT, 10, d, dev).run(Q[:NGT], H.MODE_EXACT, 0))
+    S = Searcher(g, B, 10, d, dev)
+    for ef in (32, 64, 128, 256):
+        k_, _, n_ = (x.clone() for x in S.run(Q, H.MODE_BEAM, ef))
+        dt, _ = timed(lambda: S.run(Q, H.MODE_BEAM, ef), reps=3)
+        print(json.dumps({"config": "configs[1] stress: 1M x 768 U[-1,1) cosine (no neighbour structure)",
+                          "build_s": round(bt, 1), "ef": ef, "recall_at_10": round(recall_at_k(k_[:NGT], n_[:NGT], tk, tn, 10), 4),
+                          "qps": round(B / dt, 1)}), flush=True)
     g.close()
