@@ -12,18 +12,23 @@
 
 namespace mh {
 
-// Loads of mutable graph state.  COH = true inside the single-workgroup build
-// kernel, which rewrites adjacency while searching: relaxed atomics keep the
-// compiler off the (incoherent) scalar cache; __syncthreads orders lanes.
+// Loads of mutable graph state.  COH = true inside the sequential build /
+// delete kernels, which rewrite adjacency while searching: relaxed atomics
+// keep the compiler off the (incoherent) scalar cache.  Only one wave ever
+// reads or writes graph state there (the multi-wave build's workers score
+// immutable rows), so wavefront scope suffices -- and it keeps the loads in
+// the vector L1 (workgroup scope would add sc0, sending every dependent load
+// of the walk to L2); the wave's own program order and __syncthreads /
+// ev.sync() order its lanes.
 template <bool COH>
 __device__ __forceinline__ int32_t ld_i32(const int32_t* p) {
     if constexpr (COH)
-        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     else
         return *p;
 }
 __device__ __forceinline__ void st_i32(int32_t* p, int32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
 // Evaluate the distances of candidate ids held in lanes 0..cnt-1 of `cid`
