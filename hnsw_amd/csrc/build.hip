@@ -149,6 +149,7 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
             const int row = j * capl;
             if (i < dj) {
                 int r = 0;
+#pragma unroll 8
                 for (int i2 = 0; i2 < dj && row + i2 < tot; ++i2) {
                     const int64_t k2 = S.rkey[row + i2];
                     const uint32_t v2 = S.radj[row + i2];
@@ -172,6 +173,7 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
         const int e = e0 + lane;
         const uint32_t v = e < tot ? W[e] : EMPTY_ID;
         bool first = v != EMPTY_ID;  // not repeated at a lower lane of this chunk
+#pragma unroll 9
         for (int l2 = 0; l2 < 63; ++l2) first = first && !(l2 < lane && rl_u(v, l2) == v);
         int pr = 0;
         if (first) pr = vis_probe(S.cs.vis, vmask, v);  // earlier chunks and the pre-visited set

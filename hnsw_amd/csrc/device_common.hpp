@@ -524,6 +524,7 @@ __device__ __forceinline__ void rank_sort(int64_t& key, uint32_t& id, int cnt) {
     const int lane = lane_id();
     const uint32_t klo = (uint32_t)(uint64_t)key, khi = (uint32_t)((uint64_t)key >> 32);
     int r = 0;
+#pragma unroll 8
     for (int j = 0; j < cnt; ++j) {
         const int64_t kj = (int64_t)(((uint64_t)rl_u(khi, j) << 32) | rl_u(klo, j));
         const uint32_t ij = rl_u(id, j);
