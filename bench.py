@@ -57,7 +57,8 @@ def parse():
     p.add_argument("--keep-pruned", type=int, default=1)
     p.add_argument("--alpha", type=int, default=115, help="heuristic slack x100 (prune_alpha_pct; 100 = HNSW Alg. 4)")
     p.add_argument("--screen", type=int, default=1,
-                   help="fp16 screening copy (1) or plain f32 evaluation of every candidate (0); same results")
+                   help="screening copies, bit 0 fp16, bit 1 int8 (0: plain f32 evaluation of every "
+                        "candidate); same results")
     p.add_argument("--ef-sweep", default="32,48,64,72,80,96,128,256",
                    help="extra operating points (ef values) reported at N=1; '' disables")
     p.add_argument("--seed", type=int, default=1234)
@@ -242,10 +243,13 @@ def main():
         # one adjacency row per expansion, the query
         E = stats["search_dist_evals"] / launches
         Sc = stats["search_screened"] / launches
+        S8 = stats.get("search_screened_i8", 0) / launches
         F = stats["search_f32_evals"] / launches
         Xp = stats["search_expansions"] / launches
         aux = 8 if a.metric == "euclidean" else 0  # L2 screening reads {unscale, |x|} per row
-        return F * (4 * a.dim + 4) + Sc * (2 * a.dim + aux) + Xp * 4 * cap0 + a.batch * 4 * a.dim, E, Xp, Sc, F
+        # int8 stage: one byte per dimension + {scale, bound} per screened candidate
+        return (F * (4 * a.dim + 4) + Sc * (2 * a.dim + aux) + S8 * (a.dim + 8) + Xp * 4 * cap0
+                + a.batch * 4 * a.dim, E, Xp, Sc, F)
 
     alg_bytes, E, Xp, Sc, F = alg_bytes_of(st, a.steps)
     kms = float(np.mean(kernel_ms))
@@ -304,8 +308,9 @@ def main():
             "n_base": a.nbase * (world if shard else 1), "dim": a.dim, "batch_per_gpu": a.batch, "ef": a.ef,
             "k": a.k, "M": a.M, "M0": a.M0, "ef_construction": a.efc, "keep_pruned": a.keep_pruned,
             "prune_alpha": a.alpha / 100,
-            "screen": ("fp16 row copy rejects candidates whose f32 distance provably exceeds the list's worst; "
-                       "every reported distance is f32, results identical to screen=0") if a.screen else "off",
+            "screen": ((["", "fp16", "int8", "int8 then fp16"][a.screen]
+                        + " row copy rejects candidates whose f32 distance provably exceeds the list's worst; "
+                        "every reported distance is f32, results identical to screen=0") if a.screen else "off"),
             "parallelism": f"{'shard' if shard else 'replica'}{world}",
         },
         "recall_at_10": round(recall, 4),
@@ -316,6 +321,7 @@ def main():
             "alg_bytes_per_launch": int(alg_bytes),
             "dist_evals_per_query": round(E / a.batch, 1), "expansions_per_query": round(Xp / a.batch, 1),
             "screened_per_query": round(Sc / a.batch, 1), "f32_evals_per_query": round(F / a.batch, 1),
+            "int8_screened_per_query": round(st.get("search_screened_i8", 0) / a.steps / a.batch, 1),
         },
         "build": {"inserts_per_s": round(a.nbase / build_s, 1), "seconds": round(build_s, 2),
                   "dist_evals_per_insert": round(bstats["build_dist_evals"] / a.nbase, 1),

@@ -67,7 +67,7 @@ struct mhnsw_index {
     int exact_tile = 0;       // bf16x3 GEMM tile variant (exact.hip launch_exact_scores_x3)
     int compat_waves = 8;     // compat insert: waves scoring each distance batch (1 = the walking wave alone)
     int upper_ef = 1;         // beam search: upper-layer descent width
-    int screen = 1;           // beam search: fp16 screening copy of the rows (results unchanged)
+    int screen = 1;           // beam search screening copies (results unchanged): bit 0 fp16, bit 1 int8
     int fuse_descent = 1;     // batched insert: all greedy descents of a batch in one launch (same graph)
     // shape
     int dim = 0, pitch = 0, lpr = 0, vpl = 0;
@@ -80,7 +80,9 @@ struct mhnsw_index {
     float* norms = nullptr;
     uint16_t* h16 = nullptr;  // fp16 screening copy [capn * pitch] (screen = 1)
     float2* h16aux = nullptr;  // [capn] L2 screening {unscale, |x|}
-    int h16_metric = -1;       // metric the copy was written for
+    int h16_metric = -1;       // metric the copies were written for
+    int8_t* i8 = nullptr;      // int8 screening copy [capn * pitch] (screen bit 1)
+    float2* i8aux = nullptr;   // [capn] {scale, |error| bound}
     int64_t* keys = nullptr;
     int32_t* levels = nullptr;
     uint8_t* dead = nullptr;  // [capn] deleted rows (graph.go:843-864)
@@ -301,9 +303,13 @@ int ensure_capacity(mhnsw_index* h, int64_t need) {
     int r;
     if ((r = grow(h, h->vecs, oc * h->pitch, nc * h->pitch, 0))) return r;
     if ((r = grow(h, h->norms, oc, nc, 0))) return r;
-    if (h->screen) {
+    if (h->screen & 1) {
         if ((r = grow(h, h->h16, oc * h->pitch, nc * h->pitch, 0))) return r;
         if ((r = grow(h, h->h16aux, oc, nc, 0xFF))) return r;
+    }
+    if (h->screen & 2) {
+        if ((r = grow(h, h->i8, oc * h->pitch, nc * h->pitch, 0))) return r;
+        if ((r = grow(h, h->i8aux, oc, nc, 0xFF))) return r;
     }
     if ((r = grow(h, h->keys, oc, nc, 0))) return r;
     if ((r = grow(h, h->levels, oc, nc, 0))) return r;
@@ -354,9 +360,11 @@ GraphDev graph_view(const mhnsw_index* h) {
     g.capn = (uint32_t)std::max<int64_t>(h->capn, 1);
     g.err = h->d_err;
     g.dead = h->any_dead ? h->dead : nullptr;
-    g.h16 = h->screen ? h->h16 : nullptr;
+    g.h16 = (h->screen & 1) ? h->h16 : nullptr;
     g.h16aux = h->h16aux;
-    if (h->h16_metric != h->metric) g.h16 = nullptr;  // stale format: no screening
+    g.i8 = (h->screen & 2) ? h->i8 : nullptr;
+    g.i8aux = h->i8aux;
+    if (h->h16_metric != h->metric) g.h16 = nullptr, g.i8 = nullptr;  // stale format: no screening
     return g;
 }
 
@@ -573,9 +581,12 @@ int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1, int top, uint32_t en
 
 // (re)write the fp16 screening copy of rows [r0, r1) for the current metric
 int h16_rows(mhnsw_index* h, int64_t r0, int64_t r1) {
-    if (!h->screen || !h->h16) return 0;
+    if (!(h->screen & 1 && h->h16) && !(h->screen & 2 && h->i8)) return 0;
     if (h->h16_metric != h->metric && r0 > 0) r0 = 0;  // format change: every row
-    LCHK(h, launch_h16_rows(h->vecs, h->norms, r0, r1, h->pitch, h->metric, h->h16, h->h16aux, h->stream));
+    if (h->screen & 1 && h->h16)
+        LCHK(h, launch_h16_rows(h->vecs, h->norms, r0, r1, h->pitch, h->metric, h->h16, h->h16aux, h->stream));
+    if (h->screen & 2 && h->i8)
+        LCHK(h, launch_i8_rows(h->vecs, h->norms, r0, r1, h->pitch, h->metric, h->i8, h->i8aux, h->stream));
     h->h16_metric = h->metric;
     return 0;
 }
@@ -1006,6 +1017,8 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->norms);
     F(h->h16);
     F(h->h16aux);
+    F(h->i8);
+    F(h->i8aux);
     F(h->keys);
     F(h->levels);
     F(h->dead);
@@ -1138,20 +1151,26 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
         if (v != 0 && v != 1) return fail(h, MHNSW_EINVAL, "fuse_descent must be 0 or 1");
         h->fuse_descent = (int)v;
     } else if (n == "screen") {
-        if (v != 0 && v != 1) return fail(h, MHNSW_EINVAL, "screen must be 0 or 1");
+        if (v < 0 || v > 3) return fail(h, MHNSW_EINVAL, "screen must be in [0, 3]");
         if ((int)v == h->screen) return MHNSW_OK;
         int r = drain(h);
         if (r) return r;
         HIPCHK(h, hipStreamSynchronize(h->stream));
+        auto F = [](auto*& p) {
+            if (p) (void)hipFree(p);
+            p = nullptr;
+        };
+        F(h->h16);
+        F(h->h16aux);
+        F(h->i8);
+        F(h->i8aux);
+        h->h16_metric = -1;
         h->screen = (int)v;
-        if (!v) {
-            (void)hipFree(h->h16);
-            (void)hipFree(h->h16aux);
-            h->h16 = nullptr;
-            h->h16aux = nullptr;
-            h->h16_metric = -1;
-        } else if (h->capn > 0) {
-            if ((r = grow(h, h->h16, 0, h->capn * h->pitch, 0)) || (r = grow(h, h->h16aux, 0, h->capn, 0xFF))) return r;
+        if (v && h->capn > 0) {  // rewrite the selected copies
+            if (v & 1 && ((r = grow(h, h->h16, 0, h->capn * h->pitch, 0)) || (r = grow(h, h->h16aux, 0, h->capn, 0xFF))))
+                return r;
+            if (v & 2 && ((r = grow(h, h->i8, 0, h->capn * h->pitch, 0)) || (r = grow(h, h->i8aux, 0, h->capn, 0xFF))))
+                return r;
             if ((r = h16_rows(h, 0, h->n))) return r;
             HIPCHK(h, hipStreamSynchronize(h->stream));
         }
@@ -1341,6 +1360,8 @@ void reset_graph(mhnsw_index* h) {
     F(h->norms);
     F(h->h16);
     F(h->h16aux);
+    F(h->i8);
+    F(h->i8aux);
     F(h->keys);
     F(h->levels);
     F(h->dead);
@@ -1919,9 +1940,9 @@ int mhnsw_stats(const mhnsw_index* h, int64_t* out, int n) {
     int err = 0;
     HIPCHK(hh, hipMemcpy(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (err & 4) return fail(hh, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
-    const int64_t v[10] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4], (int64_t)d[5],
-                           (int64_t)d[6], h->stats_host[6], (int64_t)d[3], (int64_t)d[8], (int64_t)d[9]};
-    for (int i = 0; i < n && i < 10; ++i) out[i] = v[i];
+    const int64_t v[11] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4], (int64_t)d[5], (int64_t)d[6],
+                           h->stats_host[6], (int64_t)d[3], (int64_t)d[8], (int64_t)d[9], (int64_t)d[10]};
+    for (int i = 0; i < n && i < 11; ++i) out[i] = v[i];
     return 0;
 }
 

@@ -979,7 +979,7 @@ static int launch_batch_descend_t(const BatchBuildArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 << a.vis_log2;
     const int64_t n = a.n1 - a.n0;
     if (n <= 0) return 0;
-    if (a.g.h16)
+    if (a.g.h16 || a.g.i8)
         hipLaunchKernelGGL((k_batch_descend<C, G, true>), dim3((unsigned)n), dim3(64), lds, s, a);
     else
         hipLaunchKernelGGL((k_batch_descend<C, G, false>), dim3((unsigned)n), dim3(64), lds, s, a);
@@ -991,7 +991,7 @@ static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 << a.vis_log2;
     const int64_t n = a.order ? a.count : a.n1 - a.n0;
     if (n <= 0) return 0;
-    if (a.g.h16)  // fp16 screening: same graph, fewer bytes per candidate
+    if (a.g.h16 || a.g.i8)  // fp16 screening: same graph, fewer bytes per candidate
         hipLaunchKernelGGL((k_batch_search<C, R, G, true>), dim3((unsigned)n), dim3(64), lds, s, a);
     else
         hipLaunchKernelGGL((k_batch_search<C, R, G, false>), dim3((unsigned)n), dim3(64), lds, s, a);

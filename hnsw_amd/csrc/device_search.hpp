@@ -79,6 +79,57 @@ __device__ __forceinline__ uint32_t compact(uint32_t v, bool keep, int& cnt) {
     return push_to(v, dst);
 }
 
+// int8 stage of the screen: drops candidates whose int8 screening distance
+// proves the f32 distance exceeds wd; returns the compacted survivors (cnt
+// updated).  2G rows per pass, as the fp16 stage (register budget).
+template <class C, int G>
+__device__ __forceinline__ uint32_t screen_i8(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int& cnt,
+                                              int metric, float wd) {
+    constexpr int GI = (2 * G <= C::LPR) ? 2 * G : G;
+    using RM = RowMap<C, GI>;
+    const int lane = lane_id();
+    bool rej = false;  // lane t: candidate t is rejected
+    for (int base = 0; base < cnt; base += RM::T) {
+        uint32_t ids[GI];
+        bool valid[GI];
+        float sc[GI];
+#pragma unroll
+        for (int gg = 0; gg < GI; ++gg) {
+            const int t = base + RM::reg_row(gg, lane);
+            valid[gg] = t < cnt;
+            if constexpr (C::RPI == 1)
+                ids[gg] = rl_u(cid, (base + gg) & 63);
+            else
+                ids[gg] = shfl_u(cid, t & 63);
+            ids[gg] = valid[gg] ? guard_id(g, ids[gg]) : 0u;
+        }
+        // the owner lane of row town fetches that row's {scale, bound} only
+        const int town = base + RM::owned_row(lane);
+        const uint32_t oid = shfl_u(cid, town & 63);
+        const float2 ax = g.i8aux[town < cnt ? guard_id(g, oid) : 0u];
+        bool r = false;
+        if (metric == EUCLIDEAN) {
+#pragma unroll
+            for (int gg = 0; gg < GI; ++gg) sc[gg] = g.i8aux[ids[gg]].x;
+            const float s = eval_rows_i8<C, GI, true>(q, g.i8, g.pitch, ids, valid, sc);
+            if (town < cnt) r = i8_rejects_l2(s, ax.y, wd);
+        } else {
+#pragma unroll
+            for (int gg = 0; gg < GI; ++gg) sc[gg] = 1.f;
+            const float s = eval_rows_i8<C, GI, false>(q, g.i8, g.pitch, ids, valid, sc);
+            if (town < cnt) r = i8_rejects_cos(s, ax.x, ax.y, qn, wd);
+        }
+        const int t = lane - base;
+        const int src = (t >= 0 && t < RM::T) ? RM::owner(t) : lane;
+        const bool rt = __shfl((int)r, src, 64) != 0;
+        if (t >= 0 && t < RM::T) rej = rt;
+    }
+    int cnt2;
+    const uint32_t cid2 = compact(cid, lane < cnt && !rej, cnt2);
+    cnt = cnt2;
+    return cid2;
+}
+
 // Screened evaluation for the sorted-list searches: candidates whose fp16
 // screening distance proves the f32 distance exceeds `wd` (the list's worst
 // entry before this batch, which only decreases) are dropped; the rest go
@@ -87,10 +138,21 @@ __device__ __forceinline__ uint32_t compact(uint32_t v, bool keep, int& cnt) {
 // Returns the number of rows evaluated in f32.
 template <class C, int G, class Sink>
 __device__ __forceinline__ int eval_screened(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int cnt,
-                                             int metric, float wd, Sink&& sink) {
+                                             int metric, float wd, Sink&& sink, unsigned long long& s8,
+                                             unsigned long long& s16) {
     constexpr int GH = (2 * G <= C::LPR) ? 2 * G : G;
     using RM = RowMap<C, GH>;
     const int lane = lane_id();
+    if (g.i8) {  // stage 1: int8 copy, compact the survivors
+        s8 += cnt;
+        cid = screen_i8<C, G>(g, q, qn, cid, cnt, metric, wd);
+        if (cnt == 0) return 0;
+    }
+    if (!g.h16) {
+        eval_list<C, G>(g, q, qn, cid, cnt, metric, sink);
+        return cnt;
+    }
+    s16 += cnt;
     bool rej = false;  // lane t: candidate t is rejected
     for (int base = 0; base < cnt; base += RM::T) {
         uint32_t ids[GH];
@@ -144,7 +206,8 @@ __device__ __forceinline__ int eval_screened(const GraphDev& g, const QReg<C>& q
 
 struct WaveStats {
     unsigned long long E = 0, X = 0, resets = 0;
-    unsigned long long S = 0, F = 0;  // screened rows (fp16) / rows evaluated in f32
+    unsigned long long S = 0, F = 0;  // screened rows (fp16, or int8 when there is no fp16 copy) / rows evaluated in f32
+    unsigned long long S8 = 0;        // rows screened on the int8 copy
 };
 
 // How the sequential (compat) walks evaluate distances and order their own
@@ -219,8 +282,7 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
             bl_at(L, ef - 1, wd, wi);
         }
         if (SCREEN && screen && wd < __int_as_float(0x7f800000)) {
-            st.S += cnt;
-            st.F += eval_screened<C, G>(g, q, qn, cid, cnt, g.metric, wd, sink);
+            st.F += eval_screened<C, G>(g, q, qn, cid, cnt, g.metric, wd, sink, st.S8, st.S);
         } else {
             st.F += cnt;
             eval_list<C, G>(g, q, qn, cid, cnt, g.metric, sink);

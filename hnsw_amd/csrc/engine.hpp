@@ -66,6 +66,8 @@ constexpr int NEG_MAX_CAND = 256;
 int launch_negatives(const NegArgs& a, int lpr, int vpl, hipStream_t s);
 
 int launch_pad_rows(const float* src, int64_t n, int dim, float* dst, int pitch, hipStream_t s);
+int launch_i8_rows(const float* X, const float* norms, int64_t n0, int64_t n1, int pitch, int metric, int8_t* I,
+                   float2* aux, hipStream_t s);
 int launch_h16_rows(const float* X, const float* norms, int64_t n0, int64_t n1, int pitch, int metric, uint16_t* H,
                     float2* aux, hipStream_t s);
 int launch_norms(const float* X, int64_t n0, int64_t n1, int pitch, int lpr, int vpl, float* out, hipStream_t s);

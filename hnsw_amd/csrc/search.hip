@@ -227,6 +227,73 @@ int launch_h16_rows(const float* X, const float* norms, int64_t n0, int64_t n1, 
 }
 
 // ---------------------------------------------------------------------------
+// int8 screening copy of rows [n0, n1) (device_common.hpp GraphDev::i8), one
+// wave per row; norms[r] (canonical |x|) must already be written.
+//   y = x * (1/|x|) (cosine) or x (L2);  s = max|y_i| / 127;
+//   q8_i = round(y_i / s) in [-127, 127];  aux[r] = {s, e} with
+//   e = |s q8 - y|_2 (1 + 2^-10) + 2^-20 |y|  (covers the rounding of e itself
+//   and of y for cosine); rows outside the screen's validity range (as for
+//   the fp16 copy) get s = NaN and zero bytes.  Rows are stored
+//   lane-contiguous (device_common.hpp eval_rows_i8).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_i8_rows(const float* __restrict__ X, const float* __restrict__ norms,
+                                                 int64_t n0, int64_t n1, int pitch, int metric,
+                                                 int8_t* __restrict__ I, float2* __restrict__ aux) {
+    const int lane = lane_id();
+    const int64_t r = n0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n1) return;
+    const float* xp = X + (size_t)r * pitch;
+    float m = 0.f;
+    bool fin = true;
+    for (int e = lane * 4; e < pitch; e += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(xp + e);
+        fin = fin && isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    fin = __ballot(!fin) == 0ull;
+    const float xn = norms[r];
+    const bool ok = fin && m >= 8.881784197001252e-16f && m <= 1.125899906842624e15f &&  // [2^-50, 2^50]
+                    xn > 0.f && isfinite(xn);
+    const bool cos = metric == COSINE;
+    const float rx = cos ? 1.0f / xn : 1.0f;
+    const float my = cos ? m * rx : m;  // max|y_i| (rounding is monotone)
+    const float inv = ok ? 127.0f / my : 0.f;
+    const float sc = my / 127.0f;
+    float e2 = 0.f;
+    for (int e = lane * 4; e < pitch; e += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(xp + e);
+        const float y[4] = {v.x * rx, v.y * rx, v.z * rx, v.w * rx};
+        uint32_t w = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float t = fminf(fmaxf(rintf(y[j] * inv), -127.f), 127.f);
+            const float d = fmaf(t, sc, -y[j]);
+            e2 = fmaf(d, d, e2);
+            w |= (uint32_t)(uint8_t)(int8_t)(int)t << (8 * j);
+        }
+        // lane-contiguous layout (device_common.hpp eval_rows_i8): element e
+        // = l*4 + v*256 + j (l = lane, v = e / 256) lands at byte l*4*VPL + v*4 + j
+        const int vpl = i8_vpl(pitch);
+        *reinterpret_cast<uint32_t*>(I + (size_t)r * pitch + lane * 4 * vpl + (e >> 8) * 4) = ok ? w : 0u;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) e2 += __shfl_xor(e2, o, 64);
+    const float eb = sqrtf(e2) * 1.0009765625f + 9.5367431640625e-07f * (cos ? 1.0f : xn);
+    if (lane == 0) aux[r] = make_float2(ok ? sc : __int_as_float(0x7fc00000), eb);
+}
+
+int launch_i8_rows(const float* X, const float* norms, int64_t n0, int64_t n1, int pitch, int metric, int8_t* I,
+                   float2* aux, hipStream_t s) {
+    const int64_t rows = n1 - n0;
+    if (rows <= 0) return 0;
+    hipLaunchKernelGGL(k_i8_rows, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, X, norms, n0, n1, pitch, metric,
+                       I, aux);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------
 // batched search: one wave per query
 // ---------------------------------------------------------------------------
 template <class C, int R, int G, bool SCREEN>
@@ -289,6 +356,7 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
         if (st.resets) atomicAdd(&a.stats[2], st.resets);
         atomicAdd(&a.stats[8], st.S);
         atomicAdd(&a.stats[9], st.F);
+        if (st.S8) atomicAdd(&a.stats[10], st.S8);
     }
 }
 
@@ -425,7 +493,7 @@ __global__ __launch_bounds__(64) void k_negatives(NegArgs a) {
 template <class C, int R, int G>
 static int launch_beam_t(const SearchArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 << a.vis_log2;
-    if (a.g.h16)
+    if (a.g.h16 || a.g.i8)
         hipLaunchKernelGGL((k_search_beam<C, R, G, true>), dim3((unsigned)a.B), dim3(64), lds, s, a);
     else
         hipLaunchKernelGGL((k_search_beam<C, R, G, false>), dim3((unsigned)a.B), dim3(64), lds, s, a);

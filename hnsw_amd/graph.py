@@ -475,11 +475,11 @@ class Graph:
         return out
 
     def stats(self) -> dict:
-        o = np.zeros(10, np.int64)
-        self._check(load().mhnsw_stats(self._h, _ptr(o, C.c_int64), 10))
+        o = np.zeros(11, np.int64)
+        self._check(load().mhnsw_stats(self._h, _ptr(o, C.c_int64), 11))
         names = ["search_dist_evals", "search_expansions", "visited_resets", "build_dist_evals",
                  "build_expansions", "dropped_proposals", "searches", "exact_uncertified",
-                 "search_screened", "search_f32_evals"]
+                 "search_screened", "search_f32_evals", "search_screened_i8"]
         return dict(zip(names, o.tolist()))
 
     def reset_stats(self):

@@ -79,8 +79,10 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * "exact_tile" (split GEMM tile: 0 best measured per split, 1 128x256, 2 128x128,
  * 3 256x256), "compat_waves" (1 or 8 waves scoring the compat insert's
  * distance batches), "upper_ef" (beam mode: upper-layer descent width, 1 =
- * greedy), "screen" (beam mode, default 1: keep an fp16 copy of the rows and
- * skip candidates it proves the f32 distance rejects; results unchanged);
+ * greedy), "screen" (beam mode and batched insert, bit set, default 1: bit 0
+ * keeps an fp16 copy of the rows, bit 1 an int8 copy screened first; a
+ * candidate is skipped only when a copy proves the f32 distance rejects it,
+ * so results are unchanged);
  * read-only: "pitch", "capacity", "strkeys", "strkey_relabels" */
 int mhnsw_set_option(mhnsw_index *h, const char *name, int64_t value);
 int mhnsw_get_option(const mhnsw_index *h, const char *name, int64_t *value);
@@ -174,7 +176,8 @@ int mhnsw_preview_levels(mhnsw_index *h, int64_t n, int32_t *out);
  * resets, [3] build distance evals, [4] build expansions, [5] dropped reverse
  * proposals, [6] searches issued, [7] exact-mode queries whose preselection
  * could not be certified and were redone by a full canonical sweep, [8] beam
- * candidates screened on the fp16 copy, [9] beam candidates evaluated in f32 */
+ * candidates screened on the fp16 copy, [9] beam candidates evaluated in f32,
+ * [10] beam candidates screened on the int8 copy */
 int mhnsw_stats(const mhnsw_index *h, int64_t *out, int n);
 int mhnsw_reset_stats(mhnsw_index *h);
 /* device time of the last search's main kernel (HIP events on its stream) */

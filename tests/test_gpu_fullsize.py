@@ -64,9 +64,14 @@ def test_fullsize_c2_beam(H, O):
     on = _search(g, Q, 10, H.MODE_BEAM, 64)
     g.set_option("screen", 0)
     off = _search(g, Q, 10, H.MODE_BEAM, 64)
-    g.set_option("screen", 1)
     assert np.array_equal(on[2], off[2]) and np.array_equal(on[0], off[0])
     assert np.array_equal(on[1].view(np.uint32), off[1].view(np.uint32))
+    for screen in (2, 3):  # int8 stage alone and before the fp16 stage
+        g.set_option("screen", screen)
+        s8 = _search(g, Q, 10, H.MODE_BEAM, 64)
+        assert np.array_equal(s8[2], off[2]) and np.array_equal(s8[0], off[0])
+        assert np.array_equal(s8[1].view(np.uint32), off[1].view(np.uint32))
+    g.set_option("screen", 1)
     keys, dist, cnt = on
     assert (cnt == 10).all()
     _check_lists(keys, dist, cnt, n)

@@ -1,5 +1,5 @@
-"""GPU: the fp16 screening copy (option "screen", DESIGN.md §6, "The fp16 screening copy") never changes
-a beam search.  Every result (keys, f32 distance bits, counts) with the screen
+"""GPU: the screening copies (option "screen": bit 0 fp16, bit 1 int8; DESIGN.md §6, "The fp16
+screening copy" and "The int8 screening copy") never change a beam search.  Every result (keys, f32 distance bits, counts) with the screen
 on must equal the screen-off search and the oracle's beam search, on data built
 to sit at the screen's edges: exact distance ties (integer-valued rows),
 duplicates, rows and queries outside the screen's validity range (huge, tiny,
@@ -49,23 +49,27 @@ def test_screen_identical_to_f32(H, O, metric, d, n):
     o = O.Graph(metric=metric, order=O.ORDER_DEV, M=16, M0=32, Ml=0.25, EfSearch=64)
     o.import_graph(**g.export())
     for ef in (10, 64, 200):
-        g.set_option("screen", 1)
-        g.reset_stats()
-        on = _search(g, Q, ef, H)
-        st = g.stats()
-        assert st["search_screened"] > 0
-        assert st["search_f32_evals"] < st["search_dist_evals"]
         g.set_option("screen", 0)
         g.reset_stats()
         off = _search(g, Q, ef, H)
         st = g.stats()
         assert st["search_screened"] == 0 and st["search_f32_evals"] == st["search_dist_evals"]
-        _same_results(*on, *off)
-        _same_results(*on, *o.search(Q, 10, mode=O.MODE_BEAM, ef=ef))
+        assert st["search_screened_i8"] == 0
+        _same_results(*off, *o.search(Q, 10, mode=O.MODE_BEAM, ef=ef))
+        for screen in (1, 2, 3):
+            g.set_option("screen", screen)
+            g.reset_stats()
+            on = _search(g, Q, ef, H)
+            st = g.stats()
+            assert (st["search_screened_i8"] > 0) == bool(screen & 2), (screen, st)
+            assert (st["search_screened"] > 0) == bool(screen & 1), (screen, st)
+            assert st["search_f32_evals"] < st["search_dist_evals"]
+            _same_results(*on, *off)
     g.close()
 
 
-def test_screen_follows_adds_and_import(H, O):
+@pytest.mark.parametrize("screen", [1, 3])
+def test_screen_follows_adds_and_import(H, O, screen):
     rng = np.random.default_rng(7)
     n, d = 6000, 96
     X, Q = _adversarial(rng, n, d, 0)
@@ -73,41 +77,43 @@ def test_screen_follows_adds_and_import(H, O):
                 ef_construction=64, heuristic=2)
     g.set_option("screen", 0)
     g.add_arrays(np.arange(n // 2), X[: n // 2])
-    g.set_option("screen", 1)                     # enabling converts the rows already held
+    g.set_option("screen", screen)                # enabling converts the rows already held
     g.add_arrays(np.arange(n // 2, n), X[n // 2:])  # later adds convert their own rows
     on = _search(g, Q, 48, H)
     g.set_option("screen", 0)
     _same_results(*on, *_search(g, Q, 48, H))
     # a graph rebuilt by Import screens the imported rows
-    g2 = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=H.CosineDistance, Rng=3, build_mode=H.BUILD_BATCH)
+    g2 = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=H.CosineDistance, Rng=3, build_mode=H.BUILD_BATCH,
+                 screen=screen)
     g2.import_graph(**g.export())
     g2.reset_stats()
     _same_results(*on, *_search(g2, Q, 48, H))
-    assert g2.stats()["search_screened"] > 0
+    assert g2.stats()["search_screened" if screen == 1 else "search_screened_i8"] > 0
     g.close()
     g2.close()
 
 
-def test_screen_follows_metric_change(H, O):
+@pytest.mark.parametrize("screen", [1, 2])
+def test_screen_follows_metric_change(H, O, screen):
     """Distance is a public field (graph.go:309): switching it rewrites the
     screening copy in the new metric's format."""
     rng = np.random.default_rng(8)
     n, d = 5000, 128
     X, Q = _adversarial(rng, n, d, 1)
     g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=H.CosineDistance, Rng=3, build_mode=H.BUILD_BATCH,
-                ef_construction=64, heuristic=2)
+                ef_construction=64, heuristic=2, screen=screen)
     g.add_arrays(np.arange(n), X)
     for dist, metric in ((H.EuclideanDistance, 1), (H.CosineDistance, 0)):
         g.Distance = dist
         g.reset_stats()
         on = _search(g, Q, 48, H)
-        assert g.stats()["search_screened"] > 0
+        assert g.stats()["search_screened" if screen == 1 else "search_screened_i8"] > 0
         o = O.Graph(metric=metric, order=O.ORDER_DEV, M=12, M0=24, Ml=0.3, EfSearch=48)
         o.import_graph(**g.export())
         _same_results(*on, *o.search(Q, 10, mode=O.MODE_BEAM, ef=48))
         g.set_option("screen", 0)
         _same_results(*on, *_search(g, Q, 48, H))
-        g.set_option("screen", 1)
+        g.set_option("screen", screen)
     g.close()
 
 
@@ -122,7 +128,7 @@ def test_screened_batch_build_identical(H, metric):
     n, d = 12000, 96
     X, _ = _adversarial(rng, n, d, metric)
     ex = {}
-    for screen, fuse in ((0, 0), (1, 0), (0, 1), (1, 1)):
+    for screen, fuse in ((0, 0), (1, 0), (0, 1), (1, 1), (2, 1), (3, 1)):
         g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
                     ef_construction=80, heuristic=2, keep_pruned=1, screen=screen, fuse_descent=fuse)
         g.add_arrays(np.arange(n // 3), X[: n // 3])   # two calls: later batches descend a multi-layer graph
@@ -130,5 +136,5 @@ def test_screened_batch_build_identical(H, metric):
         assert g.stats()["dropped_proposals"] == 0
         ex[(screen, fuse)] = g.export()
         g.close()
-    for key in ((1, 0), (0, 1), (1, 1)):
+    for key in ((1, 0), (0, 1), (1, 1), (2, 1), (3, 1)):
         _same_graph(ex[(0, 0)], ex[key])
