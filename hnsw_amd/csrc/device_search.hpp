@@ -260,11 +260,15 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
         const uint32_t cur = bl_next(L);
         if (cur == EMPTY_ID) break;
         st.X += 1;
-        const int deg = min(ld_i32<COH>(degp + guard_id(g, cur)), capl);
+        // the adjacency row is loaded together with its degree (rows are cap
+        // wide, so lanes past the degree read allocated, ignored slots): one
+        // dependent round trip per expansion instead of two
+        const uint32_t cg = guard_id(g, cur);
+        const int32_t rowv = lane < capl ? ld_i32<COH>(adjp + (size_t)cg * capl + lane) : -1;
+        const int deg = min(ld_i32<COH>(degp + cg), capl);
         if (deg <= 0) continue;
         const bool have = lane < deg;
-        uint32_t nb = 0;
-        if (have) nb = (uint32_t)ld_i32<COH>(adjp + (size_t)cur * capl + lane);
+        uint32_t nb = have ? (uint32_t)rowv : 0u;
         int pr = 0;
         if (have && nb != 0xFFFFFFFFu) {
             nb = guard_id(g, nb);
