@@ -38,7 +38,9 @@ def _search(g, Q, ef, H):
     return g.search_arrays(Q, 10, mode=H.MODE_BEAM, ef=ef)
 
 
-@pytest.mark.parametrize("metric,d,n", [(0, 64, 20000), (1, 64, 20000), (0, 768, 6000), (1, 200, 8000)])
+# dims cover every int8 row-load width (VPL 1, 2, 3, 4, 6 dwords per lane)
+@pytest.mark.parametrize("metric,d,n", [(0, 64, 20000), (1, 64, 20000), (0, 768, 6000), (1, 200, 8000),
+                                        (1, 512, 4000), (0, 1024, 3000), (1, 1536, 2500)])
 def test_screen_identical_to_f32(H, O, metric, d, n):
     rng = np.random.default_rng(100 + metric + d)
     X, Q = _adversarial(rng, n, d, metric)
