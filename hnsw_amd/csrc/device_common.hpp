@@ -253,8 +253,31 @@ __device__ __forceinline__ float eval_rows(const QReg<C>& q, const float* __rest
     return reduce_rows<G, C::LPR>(p);
 }
 
-// Approximate sums from the fp16 screening copy, same lane/row mapping as
-// eval_rows.  Dot: sum q_i * h_i.  L2: sum (q_i - h_i * inv_g)^2 with inv[g]
+// N consecutive dwords from a 4-byte aligned address, in 16-B loads then one
+// 8-B / 4-B tail (rows of the screening copies are lane-contiguous).
+template <int N>
+__device__ __forceinline__ void load_dwords(const int* p, int (&x)[N]) {
+#pragma unroll
+    for (int k = 0; k + 4 <= N; k += 4) {
+        const int4 t = *reinterpret_cast<const int4*>(p + k);
+        x[k] = t.x, x[k + 1] = t.y, x[k + 2] = t.z, x[k + 3] = t.w;
+    }
+    constexpr int R = N % 4, B = N - N % 4;
+    if constexpr (R == 3) {
+        typedef int i3 __attribute__((ext_vector_type(3)));
+        const i3 t = *reinterpret_cast<const i3*>(p + B);
+        x[B] = t.x, x[B + 1] = t.y, x[B + 2] = t.z;
+    } else if constexpr (R == 2) {
+        const int2 t = *reinterpret_cast<const int2*>(p + B);
+        x[B] = t.x, x[B + 1] = t.y;
+    } else if constexpr (R == 1) {
+        x[B] = p[B];
+    }
+}
+
+// Approximate sums from the fp16 screening copy, same lane/element mapping
+// as eval_rows, rows stored lane-contiguous (lane sub's 4*VPL halves at
+// [sub*4*VPL, (sub+1)*4*VPL) of the row: one 16-B + one 8-B load at 768-d).  Dot: sum q_i * h_i.  L2: sum (q_i - h_i * inv_g)^2 with inv[g]
 // the row's unscale.
 template <class C, int G, bool L2>
 __device__ __forceinline__ float eval_rows_h16(const QReg<C>& q, const uint16_t* __restrict__ H, int pitch,
@@ -265,14 +288,16 @@ __device__ __forceinline__ float eval_rows_h16(const QReg<C>& q, const uint16_t*
     h4 x[G][C::VPL];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-        const uint16_t* rp = H + (size_t)ids[g] * (size_t)pitch + sub * 4;
+        // lane-contiguous rows (k_h16_rows): this lane's 8*VPL bytes are adjacent
+        int d[2 * C::VPL];
+        if (valid[g]) {
+            load_dwords<2 * C::VPL>(reinterpret_cast<const int*>(H + (size_t)ids[g] * (size_t)pitch + sub * 4 * C::VPL), d);
+        } else {
 #pragma unroll
-        for (int v = 0; v < C::VPL; ++v) {
-            if (valid[g])
-                x[g][v] = *reinterpret_cast<const h4*>(rp + v * C::LPR * 4);
-            else
-                x[g][v] = h4{0, 0, 0, 0};
+            for (int k = 0; k < 2 * C::VPL; ++k) d[k] = 0;
         }
+#pragma unroll
+        for (int v = 0; v < C::VPL; ++v) x[g][v] = __builtin_bit_cast(h4, make_int2(d[2 * v], d[2 * v + 1]));
     }
     float p[G];
 #pragma unroll

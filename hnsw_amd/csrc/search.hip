@@ -212,7 +212,8 @@ __global__ __launch_bounds__(256) void k_h16_rows(const float* __restrict__ X, c
         else
             o = h4{(_Float16)ldexpf(v.x, ex), (_Float16)ldexpf(v.y, ex), (_Float16)ldexpf(v.z, ex),
                    (_Float16)ldexpf(v.w, ex)};
-        *reinterpret_cast<h4*>(H + (size_t)r * pitch + e) = o;
+        // lane-contiguous layout (eval_rows_h16), as the int8 copy
+        *reinterpret_cast<h4*>(H + (size_t)r * pitch + lane * 4 * i8_vpl(pitch) + (e >> 8) * 4) = o;
     }
     if (lane == 0) aux[r] = make_float2(ok ? ldexpf(1.f, -ex) : __int_as_float(0x7fc00000), xn);
 }
