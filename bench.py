@@ -5,14 +5,20 @@
 A "step" = one batched layer-descent + layer-0 beam search of `--batch` query
 vectors already resident in HBM, through the C ABI (mhnsw_search_device).
 
-Multi-GPU (one process per GPU, torchrun):
-  --mode replica (default): every rank holds the full 1M-vector index and
-      serves its own slice of the query stream; no data-path collective
-      (per-GPU work fixed => "scaling": "weak").
-  --mode shard: node-ID range sharding -- rank r owns keys [r*n, (r+1)*n); every
-      query is searched on every shard, per-shard top-k are all-gathered over
-      RCCL (xGMI) and merged on the GPU (mhnsw_merge_topk_device).  The index
-      grows with the GPU count (BASELINE config 4: 10M over 8 GPUs).
+Multi-GPU (one process per GPU, torchrun).  Two layouts, both measured by
+default (the headline `value` is the replica layout; the shard layout is the
+`shard` object of the same JSON line):
+  replica: every rank holds the full 1M-vector index and serves its own slice
+      of the query stream; no data-path collective (per-GPU work fixed =>
+      "scaling": "weak").
+  shard (north_star): node-ID range sharding -- rank r owns keys
+      [r*n, (r+1)*n) of one N*n-row dataset and its own sub-graph; every query
+      is searched on every shard, the per-shard (dist, key) top-k are packed
+      into one buffer, all-gathered in ONE collective over RCCL (xGMI) and
+      merged on the GPU (mhnsw_merge_topk_device).  The index grows with the GPU
+      count (BASELINE config 4: 10M over 8 GPUs), so shard QPS measures the
+      capacity layout, not a throughput layout.
+  --mode shard makes the shard layout the headline (and skips the replica leg).
 
 Also reported: recall@10 against the exact (MFMA brute-force) path, build
 throughput of the batched insert, the search kernel's roofline (HBM-bound;
@@ -34,7 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import hnsw_amd as H  # noqa: E402
-from hnsw_amd.shard import gather_topk, merge_topk, shard_range  # noqa: E402
+from hnsw_amd.shard import engine_local_search, shard_range, sharded_search  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -44,7 +50,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--mode", choices=["replica", "shard"], default="replica")
+    p.add_argument("--mode", choices=["replica", "shard"], default="replica",
+                   help="headline layout; with replica the shard layout is measured too (--no-shard-leg skips it)")
+    p.add_argument("--no-shard-leg", action="store_true")
     p.add_argument("--nbase", type=int, default=1_000_000, help="vectors per index (per shard in shard mode)")
     p.add_argument("--dim", type=int, default=768)
     p.add_argument("--batch", type=int, default=65536, help="queries per step per GPU")
@@ -111,12 +119,6 @@ class Searcher:
         return self.keys, self.dist, self.n
 
 
-def shard_merge(keys, dists, n, k):
-    """all-gather per-shard top-k over RCCL, merge on the GPU (hnsw_amd.shard)."""
-    ak, ad, an = gather_topk(keys, dists, n)
-    return merge_topk(ak, ad, an, k)
-
-
 def recall_at_k(res, n, truth, tn, k):
     res, n, truth, tn = (x.cpu().numpy() for x in (res, n, truth, tn))
     tot = 0.0
@@ -167,71 +169,108 @@ def main():
             dist.init_process_group(a.backend)
     metric = H.CosineDistance if a.metric == "cosine" else H.EuclideanDistance
 
-    # ---- index --------------------------------------------------------------
-    shard = a.mode == "shard"
-    base_off = shard_range(a.nbase * world, world, rank)[0] if shard else 0
-    X = gen_vectors(a.nbase, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=base_off)
-    g = H.Graph(M=a.M, Ml=0.25, EfSearch=a.ef, Distance=metric, Rng=a.seed + (rank if shard else 0),
-                build_mode=H.BUILD_BATCH, m0=a.M0, ef_construction=a.efc, heuristic=2, keep_pruned=a.keep_pruned,
-                prune_alpha_pct=a.alpha, screen=a.screen)
-    g.reserve(a.nbase, a.dim)
-    keys = np.arange(base_off, base_off + a.nbase, dtype=np.int64)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    g.add_device(keys, X.data_ptr(), a.nbase, a.dim)
-    torch.cuda.synchronize()
-    build_s = time.perf_counter() - t0
-    bstats = g.stats()
+    # ---- replica index: rows [0, nbase) on every rank ---------------------------
+    shard_only = a.mode == "shard"
 
-    # ---- queries ------------------------------------------------------------
+    def build(off, rng_seed):
+        X = gen_vectors(a.nbase, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=off)
+        g = H.Graph(M=a.M, Ml=0.25, EfSearch=a.ef, Distance=metric, Rng=rng_seed, build_mode=H.BUILD_BATCH,
+                    m0=a.M0, ef_construction=a.efc, heuristic=2, keep_pruned=a.keep_pruned, prune_alpha_pct=a.alpha,
+                    screen=a.screen)
+        g.reserve(a.nbase, a.dim)
+        keys = np.arange(off, off + a.nbase, dtype=np.int64)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g.add_device(keys, X.data_ptr(), a.nbase, a.dim)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        del X
+        return g, dt, g.stats()
+
     qseed = a.seed + 7_777
-    if shard:
-        Q = gen_vectors(a.batch, a.dim, qseed, a.intrinsic, a.clusters, device, a.metric)
-    else:
-        Q = gen_vectors(a.batch, a.dim, qseed, a.intrinsic, a.clusters, device, a.metric, offset=rank * a.batch)
-    S = Searcher(g, a.batch, a.k, a.dim, device)
-
-    def step():
-        kk, dd, nn = S.run(Q, H.MODE_BEAM, a.ef)
-        if shard and world > 1:
-            return shard_merge(kk, dd, nn, a.k)
-        return kk, dd, nn
-
-    # ---- recall vs exact ----------------------------------------------------
     ngt = min(a.gt_queries, a.batch)
-    res_k, _, res_n = (x.clone() for x in step())
-    G = Searcher(g, ngt, a.k, a.dim, device)
-    tk, td, tn = G.run(Q[:ngt], H.MODE_EXACT, 0)
-    if shard and world > 1:
-        tk, td, tn = shard_merge(tk, td, tn, a.k)
-    torch.cuda.synchronize()
-    recall = recall_at_k(res_k[:ngt], res_n[:ngt], tk, tn, a.k)
 
-    # ---- timed steps --------------------------------------------------------
-    for _ in range(a.warmup):
-        step()
-    g.reset_stats()
-    kernel_ms = []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-        kernel_ms.append(g.last_kernel_ms())
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    st = g.stats()
-    tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        rr = torch.tensor([recall], dtype=torch.float64, device=device)
-        dist.all_reduce(rr)
-        recall = rr.item() / world
-    elapsed = tt.item()
+    def timed_steps(step, g):
+        for _ in range(a.warmup):
+            step()
+        g.reset_stats()
+        kernel_ms = []
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+            kernel_ms.append(g.last_kernel_ms())
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        g.device_status()  # kernel-side errors of the asynchronous searches
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return tt.item(), kernel_ms, g.stats()
 
+    def mean_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=device)
+        dist.all_reduce(t)
+        return t.item() / world
+
+    g = None
+    if not shard_only:
+        g, build_s, bstats = build(0, a.seed)
+        Q = gen_vectors(a.batch, a.dim, qseed, a.intrinsic, a.clusters, device, a.metric, offset=rank * a.batch)
+        S = Searcher(g, a.batch, a.k, a.dim, device)
+
+        def step():
+            return S.run(Q, H.MODE_BEAM, a.ef)
+
+        # recall vs exact on the same index
+        res_k, _, res_n = (x.clone() for x in step())
+        G = Searcher(g, ngt, a.k, a.dim, device)
+        tk, td, tn = G.run(Q[:ngt], H.MODE_EXACT, 0)
+        torch.cuda.synchronize()
+        recall = mean_over_ranks(recall_at_k(res_k[:ngt], res_n[:ngt], tk, tn, a.k))
+        elapsed, kernel_ms, st = timed_steps(step, g)
+
+    # ---- shard layout: rank r owns rows [r*nbase, (r+1)*nbase) of one dataset --------
+    shard_out = None
+    if shard_only or not a.no_shard_leg:
+        lo, _ = shard_range(a.nbase * world, world, rank)
+        if g is not None and lo == 0:
+            gs, sbuild_s, sbstats = g, build_s, bstats  # rank 0's shard is the replica index
+        else:
+            gs, sbuild_s, sbstats = build(lo, a.seed + rank)
+        Qs = gen_vectors(a.batch, a.dim, qseed, a.intrinsic, a.clusters, device, a.metric)  # same on every rank
+
+        def sstep():
+            return sharded_search(engine_local_search(gs, a.k, H.MODE_BEAM, a.ef), Qs, a.k)
+
+        sk, _, sn = (x.clone() for x in sstep())
+        ek, ed, en = sharded_search(engine_local_search(gs, a.k, H.MODE_EXACT, 0), Qs[:ngt], a.k)
+        torch.cuda.synchronize()
+        srecall = mean_over_ranks(recall_at_k(sk[:ngt], sn[:ngt], ek, en, a.k))
+        s_el, s_kms, s_st = timed_steps(sstep, gs)
+        skms = float(np.mean(s_kms))
+        shard_out = {
+            "value": round(a.batch * a.steps / s_el, 1), "unit": "queries/s",
+            "ms_per_step": round(s_el / a.steps * 1e3, 3), "recall_at_10": round(srecall, 4),
+            "n_base_total": a.nbase * world, "shards": world, "rows_per_shard": a.nbase,
+            "queries_per_step": a.batch, "search_kernel_ms": round(skms, 4),
+            "exchange": ("none (one shard)" if world == 1 else
+                         f"one all-gather of {a.batch * (12 * a.k + 4)} B per rank ({a.backend}), k_merge on the GPU"),
+            "recall_reference": "sharded exact search (per-shard MFMA exact + the same gather + merge)",
+            "build_inserts_per_s_per_rank": round(a.nbase / sbuild_s, 1),
+        }
+        if shard_only:
+            g, build_s, bstats, recall, elapsed, kernel_ms, st = gs, sbuild_s, sbstats, srecall, s_el, s_kms, s_st
+            Q, S = Qs, Searcher(gs, a.batch, a.k, a.dim, device)
+            tk, tn = ek, en
+
+    shard = shard_only
     queries_done = a.batch * a.steps * (1 if shard else world)
     qps = queries_done / elapsed
 
@@ -303,8 +342,10 @@ def main():
                  f"random linear map + N(0,0.05^2) noise, L2-normalised; seed {a.seed}; queries from the same "
                  f"distribution (seed {qseed})"),
         "config": {
-            "workload": f"{a.nbase // 1000}k x {a.dim}-d {a.metric}, batched beam search ef={a.ef} k={a.k}, "
-                        f"{a.batch} queries/step/GPU (BASELINE configs[1])",
+            "workload": (f"{a.nbase // 1000}k x {a.dim}-d {a.metric}, batched beam search ef={a.ef} k={a.k}, "
+                         f"{a.batch} queries/step/GPU (BASELINE configs[1])") if not shard else
+                        (f"{world} node-ID range shards of {a.nbase // 1000}k x {a.dim}-d {a.metric}, every query on "
+                         f"every shard, beam ef={a.ef} k={a.k}, {a.batch} queries/step (BASELINE configs[3] layout)"),
             "n_base": a.nbase * (world if shard else 1), "dim": a.dim, "batch_per_gpu": a.batch, "ef": a.ef,
             "k": a.k, "M": a.M, "M0": a.M0, "ef_construction": a.efc, "keep_pruned": a.keep_pruned,
             "prune_alpha": a.alpha / 100,
@@ -330,6 +371,8 @@ def main():
         "operating_points": points,
         "at_recall_0.99": at99,
     }
+    if shard_out is not None and not shard_only:
+        out["shard"] = shard_out
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
         qn = Q[: min(a.batch, 4096)].cpu().numpy()
         cb = cpu_baseline(g, qn, a.k, a.ef, a.metric, a.cpu_seconds)

@@ -40,6 +40,7 @@ SIGNATURES = {
                                _i32p]),
     "mhnsw_search_device": (C.c_int, [_vp, _vp, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp,
                                       _vp]),
+    "mhnsw_device_status": (C.c_int, [_vp]),
     "mhnsw_search_negatives": (C.c_int, [_vp, _f32p, C.c_int64, C.c_int, _f32p, _i32p, C.c_int, C.c_float, C.c_int,
                                          C.c_int, C.c_int, _i64p, _f32p, _i32p]),
     "mhnsw_len": (C.c_int64, [_vp]),

@@ -7,6 +7,10 @@
 // per-node levels and per-layer counts/entries.
 #include <hip/hip_runtime.h>
 
+#include <errno.h>
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
@@ -99,6 +103,9 @@ struct mhnsw_index {
     LayerDev* d_layers = nullptr;
     LayerDev layers_host[MH_MAXL] = {};
     unsigned long long* d_stats = nullptr;
+    // d_err[0]: error word of the current synchronous call (zeroed per call);
+    // d_err[1]: sticky word of *_device searches, which return before their
+    // kernels run -- read and cleared by mhnsw_device_status
     int* d_err = nullptr;
     std::vector<Layer> layers;
     // scratch
@@ -699,16 +706,18 @@ int drain(mhnsw_index* h) {
 
 int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B, int dim, int k, int mode, int ef,
                 const int64_t* entry_key, int64_t* okeys, float* odist, int32_t* on, hipStream_t s, bool timing,
-                int32_t* out_ids);
+                int32_t* out_ids, bool sticky);
 
 // every search: order after the previous scratch user (another stream), and
-// after the metadata copies this call makes on the handle's stream
+// after the metadata copies this call makes on the handle's stream.  sticky:
+// the kernels report into d_err[1] (an asynchronous *_device search the caller
+// checks with mhnsw_device_status); otherwise into d_err[0], zeroed first.
 int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B, int dim, int k, int mode, int ef,
                 const int64_t* entry_key, int64_t* okeys, float* odist, int32_t* on, hipStream_t s, bool timing,
-                int32_t* out_ids = nullptr) {
+                int32_t* out_ids = nullptr, bool sticky = false) {
     if (h->scr_valid && h->scr_stream != s) HIPCHK(h, hipStreamWaitEvent(s, h->scr_ev, 0));
     const int r = search_body(h, queries, on_device, B, dim, k, mode, ef, entry_key, okeys, odist, on, s, timing,
-                              out_ids);
+                              out_ids, sticky);
     HIPCHK(h, hipEventRecord(h->scr_ev, s));
     h->scr_stream = s;
     h->scr_valid = true;
@@ -725,7 +734,7 @@ int order_meta(mhnsw_index* h, hipStream_t s) {
 
 int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B, int dim, int k, int mode, int ef,
                 const int64_t* entry_key, int64_t* okeys, float* odist, int32_t* on, hipStream_t s, bool timing,
-                int32_t* out_ids) {
+                int32_t* out_ids, bool sticky) {
     int r = validate(h);
     if (r) return r;
     if (k <= 0) return fail(h, MHNSW_EK, "k must be greater than 0, got %d", k);  // graph.go:542-544
@@ -772,7 +781,8 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         dd = h->odist.p;
         dn = h->on.p;
     }
-    HIPCHK(h, hipMemsetAsync(h->d_err, 0, sizeof(int), s));
+    int* errw = sticky ? h->d_err + 1 : h->d_err;
+    if (!sticky) HIPCHK(h, hipMemsetAsync(h->d_err, 0, sizeof(int), s));
     if (mode == MHNSW_MODE_EXACT) {
         if (k > 256) return fail(h, MHNSW_EUNSUPPORTED, "exact mode supports k <= 256");
         const bool split = h->exact_precision != 0;
@@ -814,6 +824,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         LCHK(h, launch_norms(h->qpad.p, 0, B, h->pitch, h->lpr, h->vpl, h->qnorm.p, s));
         if ((r = sync_layer_table(h)) || (r = order_meta(h, s))) return r;
         GraphDev g = graph_view(h);
+        g.err = errw;
         // certificate constants (u = 2^-24; gamma_n = n u / (1 - n u) bounds any
         // order of n-term f32 summation relative to the sum of magnitudes)
         const double u = std::ldexp(1.0, -24);
@@ -922,6 +933,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         if ((r = sync_layer_table(h)) || (r = order_meta(h, s))) return r;
         SearchArgs a;
         a.g = graph_view(h);
+        a.g.err = errw;
         a.q = h->qpad.p;
         a.B = B;
         a.k = k;
@@ -934,7 +946,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         a.out_n = dn;
         a.out_ids = out_ids;
         a.stats = h->d_stats;
-        a.err = h->d_err;
+        a.err = errw;
         a.vis_log2 = h->vis_log2;
         a.upper_ef = h->upper_ef;
         if (mode == MHNSW_MODE_BEAM) {
@@ -993,7 +1005,7 @@ int mhnsw_create(int metric, int M, double ml, int ef_search, uint64_t seed, mhn
         return fail(nullptr, MHNSW_EDEVICE, "no HIP device available");
     }
     if (hipMalloc(&h->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&h->d_err, sizeof(int)) != hipSuccess || hipMalloc(&h->touched_cnt, 16) != hipSuccess ||
+        hipMalloc(&h->d_err, 2 * sizeof(int)) != hipSuccess || hipMemset(h->d_err, 0, 2 * sizeof(int)) != hipSuccess || hipMalloc(&h->touched_cnt, 16) != hipSuccess ||
         hipMalloc(&h->d_layer_entry, MH_MAXL * 4) != hipSuccess ||
         hipMalloc(&h->d_layers, MH_MAXL * sizeof(LayerDev)) != hipSuccess || hipEventCreate(&h->ev0) != hipSuccess ||
         hipEventCreate(&h->ev1) != hipSuccess || hipEventCreateWithFlags(&h->scr_ev, hipEventDisableTiming) != hipSuccess ||
@@ -1097,6 +1109,7 @@ int mhnsw_set_params(mhnsw_index* h, int metric, int M, double ml, int ef_search
 }
 
 int mhnsw_get_params(const mhnsw_index* h, int* metric, int* M, double* ml, int* ef_search) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
     if (metric) *metric = h->metric;
     if (M) *M = h->M;
     if (ml) *ml = h->ml;
@@ -1138,7 +1151,7 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "batch_ratio_pct") {
         h->batch_ratio_pct = (int)std::max<int64_t>(0, v);
     } else if (n == "vis_log2") {
-        if (v < 8 || v > 15) return fail(h, MHNSW_EINVAL, "vis_log2 must be in [8, 15]");
+        if (v < 6 || v > 15) return fail(h, MHNSW_EINVAL, "vis_log2 must be in [6, 15]");
         h->vis_log2 = (int)v;
     } else if (n == "exact_kk") {
         h->exact_kk = (int)v;
@@ -1188,6 +1201,7 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
 }
 
 int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
     std::string n(name ? name : "");
     if (n == "build_mode") *v = h->build_mode;
     else if (n == "m0") *v = m0_of(h);
@@ -1260,13 +1274,35 @@ int mhnsw_search_device(mhnsw_index* h, const float* d_queries, int64_t B, int d
     std::unique_lock<std::shared_mutex> lk(h->mu);
     // NULL is the HIP null stream (torch's default stream handle is 0)
     return search_impl(h, d_queries, true, B, dim, k, mode, ef, nullptr, d_keys, d_dist, d_n, (hipStream_t)stream,
-                       true);
+                       true, nullptr, true);
 }
 
-int64_t mhnsw_len(const mhnsw_index* h) { return h->layers.empty() ? 0 : h->layers[0].count; }
-int mhnsw_dims(const mhnsw_index* h) { return h->layers_exist ? h->dim : 0; }
-int mhnsw_num_layers(const mhnsw_index* h) { return (int)h->layers.size(); }
+int mhnsw_device_status(mhnsw_index* h) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    if (h->scr_valid) HIPCHK(h, hipEventSynchronize(h->scr_ev));
+    int err = 0;
+    HIPCHK(h, hipMemcpy(&err, h->d_err + 1, sizeof(int), hipMemcpyDeviceToHost));
+    if (!err) return MHNSW_OK;
+    HIPCHK(h, hipMemset(h->d_err + 1, 0, sizeof(int)));
+    if (err & 4) return fail(h, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
+    return fail(h, MHNSW_EINTERNAL, "visited set overflow (raise vis_log2)");
+}
+
+// read-locked like the reference's Len/Dims (graph.go:421,829): a concurrent Add may grow h->layers
+int64_t mhnsw_len(const mhnsw_index* h) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    return h->layers.empty() ? 0 : h->layers[0].count;
+}
+int mhnsw_dims(const mhnsw_index* h) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    return h->layers_exist ? h->dim : 0;
+}
+int mhnsw_num_layers(const mhnsw_index* h) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    return (int)h->layers.size();
+}
 int64_t mhnsw_layer_count(const mhnsw_index* h, int l) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
     return l >= 0 && l < (int)h->layers.size() ? h->layers[l].count : 0;
 }
 
@@ -1700,18 +1736,37 @@ int mhnsw_import_go(mhnsw_index* h, const uint8_t* buf, int64_t size, int key_ki
     return import_go(h, buf, size, key_kind);
 }
 
-// encode.go:301-327 SavedGraph.Save: write to a temp file, then rename over path
+// encode.go:301-327 SavedGraph.Save (renameio): write a uniquely named temp file
+// in the target directory, fsync it, then rename it over path.  Concurrent
+// Saves (the read lock allows them) never share a temp file.
 int mhnsw_save(mhnsw_index* h, const char* path, int key_kind) {
     std::shared_lock<std::shared_mutex> lk(h->mu);
     std::vector<uint8_t> out;
     int r = export_go(h, key_kind, out);
     if (r) return r;
-    const std::string tmp = std::string(path) + ".tmp";
-    FILE* f = fopen(tmp.c_str(), "wb");
-    if (!f) return fail(h, MHNSW_EINVAL, "open %s failed", tmp.c_str());
-    const bool ok = fwrite(out.data(), 1, out.size(), f) == out.size();
-    if (fclose(f) != 0 || !ok) return fail(h, MHNSW_EINVAL, "write %s failed", tmp.c_str());
-    if (rename(tmp.c_str(), path) != 0) return fail(h, MHNSW_EINVAL, "rename to %s failed", path);
+    std::string tmpl = std::string(path) + ".tmp.XXXXXX";
+    std::vector<char> name(tmpl.begin(), tmpl.end());
+    name.push_back('\0');
+    const int fd = mkstemp(name.data());
+    if (fd < 0) return fail(h, MHNSW_EINVAL, "create temp file for %s failed", path);
+    size_t off = 0;
+    bool ok = true;
+    while (ok && off < out.size()) {
+        const ssize_t w = write(fd, out.data() + off, out.size() - off);
+        if (w < 0 && errno == EINTR) continue;
+        ok = w > 0;
+        if (ok) off += (size_t)w;
+    }
+    ok = ok && fsync(fd) == 0;
+    ok = (close(fd) == 0) && ok;
+    if (!ok) {
+        unlink(name.data());
+        return fail(h, MHNSW_EINVAL, "write %s failed", name.data());
+    }
+    if (rename(name.data(), path) != 0) {
+        unlink(name.data());
+        return fail(h, MHNSW_EINVAL, "rename to %s failed", path);
+    }
     return 0;
 }
 
@@ -1832,7 +1887,11 @@ int mhnsw_search_negatives(mhnsw_index* h, const float* queries, int64_t B, int 
     HIPCHK(h, hipMemcpyAsync(kk.data(), h->nok.p, kk.size() * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipMemcpyAsync(ss.data(), h->nos.p, ss.size() * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipMemcpyAsync(nn.data(), h->non.p, nn.size() * 4, hipMemcpyDeviceToHost, s));
+    int err = 0;  // the candidate search and the re-ranking report into d_err[0]
+    HIPCHK(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipStreamSynchronize(s));
+    if (err & 4) return fail(h, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
+    if (err) return fail(h, MHNSW_EINTERNAL, "visited set overflow (raise vis_log2)");
     for (int64_t i = 0; i < R; ++i) {
         const int64_t b = rer[(size_t)i];
         memcpy(out_keys + (size_t)b * k, &kk[(size_t)i * k], (size_t)k * 8);
@@ -1937,8 +1996,9 @@ int mhnsw_stats(const mhnsw_index* h, int64_t* out, int n) {
     unsigned long long d[16];
     HIPCHK(hh, hipDeviceSynchronize());
     HIPCHK(hh, hipMemcpy(d, h->d_stats, sizeof(d), hipMemcpyDeviceToHost));
-    int err = 0;
-    HIPCHK(hh, hipMemcpy(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    int err2[2] = {0, 0};
+    HIPCHK(hh, hipMemcpy(err2, h->d_err, sizeof(err2), hipMemcpyDeviceToHost));
+    const int err = err2[0] | err2[1];
     if (err & 4) return fail(hh, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
     const int64_t v[11] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4], (int64_t)d[5], (int64_t)d[6],
                            h->stats_host[6], (int64_t)d[3], (int64_t)d[8], (int64_t)d[9], (int64_t)d[10]};

@@ -748,11 +748,22 @@ __global__ __launch_bounds__(256) void k_exact_fallback(const float* __restrict_
 // ---------------------------------------------------------------------------
 // merge S shard lists (each sorted, n_in valid) -> best k by (distance, key)
 // ---------------------------------------------------------------------------
+// Total order on distances: the float order with -0 == +0, every NaN after
+// +inf (NaN distances come back from compat searches over zero rows), and the
+// padding of short lists after everything.  Ranks are then a permutation, so
+// every output slot below min(k, valid) is written exactly once.
+__device__ __forceinline__ uint32_t merge_ord(float d, bool valid) {
+    if (!valid) return 0xFFFFFFFFu;
+    if (d != d) return 0xFFFFFFFEu;
+    uint32_t u = __float_as_uint(d == 0.0f ? 0.0f : d);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
 __global__ __launch_bounds__(64) void k_merge(const int64_t* keys_in, const float* dist_in, const int32_t* n_in,
                                               int S, int64_t B, int k, int64_t* out_keys, float* out_dist,
                                               int32_t* out_n) {
     extern __shared__ __attribute__((aligned(16))) unsigned char msm[];
-    float* sd = reinterpret_cast<float*>(msm);
+    uint32_t* so = reinterpret_cast<uint32_t*>(msm);
     int64_t* sk = reinterpret_cast<int64_t*>(msm + ((size_t)S * k * 4 + 15) / 16 * 16);
     const int64_t b = blockIdx.x;
     if (b >= B) return;
@@ -762,24 +773,25 @@ __global__ __launch_bounds__(64) void k_merge(const int64_t* keys_in, const floa
         const int s = e / k, j = e % k;
         const int nv = n_in[(size_t)s * B + b];
         const bool ok = j < nv;
-        sd[e] = ok ? dist_in[((size_t)s * B + b) * k + j] : __int_as_float(0x7f800000);
+        so[e] = merge_ord(ok ? dist_in[((size_t)s * B + b) * k + j] : 0.0f, ok);
         sk[e] = ok ? keys_in[((size_t)s * B + b) * k + j] : INT64_MAX;
     }
     __syncthreads();
     int nvalid = 0;
     for (int e = lane; e < tot; e += 64) {
-        const float d = sd[e];
+        const uint32_t d = so[e];
         const int64_t key = sk[e];
-        const bool valid = key != INT64_MAX || d < __int_as_float(0x7f800000);
+        const bool valid = d != 0xFFFFFFFFu;
         int rank = 0;
         for (int f = 0; f < tot; ++f) {
-            const float od = sd[f];
+            const uint32_t od = so[f];
             const int64_t ok = sk[f];
             rank += (od < d || (od == d && (ok < key || (ok == key && f < e)))) ? 1 : 0;
         }
         if (valid && rank < k) {
+            const int s = e / k, j = e % k;
             out_keys[b * k + rank] = key;
-            out_dist[b * k + rank] = d;
+            out_dist[b * k + rank] = dist_in[((size_t)s * B + b) * k + j];
         }
         nvalid += valid ? 1 : 0;
     }

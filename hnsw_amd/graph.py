@@ -128,22 +128,64 @@ def _metric_of(fn) -> int:
                         "EuclideanDistance)")
 
 
+def max_level(ml: float, num_nodes: int) -> int:
+    """graph.go:370-385 maxLevel."""
+    if num_nodes == 0:
+        return 1
+    return int(np.round(np.log(float(num_nodes)) / np.log(1.0 / ml))) + 1
+
+
+def random_level(rng, ml: float, layers_exist: bool, base: int) -> int:
+    """graph.go:388-417 randomLevel for a layer 0 of `base` nodes, drawing from
+    rng.Float64()."""
+    mx = max_level(ml, base) if layers_exist else 1
+    for level in range(mx):
+        if rng.Float64() > ml:
+            return level
+    return mx
+
+
+class SplitMix64Rand:
+    """A Go-style *rand.Rand (Float64 in [0,1)) on the engine's own stream:
+    levels drawn from SplitMix64Rand(s) equal the engine's seed-s levels."""
+
+    def __init__(self, seed: int):
+        self.state = int(seed) & (2**64 - 1)
+
+    def Float64(self) -> float:
+        m = 2**64 - 1
+        self.state = (self.state + 0x9E3779B97F4A7C15) & m
+        z = self.state
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+        z ^= z >> 31
+        return (z >> 11) * (1.0 / 9007199254740992.0)
+
+
+DOG_QUERY_HACK = 1  # Graph.TestHacks bit: graph.go:563-569, 595-619
+
+
 class Graph:
     """graph.go:305-332 Graph[K].  Public fields M, Ml, EfSearch, Distance and
-    Rng (a seed) are read by every call, like the Go struct fields."""
+    Rng are read by every call, like the Go struct fields.  Rng is either a
+    seed (the engine draws levels from its SplitMix64 stream) or, like Go's
+    `*rand.Rand`, any object with Float64(): then every Add draws the levels
+    on the host with the reference's rule (graph.go:388-417) and injects them.
+    TestHacks (bit DOG_QUERY_HACK) opts into the reference's Search test hack."""
 
     def __init__(self, M: int = 16, Ml: float = 0.25, EfSearch: int = 20, Distance=CosineDistance,
-                 Rng: int = 0, build_mode: int = BUILD_COMPAT, _handle=None, **options):
+                 Rng=0, build_mode: int = BUILD_COMPAT, _handle=None, TestHacks: int = 0, **options):
         lib = load()
         h = _handle
         if h is None:
             # a Go struct literal may hold an invalid config; Validate() errors
             # surface at call time, so create with a valid one and apply fields
             h = C.c_void_p()
-            check(lib.mhnsw_create(COSINE, 16, 0.25, 20, int(Rng) & (2**64 - 1), C.byref(h)))
+            check(lib.mhnsw_create(COSINE, 16, 0.25, 20, 0, C.byref(h)))
         self._h = h
         self.M, self.Ml, self.EfSearch, self.Distance = M, Ml, EfSearch, Distance
-        self._rng = int(Rng)
+        self.TestHacks = TestHacks
+        self.Rng = Rng
         self._values = {}  # original key -> value (Node.Value)
         self._kt = None    # "int" | "float" | "str" once the first key is seen
         self.set_option("build_mode", build_mode)
@@ -174,9 +216,21 @@ class Graph:
         return self._rng
 
     @Rng.setter
-    def Rng(self, seed: int):
-        self._rng = int(seed)
-        self._check(load().mhnsw_seed(self._h, int(seed) & (2**64 - 1)))
+    def Rng(self, rng):
+        if hasattr(rng, "Float64"):
+            self._rng = rng
+            return
+        self._rng = int(rng)
+        self._check(load().mhnsw_seed(self._h, int(rng) & (2**64 - 1)))
+
+    def _draw_levels(self, n: int):
+        """Levels of the next n inserts from a host Rng (None: the engine draws)."""
+        if not hasattr(self._rng, "Float64"):
+            return None
+        existed = load().mhnsw_num_layers(self._h) > 0
+        base = self.Len()
+        return np.array([random_level(self._rng, float(self.Ml), existed or i > 0, base + i) for i in range(n)],
+                        np.int32)
 
     def set_option(self, name: str, value: int):
         self._check(load().mhnsw_set_option(self._h, name.encode(), int(value)))
@@ -266,6 +320,8 @@ class Graph:
         self._sync()
         keys = np.ascontiguousarray(keys, dtype=np.int64)
         vecs = _f32(vecs).reshape(len(keys), -1)
+        if levels is None and self.get_option("build_mode") != 2:
+            levels = self._draw_levels(len(keys))
         lv = None if levels is None else np.ascontiguousarray(levels, dtype=np.int32)
         self._check(load().mhnsw_add(self._h, _ptr(keys, C.c_int64), _ptr(vecs, C.c_float), len(keys),
                                      vecs.shape[1], None if lv is None else _ptr(lv, C.c_int32)))
@@ -274,6 +330,8 @@ class Graph:
         """BatchAdd with vectors already resident in HBM (device pointer)."""
         self._sync()
         keys = np.ascontiguousarray(keys, dtype=np.int64)
+        if levels is None and self.get_option("build_mode") != 2:
+            levels = self._draw_levels(n)
         lv = None if levels is None else np.ascontiguousarray(levels, dtype=np.int32)
         self._check(load().mhnsw_add_device(self._h, _ptr(keys, C.c_int64), C.c_void_p(vecs_dev_ptr), n, dim,
                                             None if lv is None else _ptr(lv, C.c_int32)))
@@ -305,6 +363,11 @@ class Graph:
                                                C.c_void_p(keys_ptr), C.c_void_p(dist_ptr), C.c_void_p(n_ptr),
                                                C.c_void_p(stream)))
 
+    def device_status(self):
+        """Wait for the last enqueued search_device and raise what its kernels
+        reported (compat visited-set overflow, out-of-range ids); clears it."""
+        self._check(load().mhnsw_device_status(self._h))
+
     def _node(self, key) -> Node:
         v = self._values.get(key)
         if v is None:
@@ -312,8 +375,17 @@ class Graph:
         return Node(key, v)
 
     def Search(self, near, k: int, mode: int = MODE_COMPAT) -> List[Node]:
-        ok, _, on = self.search_arrays(np.asarray(near, np.float32).reshape(1, -1), k, mode)
-        return self._nodes(ok[0, : on[0]])
+        q = np.asarray(near, np.float32).reshape(1, -1)
+        # graph.go:563-569 (opt-in test hack): the dog query searches with 2*EfSearch
+        dog = bool(self.TestHacks & DOG_QUERY_HACK) and q.size == 3 and q[0].tolist() == [1.0, np.float32(0.2),
+                                                                                           np.float32(0.1)]
+        ok, _, on = self.search_arrays(q, k, mode, ef=2 * int(self.EfSearch) if dog else 0)
+        out = self._nodes(ok[0, : on[0]])
+        if dog and len(out) == 3 and self._kt in (None, "int") and all(n.Key != 3 for n in out):
+            v, found = self.Lookup(3)  # graph.go:595-619: canine replaces the last result
+            if found:
+                out[2] = Node(3, v)
+        return out
 
     def BatchSearch(self, queries: Iterable, k: int, mode: int = MODE_COMPAT) -> List[List[Node]]:
         qs = [np.asarray(q, np.float32).ravel() for q in queries]

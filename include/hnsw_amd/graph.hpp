@@ -8,8 +8,11 @@
 // 911 -- documented in DESIGN.md).
 #pragma once
 
+#include <chrono>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <initializer_list>
 #include <map>
 #include <memory>
@@ -65,6 +68,64 @@ struct DistanceFunc {
 };
 inline const DistanceFunc CosineDistance{MHNSW_COSINE, "cosine"};        // distance.go:15-17
 inline const DistanceFunc EuclideanDistance{MHNSW_EUCLIDEAN, "euclidean"};  // distance.go:20-23
+
+// ---- Graph.Rng (graph.go:312 `Rng *rand.Rand`) -----------------------------
+// Levels are drawn on the host from the caller's generator, exactly where and
+// how the reference draws them (graph.go:388-417, below), and handed to the
+// engine as injected levels -- so a graph built through this shim depends on
+// the caller's Rng the way a Go graph does.  Any source of Float64() in [0, 1)
+// will do: SplitMix64Rand reproduces the engine's own seeded stream
+// (mhnsw_seed / mhnsw_preview_levels), FuncRand wraps any callable.
+struct Rand {
+    virtual ~Rand() = default;
+    virtual double Float64() = 0;  // math/rand (*Rand).Float64
+};
+
+struct SplitMix64Rand : Rand {
+    uint64_t state;
+    explicit SplitMix64Rand(uint64_t seed) : state(seed) {}
+    double Float64() override {
+        uint64_t z = (state += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z = z ^ (z >> 31);
+        return (double)(z >> 11) * (1.0 / 9007199254740992.0);
+    }
+};
+
+struct FuncRand : Rand {
+    std::function<double()> fn;
+    explicit FuncRand(std::function<double()> f) : fn(std::move(f)) {}
+    double Float64() override { return fn(); }
+};
+
+inline std::shared_ptr<Rand> NewRand(uint64_t seed) { return std::make_shared<SplitMix64Rand>(seed); }
+
+// graph.go:340-342 defaultRand: time-seeded
+inline std::shared_ptr<Rand> defaultRand() {
+    return NewRand((uint64_t)std::chrono::high_resolution_clock::now().time_since_epoch().count());
+}
+
+// graph.go:370-385
+inline int maxLevel(double ml, int64_t numNodes) {
+    if (numNodes == 0) return 1;
+    double l = std::log((double)numNodes);
+    l /= std::log(1.0 / ml);
+    return (int)std::round(l) + 1;
+}
+
+// graph.go:388-417 randomLevel, for a graph whose layer 0 holds `base` nodes
+// (`layersExist` = len(h.layers) > 0); draws from rng
+inline int randomLevel(Rand& rng, double ml, bool layersExist, int64_t base) {
+    int max = 1;
+    if (layersExist) max = maxLevel(ml, base);
+    for (int level = 0; level < max; ++level)
+        if (rng.Float64() > ml) return level;
+    return max;
+}
+
+// Search test hacks of the reference, opt-in (Graph::TestHacks bits)
+enum : unsigned { kDogQueryHack = 1u };  // graph.go:563-569, 595-619
 
 // ---- K of Graph[K cmp.Ordered] -> the engine's int64 key -------------------
 // The engine only compares keys, so each key type travels as an
@@ -153,14 +214,20 @@ class Graph {  // graph.go:305-332
 
    public:
     const DistanceFunc* Distance = &CosineDistance;
-    uint64_t Rng = 0;
+    std::shared_ptr<Rand> Rng;  // nullptr: defaultRand() at the first Add (graph.go:407-409)
     int M = 16;
     double Ml = 0.25;
     int EfSearch = 20;
+    // opt-in reproduction of the reference's test hacks in Search (kDogQueryHack)
+    unsigned TestHacks = 0;
 
-    Graph() { create(); }
+    Graph() : Rng(NewRand(0)) { create(); }
     Graph(int m, double ml, int ef, const DistanceFunc* dist, uint64_t seed)
-        : Distance(dist), Rng(seed), M(m), Ml(ml), EfSearch(ef) {
+        : Distance(dist), Rng(NewRand(seed)), M(m), Ml(ml), EfSearch(ef) {
+        create();
+    }
+    Graph(int m, double ml, int ef, const DistanceFunc* dist, std::shared_ptr<Rand> rng)
+        : Distance(dist), Rng(std::move(rng)), M(m), Ml(ml), EfSearch(ef) {
         create();
     }
     Graph(const Graph&) = delete;
@@ -182,7 +249,9 @@ class Graph {  // graph.go:305-332
     Error Add(std::initializer_list<Node<K>> nodes) { return BatchAdd(std::vector<Node<K>>(nodes)); }
     Error Add(const Node<K>& n) { return BatchAdd(std::vector<Node<K>>{n}); }
 
-    // graph.go:942-1042 (levels: optional injection for parity tests)
+    // graph.go:942-1042.  Levels come from Rng, one draw sequence per node in
+    // order with the layer-0 size growing by one per insert, as BatchAdd /
+    // Add draw them (graph.go:457, 962); `levels` overrides them (parity tests).
     Error BatchAdd(const std::vector<Node<K>>& nodes, const std::vector<int32_t>* levels = nullptr) {
         sync();
         if (nodes.empty()) return make_error(mhnsw_validate(h_), h_);
@@ -201,25 +270,50 @@ class Graph {  // graph.go:305-332
             ks.push_back(n.Key);
             flat.insert(flat.end(), n.Value.begin(), n.Value.end());
         }
+        std::vector<int32_t> drawn;
+        if (!levels) {
+            if (!Rng) Rng = defaultRand();
+            const bool existed = mhnsw_num_layers(h_) > 0;
+            const int64_t base = Len();
+            drawn.resize(nodes.size());
+            for (size_t i = 0; i < nodes.size(); ++i)
+                drawn[i] = randomLevel(*Rng, Ml, existed || i > 0, base + (int64_t)i);
+            levels = &drawn;
+        }
         const std::vector<int64_t> keys = Codec::encode(h_, ks, /*assign=*/true);
-        int rc = mhnsw_add(h_, keys.data(), flat.data(), (int64_t)nodes.size(), (int)d,
-                           levels ? levels->data() : nullptr);
+        int rc = mhnsw_add(h_, keys.data(), flat.data(), (int64_t)nodes.size(), (int)d, levels->data());
         if (rc < 0) return make_error(rc, h_);
         for (const auto& n : nodes) values_[n.Key] = n.Value;
         return {};
     }
 
-    // graph.go:534-625 (mode: MHNSW_MODE_COMPAT = the reference's semantics)
+    // graph.go:534-625 (mode: MHNSW_MODE_COMPAT = the reference's semantics).
+    // With TestHacks & kDogQueryHack, the reference's special case for the
+    // query {1.0, 0.2, 0.1} is reproduced: EfSearch doubled, and key 3 put in
+    // the last of exactly three results when missing (graph.go:563-569,595-619).
     std::pair<std::vector<Node<K>>, Error> Search(const Vector& near, int k, int mode = MHNSW_MODE_COMPAT) {
-        auto r = BatchSearch(std::vector<Vector>{near}, k, mode, /*single=*/true);
+        const bool dog = (TestHacks & kDogQueryHack) && near.size() == 3 && near[0] == 1.0f && near[1] == 0.2f &&
+                         near[2] == 0.1f;
+        auto r = BatchSearch(std::vector<Vector>{near}, k, mode, /*single=*/true, dog ? 2 * EfSearch : 0);
         if (r.second) return {{}, r.second};
-        return {r.first.empty() ? std::vector<Node<K>>{} : r.first[0], {}};
+        std::vector<Node<K>> out = r.first.empty() ? std::vector<Node<K>>{} : r.first[0];
+        if constexpr (std::is_integral<K>::value) {
+            if (dog && out.size() == 3) {
+                bool has = false;
+                for (const auto& n : out) has = has || n.Key == (K)3;
+                if (!has) {
+                    auto v = Lookup((K)3);
+                    if (v.second) out[2] = Node<K>{(K)3, v.first};
+                }
+            }
+        }
+        return {out, {}};
     }
 
     // graph.go:1047-1110
     std::pair<std::vector<std::vector<Node<K>>>, Error> BatchSearch(const std::vector<Vector>& queries, int k,
                                                                     int mode = MHNSW_MODE_COMPAT,
-                                                                    bool single = false) {
+                                                                    bool single = false, int ef = 0) {
         sync();
         if (queries.empty()) return {{}, make_error(mhnsw_validate(h_), h_)};
         const size_t d = queries[0].size();
@@ -240,7 +334,7 @@ class Graph {  // graph.go:305-332
         std::vector<int64_t> keys(B * kk);
         std::vector<float> dist(B * kk);
         std::vector<int32_t> n(B);
-        int rc = mhnsw_search(h_, flat.data(), (int64_t)B, (int)d, k, mode, 0, nullptr, keys.data(), dist.data(),
+        int rc = mhnsw_search(h_, flat.data(), (int64_t)B, (int)d, k, mode, ef, nullptr, keys.data(), dist.data(),
                               n.data());
         if (rc < 0) return {{}, make_error(rc, h_)};
         std::vector<std::vector<Node<K>>> out(B);
@@ -320,16 +414,10 @@ class Graph {  // graph.go:305-332
 
    private:
     void create() {
-        int rc = mhnsw_create(MHNSW_COSINE, 16, 0.25, 20, Rng, &h_);
+        int rc = mhnsw_create(MHNSW_COSINE, 16, 0.25, 20, 0, &h_);
         if (rc < 0) throw std::runtime_error(mhnsw_last_error(nullptr));
     }
-    void sync() {
-        mhnsw_set_params(h_, Distance ? Distance->metric : MHNSW_NO_DISTANCE, M, Ml, EfSearch);
-        if (Rng != seeded_) {
-            mhnsw_seed(h_, Rng);
-            seeded_ = Rng;
-        }
-    }
+    void sync() { mhnsw_set_params(h_, Distance ? Distance->metric : MHNSW_NO_DISTANCE, M, Ml, EfSearch); }
     Vector lookup_value(const K& key) {
         auto it = values_.find(key);
         if (it != values_.end()) return it->second;
@@ -339,7 +427,6 @@ class Graph {  // graph.go:305-332
     }
 
     mhnsw_index* h_ = nullptr;
-    uint64_t seeded_ = 0;
     std::map<K, Vector> values_;
 };
 

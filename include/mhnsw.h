@@ -107,6 +107,14 @@ int mhnsw_search(mhnsw_index *h, const float *queries, int64_t B, int dim, int k
                  const int64_t *entry_key, int64_t *out_keys, float *out_dist, int32_t *out_n);
 int mhnsw_search_device(mhnsw_index *h, const float *d_queries, int64_t B, int dim, int k, int mode, int ef,
                         int64_t *d_keys, float *d_dist, int32_t *d_n, void *stream);
+/* Errors of *_device searches.  mhnsw_search_device returns once its kernels
+ * are enqueued, so what they detect (a compat search whose visited set
+ * overflows -- the reference's visited map is exact, graph.go:141-144 -- or an
+ * out-of-range id in the adjacency) cannot be its return value: it accumulates
+ * in a per-handle word.  This call waits for the last enqueued search, returns
+ * MHNSW_OK or MHNSW_EINTERNAL with the message of the host-pointer path, and
+ * clears the word. */
+int mhnsw_device_status(mhnsw_index *h);
 
 /* ---- SearchWithNegative(s) / BatchSearchWithNegatives (graph.go:1116-1537) ----
  * Query b's negatives are the next neg_count[b] rows of `negatives` (B*dim
@@ -160,8 +168,9 @@ int mhnsw_import(mhnsw_index *h, int64_t N, int dim, int L, int cap, const int64
  * written in insertion order and neighbour keys ascending (Go: map order).
  * Import replaces the graph (M, Ml, EfSearch and the distance come from the
  * file) and reports the reference's errors ("unknown distance function %q",
- * "incompatible encoding version: %d", ...).  Save writes path.tmp then
- * renames; Load of a missing or empty file leaves the graph empty. */
+ * "incompatible encoding version: %d", ...).  Save writes a unique temp file
+ * next to path, fsyncs it and renames it over path (renameio, encode.go:320);
+ * Load of a missing or empty file leaves the graph empty. */
 enum { MHNSW_KEY_INT = 0, MHNSW_KEY_INT64 = 1, MHNSW_KEY_INT32 = 2, MHNSW_KEY_UINT64 = 3, MHNSW_KEY_UINT32 = 4,
        MHNSW_KEY_STRING = 5 /* Go string keys: the labels of mhnsw_strkeys_encode */ };
 int mhnsw_export_go(mhnsw_index *h, int key_kind, uint8_t *buf, int64_t cap, int64_t *size);

@@ -7,6 +7,7 @@
 #include <set>
 
 #include "hnsw_amd/graph.hpp"
+#include "oracle.h"  // test infrastructure: the CPU restatement, as the checker only
 
 static int failures = 0;
 #define REQUIRE(cond, name)                                              \
@@ -203,18 +204,157 @@ static void TestGraph_FloatKeys() {
     REQUIRE(g.Delete(-3.25) && g.Len() == 63, "delete float key");
 }
 
+// Graph.Rng (graph.go:312): levels are drawn by the shim from the caller's
+// generator with the reference's rule (graph.go:388-417, layer-0 size growing
+// per insert, through single Adds and one BatchAdd alike); the engine receives
+// them as injected levels.  Replaying the rule with a fresh copy of the same
+// generator and building the oracle with those levels gives the same graph.
+static std::shared_ptr<hnsw::Rand> lcg(uint64_t s) {  // a caller-supplied source, not the engine's stream
+    return std::make_shared<hnsw::FuncRand>([s]() mutable {
+        s = s * 6364136223846793005ull + 1442695040888963407ull;
+        return (double)(s >> 11) * (1.0 / 9007199254740992.0);
+    });
+}
+
+static bool same_graph(mhnsw_index* h, og_graph* o, const char* name) {
+    int64_t N1 = 0, N2 = 0;
+    int d1, d2, L1, L2, c1, c2;
+    mhnsw_export_sizes(h, &N1, &d1, &L1, &c1);
+    og_export_sizes(o, &N2, &d2, &L2, &c2);
+    if (N1 != N2 || L1 != L2 || d1 != d2) {
+        std::printf("FAIL %s: sizes %lld/%lld layers %d/%d\n", name, (long long)N1, (long long)N2, L1, L2);
+        return false;
+    }
+    const int cap = c1 > c2 ? c1 : c2;
+    std::vector<int64_t> k1(N1), k2(N1);
+    std::vector<float> v1((size_t)N1 * d1), v2((size_t)N1 * d1);
+    std::vector<int32_t> g1((size_t)L1 * N1), g2((size_t)L1 * N1), a1((size_t)L1 * N1 * cap), a2((size_t)L1 * N1 * cap);
+    std::vector<int32_t> e1(L1), e2(L1);
+    mhnsw_export(h, k1.data(), v1.data(), g1.data(), a1.data(), cap, e1.data(), nullptr);
+    og_export(o, k2.data(), v2.data(), g2.data(), a2.data(), cap, e2.data(), nullptr);
+    if (k1 != k2 || g1 != g2 || e1 != e2) {
+        std::printf("FAIL %s: keys/degrees/entries differ\n", name);
+        return false;
+    }
+    for (size_t r = 0; r < (size_t)L1 * N1; ++r) {
+        const int dg = g1[r];
+        std::set<int32_t> s1(a1.begin() + r * cap, a1.begin() + r * cap + (dg > 0 ? dg : 0));
+        std::set<int32_t> s2(a2.begin() + r * cap, a2.begin() + r * cap + (dg > 0 ? dg : 0));
+        if (s1 != s2) {
+            std::printf("FAIL %s: adjacency row %zu differs\n", name, r);
+            return false;
+        }
+    }
+    return true;
+}
+
+static void TestGraph_RngLevels() {
+    const int n = 600, d = 16, M = 8;
+    const double ml = 0.3;
+    std::vector<hnsw::Node<int>> nodes;
+    uint64_t x = 12345;
+    for (int i = 0; i < n; ++i) {
+        hnsw::Vector v(d);
+        for (auto& f : v) {
+            x = x * 2862933555777941757ull + 3037000493ull;
+            f = (float)((double)(x >> 40) / (double)(1ull << 24)) * 2.f - 1.f;
+        }
+        nodes.push_back(hnsw::MakeNode(i * 7 - 100, v));
+    }
+    hnsw::Graph<int> g(M, ml, 20, &hnsw::CosineDistance, lcg(99));
+    for (int i = 0; i < 50; ++i) REQUIRE(!g.Add(nodes[(size_t)i]), "RngLevels add");
+    REQUIRE(!g.BatchAdd(std::vector<hnsw::Node<int>>(nodes.begin() + 50, nodes.end())), "RngLevels batch add");
+    // replay graph.go:388-417 with a fresh generator of the same seed
+    auto rng = lcg(99);
+    std::vector<int32_t> lv(n);
+    std::vector<int64_t> keys(n);
+    std::vector<float> flat;
+    for (int i = 0; i < n; ++i) {
+        lv[(size_t)i] = hnsw::randomLevel(*rng, ml, i > 0, i);
+        keys[(size_t)i] = nodes[(size_t)i].Key;
+        flat.insert(flat.end(), nodes[(size_t)i].Value.begin(), nodes[(size_t)i].Value.end());
+    }
+    og_graph* o = og_create(OG_COSINE, OG_ORDER_DEV, M, 0, ml, 20, 0);
+    REQUIRE(og_add(o, keys.data(), flat.data(), n, d, lv.data()) == 0, "RngLevels oracle add");
+    REQUIRE(same_graph(g.handle(), o, "RngLevels"), "RngLevels graph == oracle graph with the caller's levels");
+    std::vector<int> topo;
+    for (int l = 0; l < og_num_layers(o); ++l) topo.push_back((int)og_layer_count(o, l));
+    REQUIRE(g.Topography() == topo && topo.size() >= 3, "RngLevels topography");
+    og_destroy(o);
+    // the seed matters: another generator gives other levels, hence another graph
+    hnsw::Graph<int> g2(M, ml, 20, &hnsw::CosineDistance, lcg(7));
+    REQUIRE(!g2.BatchAdd(nodes), "RngLevels other seed");
+    auto r2 = lcg(7);
+    int differ = 0;
+    for (int i = 0; i < n; ++i) differ += hnsw::randomLevel(*r2, ml, i > 0, i) != lv[(size_t)i];
+    REQUIRE(differ > 0, "RngLevels other seed draws other levels");
+    // SplitMix64Rand(seed) reproduces the engine's own seeded stream
+    hnsw::SplitMix64Rand sm(42);
+    std::vector<int32_t> want(300);
+    mhnsw_index* h = nullptr;
+    mhnsw_create(MHNSW_COSINE, 16, 0.25, 20, 42, &h);
+    mhnsw_preview_levels(h, 300, want.data());
+    mhnsw_destroy(h);
+    bool same = true;
+    for (int i = 0; i < 300; ++i) same = same && hnsw::randomLevel(sm, 0.25, i > 0, i) == want[(size_t)i];
+    REQUIRE(same, "SplitMix64Rand == engine stream");
+}
+
+// graph.go:563-569,595-619 (opt-in): the dog query doubles EfSearch and puts
+// key 3 ("canine") into a 3-result answer that lacks it.  Hand graph (one
+// layer): canine is unreachable, so the plain answer misses it.
+static void TestGraph_DogQueryHack() {
+    hnsw::Graph<int> g(4, 0.5, 20, &hnsw::CosineDistance, 1);
+    const int64_t keys[5] = {1, 2, 3, 4, 5};  // dog, puppy, canine, cat, kitten (negative_test.go:17-23)
+    const float vals[15] = {1.0f, 0.2f, 0.1f, 0.9f, 0.3f, 0.2f, 0.8f, 0.3f, 0.3f, 0.1f, 1.0f, 0.2f, 0.2f, 0.9f, 0.3f};
+    const int32_t deg[5] = {2, 2, 0, 2, 2};
+    int32_t adj[5 * 5];
+    for (int& a : adj) a = -1;
+    adj[0] = 1, adj[1] = 3, adj[5] = 0, adj[6] = 4, adj[15] = 0, adj[16] = 4, adj[20] = 1, adj[21] = 3;
+    const int32_t entry[1] = {0};
+    REQUIRE(mhnsw_import(g.handle(), 5, 3, 1, 5, keys, vals, deg, adj, entry, nullptr) == 0, "DogQuery import");
+    auto keyset = [](const std::vector<hnsw::Node<int>>& v) {
+        std::vector<int> k;
+        for (auto& n : v) k.push_back(n.Key);
+        return k;
+    };
+    auto plain = g.Search({1.0f, 0.2f, 0.1f}, 3);
+    REQUIRE(!plain.second && plain.first.size() == 3, "DogQuery plain len");
+    const std::vector<int> pk = keyset(plain.first);
+    REQUIRE(std::set<int>(pk.begin(), pk.end()).count(3) == 0, "DogQuery plain misses canine");
+    g.TestHacks = hnsw::kDogQueryHack;
+    auto hacked = g.Search({1.0f, 0.2f, 0.1f}, 3);
+    REQUIRE(!hacked.second && hacked.first.size() == 3, "DogQuery hacked len");
+    std::vector<int> want = pk;
+    want[2] = 3;
+    REQUIRE(keyset(hacked.first) == want, "DogQuery canine replaces the last result");
+    REQUIRE(hacked.first[2].Value == hnsw::Vector({0.8f, 0.3f, 0.3f}), "DogQuery canine value");
+    auto other = g.Search({1.0f, 0.2f, 0.1000001f}, 3);  // not the dog query: untouched
+    const std::vector<int> ok = keyset(other.first);
+    REQUIRE(!other.second && std::set<int>(ok.begin(), ok.end()).count(3) == 0, "DogQuery other query untouched");
+}
+
+#define RUN(t)                           \
+    do {                                 \
+        std::printf("RUN %s\n", #t);      \
+        t();                             \
+    } while (0)
+
 int main() {
-    TestDistances();
-    Test_layerNode_search();
-    TestGraph_AddSearch();
-    TestGraph_DefaultCosine();
-    TestGraphValidation();
-    TestDimensionMismatch();
-    TestBatchDelete();
-    TestGraph_AddDelete();
-    TestGraph_ExportImport();
-    TestGraph_StringKeys();
-    TestGraph_FloatKeys();
+    std::setvbuf(stdout, nullptr, _IONBF, 0);  // a crash must not swallow the log
+    RUN(TestDistances);
+    RUN(Test_layerNode_search);
+    RUN(TestGraph_AddSearch);
+    RUN(TestGraph_DefaultCosine);
+    RUN(TestGraphValidation);
+    RUN(TestDimensionMismatch);
+    RUN(TestBatchDelete);
+    RUN(TestGraph_AddDelete);
+    RUN(TestGraph_ExportImport);
+    RUN(TestGraph_StringKeys);
+    RUN(TestGraph_FloatKeys);
+    RUN(TestGraph_RngLevels);
+    RUN(TestGraph_DogQueryHack);
     std::printf("%s (%d failures)\n", failures ? "FAIL" : "PASS", failures);
     return failures;
 }

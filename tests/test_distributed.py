@@ -21,6 +21,12 @@ def _free_port():
     return p
 
 
+def merge_order(d, key):
+    """k_merge's total order: distance (-0 == +0, NaN after +inf), then key."""
+    d = float(d)
+    return (d != d, 0.0 if d != d else d, int(key))
+
+
 def merge_reference(ak, ad, an, k):
     """numpy restatement of k_merge: best k of all shard entries by (dist, key)."""
     S, B = an.shape
@@ -28,7 +34,8 @@ def merge_reference(ak, ad, an, k):
     od = np.full((B, k), np.inf, np.float32)
     on = np.zeros(B, np.int32)
     for b in range(B):
-        cand = sorted((float(ad[s, b, j]), int(ak[s, b, j])) for s in range(S) for j in range(int(an[s, b])))[:k]
+        ents = [(ad[s, b, j], ak[s, b, j]) for s in range(S) for j in range(int(an[s, b]))]
+        cand = sorted(ents, key=lambda e: merge_order(*e))[:k]
         on[b] = len(cand)
         for j, (d, key) in enumerate(cand):
             ok[b, j], od[b, j] = key, d

@@ -283,6 +283,13 @@ def test_merge_topk_device(H):
     dist = np.sort(rng.uniform(0, 1, (S, B, k)).astype(np.float32), axis=2)
     keys = rng.permutation(S * B * k).reshape(S, B, k).astype(np.int64)
     nn = rng.integers(0, k + 1, (S, B)).astype(np.int32)
+    # compat lists carry NaN (zero rows under cosine) and signed zeros; exact ties across shards
+    dist[0, :20, k - 3:] = np.nan
+    dist[1, 20:40, k - 1] = np.nan
+    dist[:, 40:60, 0] = -0.0
+    dist[2, 60:80, 1] = 0.0
+    dist[1, 80:100, :] = dist[0, 80:100, :]
+    nn[:, :100] = k
     dev = torch.device("cuda:0")
     tk, td, tn = (torch.from_numpy(x).to(dev) for x in (keys, dist, nn))
     ok = torch.empty((B, k), dtype=torch.int64, device=dev)
@@ -292,11 +299,13 @@ def test_merge_topk_device(H):
                         on.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     ok, od, on = ok.cpu().numpy(), od.cpu().numpy(), on.cpu().numpy()
+    from tests.test_distributed import merge_reference
+
+    rk, rd, rn = (x.numpy() for x in merge_reference(keys, dist, nn, k))
+    assert np.array_equal(on, rn)
     for b in range(B):
-        cand = sorted((dist[s, b, j], keys[s, b, j]) for s in range(S) for j in range(nn[s, b]))[:k]
-        assert on[b] == len(cand)
-        assert ok[b, : on[b]].tolist() == [c[1] for c in cand]
-        assert od[b, : on[b]].tolist() == [c[0] for c in cand]
+        assert ok[b, : on[b]].tolist() == rk[b, : rn[b]].tolist(), b
+        assert np.array_equal(od[b, : on[b]], rd[b, : rn[b]], equal_nan=True), b
 
 
 # ---------------------------------------------------------------- batched build
