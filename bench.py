@@ -65,8 +65,7 @@ def parse():
     p.add_argument("--keep-pruned", type=int, default=1)
     p.add_argument("--alpha", type=int, default=115, help="heuristic slack x100 (prune_alpha_pct; 100 = HNSW Alg. 4)")
     p.add_argument("--screen", type=int, default=1,
-                   help="screening copies, bit 0 fp16, bit 1 int8 (0: plain f32 evaluation of every "
-                        "candidate); same results")
+                   help="1: fp16 screening copy, 0: plain f32 evaluation of every candidate; same results")
     p.add_argument("--ef-sweep", default="32,48,64,72,80,96,128,256",
                    help="extra operating points (ef values) reported at N=1; '' disables")
     p.add_argument("--seed", type=int, default=1234)
@@ -172,11 +171,14 @@ def main():
     # ---- replica index: rows [0, nbase) on every rank ---------------------------
     shard_only = a.mode == "shard"
 
+    sweep = None
+
     def build(off, rng_seed):
+        nonlocal sweep
         X = gen_vectors(a.nbase, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=off)
         g = H.Graph(M=a.M, Ml=0.25, EfSearch=a.ef, Distance=metric, Rng=rng_seed, build_mode=H.BUILD_BATCH,
                     m0=a.M0, ef_construction=a.efc, heuristic=2, keep_pruned=a.keep_pruned, prune_alpha_pct=a.alpha,
-                    screen=a.screen)
+                    screen=a.screen, time_build=1)
         g.reserve(a.nbase, a.dim)
         keys = np.arange(off, off + a.nbase, dtype=np.int64)
         torch.cuda.synchronize()
@@ -184,8 +186,31 @@ def main():
         g.add_device(keys, X.data_ptr(), a.nbase, a.dim)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        if sweep is None and rank == 0:
+            sweep = sweep_bench(X)
         del X
         return g, dt, g.stats()
+
+    def sweep_bench(X, reps=10):
+        """K1 microbench (SURVEY 8(d)): one query against every row, mhnsw_distance_device;
+        HBM-bound at n*d*4 bytes per sweep, HIP events on the launch stream."""
+        out = torch.empty(X.shape[0], dtype=torch.float32, device=device)
+        q = X[12345].clone()
+        s = torch.cuda.current_stream()
+        H.sweep_device(metric.metric, q.data_ptr(), X.data_ptr(), X.shape[0], a.dim, out.data_ptr(), s.cuda_stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            H.sweep_device(metric.metric, q.data_ptr(), X.data_ptr(), X.shape[0], a.dim, out.data_ptr(),
+                           s.cuda_stream)
+        e1.record(s)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        byts = X.shape[0] * a.dim * 4
+        return {"kernel": "k_sweep_raw4", "rows": X.shape[0], "dim": a.dim, "ms": round(ms, 4),
+                "alg_bytes": byts, "achieved_GBps": round(byts / ms / 1e6, 1),
+                "frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4),
+                "self_distance_zero": bool(abs(float(out[12345])) <= 1e-6)}
 
     qseed = a.seed + 7_777
     ngt = min(a.gt_queries, a.batch)
@@ -270,6 +295,26 @@ def main():
             Q, S = Qs, Searcher(gs, a.batch, a.k, a.dim, device)
             tk, tn = ek, en
 
+    def build_roofline(bs, secs):
+        """Batched insert (configs[2] kernel family, here on the bench index): the
+        search kernels' algorithmic bytes -- f32 rows (4d + 4: row + norm) for every
+        f32 evaluation and neighbour-selection row, fp16 rows (2d) for every screened
+        candidate, one layer-0 adjacency row per expansion, the new row and its
+        adjacency/proposal writes -- over their device time (HIP events)."""
+        F, Sc, Xp = bs["build_f32_rows"], bs["build_screened"], bs["build_expansions"]
+        aux = 8 if a.metric == "euclidean" else 0
+        byts = F * (4 * a.dim + 4) + Sc * (2 * a.dim + aux) + Xp * 4 * (a.M0 + 1) + a.nbase * (4 * a.dim + 16 * a.M0)
+        us = bs["build_search_us"]
+        gbs = byts / (us * 1e-6) / 1e9 if us > 0 else None
+        return {"inserts_per_s": round(a.nbase / secs, 1), "seconds": round(secs, 2),
+                "dist_evals_per_insert": round(bs["build_dist_evals"] / a.nbase, 1),
+                "f32_rows_per_insert": round(F / a.nbase, 1), "screened_per_insert": round(Sc / a.nbase, 1),
+                "expansions_per_insert": round(Xp / a.nbase, 1), "dropped_proposals": bs["dropped_proposals"],
+                "roofline": {"bound": "hbm", "kernel": "k_batch_search + k_batch_descend",
+                             "kernel_ms_total": round(us / 1e3, 2), "alg_bytes": int(byts),
+                             "achieved": round(gbs, 1) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None}}
+
     shard = shard_only
     queries_done = a.batch * a.steps * (1 if shard else world)
     qps = queries_done / elapsed
@@ -282,12 +327,10 @@ def main():
         # one adjacency row per expansion, the query
         E = stats["search_dist_evals"] / launches
         Sc = stats["search_screened"] / launches
-        S8 = stats.get("search_screened_i8", 0) / launches
         F = stats["search_f32_evals"] / launches
         Xp = stats["search_expansions"] / launches
         aux = 8 if a.metric == "euclidean" else 0  # L2 screening reads {unscale, |x|} per row
-        # int8 stage: one byte per dimension + {scale, bound} per screened candidate
-        return (F * (4 * a.dim + 4) + Sc * (2 * a.dim + aux) + S8 * (a.dim + 8) + Xp * 4 * cap0
+        return (F * (4 * a.dim + 4) + Sc * (2 * a.dim + aux) + Xp * 4 * cap0
                 + a.batch * 4 * a.dim, E, Xp, Sc, F)
 
     alg_bytes, E, Xp, Sc, F = alg_bytes_of(st, a.steps)
@@ -349,7 +392,7 @@ def main():
             "n_base": a.nbase * (world if shard else 1), "dim": a.dim, "batch_per_gpu": a.batch, "ef": a.ef,
             "k": a.k, "M": a.M, "M0": a.M0, "ef_construction": a.efc, "keep_pruned": a.keep_pruned,
             "prune_alpha": a.alpha / 100,
-            "screen": ((["", "fp16", "int8", "int8 then fp16"][a.screen]
+            "screen": (("fp16"
                         + " row copy rejects candidates whose f32 distance provably exceeds the list's worst; "
                         "every reported distance is f32, results identical to screen=0") if a.screen else "off"),
             "parallelism": f"{'shard' if shard else 'replica'}{world}",
@@ -362,11 +405,9 @@ def main():
             "alg_bytes_per_launch": int(alg_bytes),
             "dist_evals_per_query": round(E / a.batch, 1), "expansions_per_query": round(Xp / a.batch, 1),
             "screened_per_query": round(Sc / a.batch, 1), "f32_evals_per_query": round(F / a.batch, 1),
-            "int8_screened_per_query": round(st.get("search_screened_i8", 0) / a.steps / a.batch, 1),
         },
-        "build": {"inserts_per_s": round(a.nbase / build_s, 1), "seconds": round(build_s, 2),
-                  "dist_evals_per_insert": round(bstats["build_dist_evals"] / a.nbase, 1),
-                  "dropped_proposals": bstats["dropped_proposals"]},
+        "build": build_roofline(bstats, build_s),
+        "sweep": sweep,
         "cpu_baseline": None,
         "operating_points": points,
         "at_recall_0.99": at99,

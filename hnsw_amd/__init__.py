@@ -9,7 +9,7 @@ from ._lib import (BUILD_BATCH, BUILD_COMPAT, BUILD_FLAT, COSINE, EUCLIDEAN, KEY
                    KEY_UINT64, MODE_BEAM, MODE_COMPAT, MODE_EXACT, HnswError, LIB_PATH, SIGNATURES, load)
 from .graph import (DOG_QUERY_HACK, CosineDistance, DistanceFunc, EuclideanDistance, Graph, LoadSavedGraph, MakeNode,
                     NewGraph, NewGraphWithConfig, Node, RegisterDistanceFunc, SavedGraph, SplitMix64Rand, Vector,
-                    distance_func_to_name, max_level, merge_topk_device, random_level)
+                    distance_func_to_name, max_level, merge_topk_device, random_level, sweep_device)
 from .adapters import ExactAdapter, ExactIndex, HNSWAdapter
 
 __all__ = [
@@ -17,5 +17,5 @@ __all__ = [
     "LIB_PATH", "SIGNATURES", "load", "CosineDistance", "DistanceFunc", "EuclideanDistance", "Graph", "MakeNode",
     "NewGraph", "NewGraphWithConfig", "Node", "RegisterDistanceFunc", "Vector", "distance_func_to_name",
     "merge_topk_device", "KEY_INT", "KEY_INT32", "KEY_INT64", "KEY_UINT32", "KEY_UINT64", "LoadSavedGraph",
-    "SavedGraph", "DOG_QUERY_HACK", "SplitMix64Rand", "max_level", "random_level",
+    "SavedGraph", "sweep_device", "DOG_QUERY_HACK", "SplitMix64Rand", "max_level", "random_level",
 ]

@@ -67,12 +67,17 @@ struct mhnsw_index {
     int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
     int vis_log2 = 12;
     int exact_kk = 0;
-    int exact_precision = 2;  // scores: 0 f32-input MFMA, 1 bf16x3 split, 2 fp16 2-product split (all certified)
+    int exact_precision = 3;  // scores: 0 f32-input MFMA, 1 bf16x3 split, 2 fp16 2-product split,
+                              // 3 fp16 1-product with the fused preselection (all certified, same results)
     int exact_tile = 0;       // bf16x3 GEMM tile variant (exact.hip launch_exact_scores_x3)
     int compat_waves = 8;     // compat insert: waves scoring each distance batch (1 = the walking wave alone)
     int upper_ef = 1;         // beam search: upper-layer descent width
-    int screen = 1;           // beam search screening copies (results unchanged): bit 0 fp16, bit 1 int8
+    int screen = 1;           // beam search / batched insert fp16 screening copy (results unchanged)
     int fuse_descent = 1;     // batched insert: all greedy descents of a batch in one launch (same graph)
+    int time_build = 0;       // batched insert: time its search kernels with HIP events (stats [12])
+    std::vector<hipEvent_t> tev;  // event pairs around the timed launches of the current Add
+    size_t tev_used = 0;
+    double build_search_us = 0;
     // shape
     int dim = 0, pitch = 0, lpr = 0, vpl = 0;
     bool layers_exist = false;
@@ -85,8 +90,7 @@ struct mhnsw_index {
     uint16_t* h16 = nullptr;  // fp16 screening copy [capn * pitch] (screen = 1)
     float2* h16aux = nullptr;  // [capn] L2 screening {unscale, |x|}
     int h16_metric = -1;       // metric the copies were written for
-    int8_t* i8 = nullptr;      // int8 screening copy [capn * pitch] (screen bit 1)
-    float2* i8aux = nullptr;   // [capn] {scale, |error| bound}
+    float* h16err = nullptr;   // [1] the copy's measured max relative rounding (screening margin)
     int64_t* keys = nullptr;
     int32_t* levels = nullptr;
     uint8_t* dead = nullptr;  // [capn] deleted rows (graph.go:843-864)
@@ -130,6 +134,12 @@ struct mhnsw_index {
     int xsplit_kind = 0;                        // 1: bf16 hi/lo planes, 2: fp16 hi plane + xinv (exact_precision)
     DevBuf<float> xinv, qinv;                   // exact_precision 2: per-row / per-query unscale
     DevBuf<float> xerr;                         // ... and the rows' max relative fp16 rounding
+    // exact_precision 3 (fp16 1-product, fused preselection): sample thresholds,
+    // filter constants, tile regions + counts, per-query buckets, the queries' rounding
+    DevBuf<float> h1thr, h1c, h1s, qerr;
+    DevBuf<uint2> h1region, h1bucket;
+    DevBuf<int32_t> h1rcnt, h1qcnt;
+    DevBuf<uint8_t> h1ovf;
     DevBuf<float> xbound, xmaxn, xsegd;
     DevBuf<uint32_t> xsegi;
     DevBuf<uint8_t> xflag;
@@ -314,10 +324,6 @@ int ensure_capacity(mhnsw_index* h, int64_t need) {
         if ((r = grow(h, h->h16, oc * h->pitch, nc * h->pitch, 0))) return r;
         if ((r = grow(h, h->h16aux, oc, nc, 0xFF))) return r;
     }
-    if (h->screen & 2) {
-        if ((r = grow(h, h->i8, oc * h->pitch, nc * h->pitch, 0))) return r;
-        if ((r = grow(h, h->i8aux, oc, nc, 0xFF))) return r;
-    }
     if ((r = grow(h, h->keys, oc, nc, 0))) return r;
     if ((r = grow(h, h->levels, oc, nc, 0))) return r;
     if ((r = grow(h, h->dead, oc, nc, 0))) return r;
@@ -369,9 +375,8 @@ GraphDev graph_view(const mhnsw_index* h) {
     g.dead = h->any_dead ? h->dead : nullptr;
     g.h16 = (h->screen & 1) ? h->h16 : nullptr;
     g.h16aux = h->h16aux;
-    g.i8 = (h->screen & 2) ? h->i8 : nullptr;
-    g.i8aux = h->i8aux;
-    if (h->h16_metric != h->metric) g.h16 = nullptr, g.i8 = nullptr;  // stale format: no screening
+    g.h16err = h->h16err;
+    if (h->h16_metric != h->metric) g.h16 = nullptr;  // stale format: no screening
     return g;
 }
 
@@ -525,14 +530,31 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         a.touched_cnt = h->touched_cnt;
         a.stats = h->d_stats + 4;
         a.vis_log2 = h->vis_log2;
+        // time_build: HIP events around the search launches (descent + layer searches)
+        auto tmark = [&]() -> int {
+            if (!h->time_build) return 0;
+            if (h->tev_used == h->tev.size()) {
+                hipEvent_t e;
+                HIPCHK(h, hipEventCreate(&e));
+                h->tev.push_back(e);
+            }
+            HIPCHK(h, hipEventRecord(h->tev[h->tev_used++], h->stream));
+            return 0;
+        };
         if (fuse) {
-            if (l == top) LCHK(h, launch_build_batch_descend(a, h->lpr, h->vpl, h->stream));  // a.layer = top
+            if (l == top) {
+                if ((r = tmark())) return r;
+                LCHK(h, launch_build_batch_descend(a, h->lpr, h->vpl, h->stream));  // a.layer = top
+                if ((r = tmark())) return r;
+            }
             if (l > maxlvl) continue;
             a.order = h->border.p;
             a.count = count[std::min(l, MH_MAXL)];
         }
         HIPCHK(h, hipMemsetAsync(h->touched_cnt, 0, 4, h->stream));
+        if ((r = tmark())) return r;
         LCHK(h, launch_build_batch_search(a, h->lpr, h->vpl, h->stream));
+        if ((r = tmark())) return r;
         if (maxlvl >= l) LCHK(h, launch_build_batch_commit(a, h->lpr, h->vpl, (a1 - a0) * mcap, h->stream));
     }
     return 0;
@@ -588,12 +610,14 @@ int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1, int top, uint32_t en
 
 // (re)write the fp16 screening copy of rows [r0, r1) for the current metric
 int h16_rows(mhnsw_index* h, int64_t r0, int64_t r1) {
-    if (!(h->screen & 1 && h->h16) && !(h->screen & 2 && h->i8)) return 0;
+    if (!(h->screen & 1 && h->h16)) return 0;
     if (h->h16_metric != h->metric && r0 > 0) r0 = 0;  // format change: every row
     if (h->screen & 1 && h->h16)
-        LCHK(h, launch_h16_rows(h->vecs, h->norms, r0, r1, h->pitch, h->metric, h->h16, h->h16aux, h->stream));
-    if (h->screen & 2 && h->i8)
-        LCHK(h, launch_i8_rows(h->vecs, h->norms, r0, r1, h->pitch, h->metric, h->i8, h->i8aux, h->stream));
+    {
+        if (r0 == 0) HIPCHK(h, hipMemsetAsync(h->h16err, 0, sizeof(float), h->stream));  // whole copy rewritten
+        LCHK(h, launch_h16_rows(h->vecs, h->norms, r0, r1, h->pitch, h->metric, h->h16, h->h16aux, h->h16err,
+                                h->stream));
+    }
     h->h16_metric = h->metric;
     return 0;
 }
@@ -693,6 +717,12 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     else
         r = run_build_batch(h, n0, n1, top_live, entry_live);
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    for (size_t i = 0; i + 1 < h->tev_used; i += 2) {
+        float ms = 0.f;
+        HIPCHK(h, hipEventElapsedTime(&ms, h->tev[i], h->tev[i + 1]));
+        h->build_search_us += ms * 1e3;
+    }
+    h->tev_used = 0;
     return r;
 }
 
@@ -786,7 +816,9 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
     if (mode == MHNSW_MODE_EXACT) {
         if (k > 256) return fail(h, MHNSW_EUNSUPPORTED, "exact mode supports k <= 256");
         const bool split = h->exact_precision != 0;
-        const bool h2 = h->exact_precision == 2;
+        // fp16 1-product with the fused preselection (needs one full sample tile of rows)
+        const bool h1 = h->exact_precision == 3 && h->n >= H1_BN;
+        const bool h2 = h->exact_precision >= 2;  // fp16 row plane (1- and 2-product)
         // preselect width: the fp16 2-product scores carry a ~2x larger error bound, so the
         // kk-th score must sit further from the k-th distance for the certificate
         const int kk = h->exact_kk > 0 ? std::min(256, std::max(h->exact_kk, k))
@@ -801,11 +833,45 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             (r = ensure_buf(h, h->xnflag, 1)) || (r = ensure_buf(h, h->xmaxn, 1)))
             return r;
         // selection: enough (query, row-segment) waves to stream the score rows at full rate
-        int nseg = (int)std::min<int64_t>(16, std::max<int64_t>(1, (16384 + qc - 1) / qc));
-        nseg = (int)std::max<int64_t>(1, std::min<int64_t>(nseg, (h->n + 4095) / 4096));
-        nseg = std::max(1, std::min(nseg, 1024 / kk));  // merge holds nseg * kk entries
-        const int64_t seglen = ((h->n + nseg - 1) / nseg + 1023) / 1024 * 1024;
+        auto segs = [&](int64_t rows, int& ns, int64_t& sl) {
+            ns = (int)std::min<int64_t>(16, std::max<int64_t>(1, (16384 + qc - 1) / qc));
+            ns = (int)std::max<int64_t>(1, std::min<int64_t>(ns, (rows + 4095) / 4096));
+            ns = std::max(1, std::min(ns, 1024 / kk));  // merge holds nseg * kk entries
+            sl = ((rows + ns - 1) / ns + 1023) / 1024 * 1024;
+        };
+        int nseg;
+        int64_t seglen;
+        segs(h->n, nseg, seglen);
         if ((r = ensure_buf(h, h->xsegd, (size_t)qc * nseg * kk)) || (r = ensure_buf(h, h->xsegi, (size_t)qc * nseg * kk)))
+            return r;
+        // fused preselection (h1): the sample = every stride-th full row tile (about 32
+        // tiles), its J-th best score per query is the threshold (J = kk when the
+        // sample is every tile); a row passes at a rate of ~J / sample rows
+        const int bm = h1_tile_bm(h->exact_tile);
+        const int64_t nnt = (h->n + H1_BN - 1) / H1_BN, nqt = (qc + bm - 1) / bm;
+        const int stride = (int)std::max<int64_t>(1, std::min<int64_t>(128, nnt / 32));
+        const int64_t nsamp = h1 ? ((h->n / H1_BN) - 1) / stride + 1 : 0;  // sampled full tiles
+        const int J = stride >= 8 ? std::max(k, kk / 4) : kk;
+        int sseg = 1;
+        int64_t sseglen = 0;
+        if (h1) {
+            segs(nsamp * H1_BN, sseg, sseglen);
+            sseg = std::max(1, std::min(sseg, 1024 / J));
+        }
+        // pairs per tile region / per query sub-bucket: 4x what the threshold lets
+        // through on average (~J N / ns per query, ~bm J BN / ns per tile), with floors
+        const int64_t ns = std::max<int64_t>(1, nsamp * H1_BN);
+        const int rcap = (int)std::min<int64_t>((int64_t)bm * H1_BN, std::max<int64_t>(2048, 4 * bm * J * H1_BN / ns));
+        const int scap = (int)std::min<int64_t>(std::max<int64_t>(h->n, 1),
+                                                std::max<int64_t>(512, 8 * J * h->n / ns / H1_BSUB));
+        if (h1 && ((r = ensure_buf(h, h->h1thr, (size_t)qc)) || (r = ensure_buf(h, h->h1c, (size_t)nqt * bm + 256)) ||
+                   (r = ensure_buf(h, h->h1s, (size_t)nqt * bm + 256)) ||
+                   (r = ensure_buf(h, h->h1region, (size_t)nqt * nnt * rcap)) ||
+                   (r = ensure_buf(h, h->h1rcnt, (size_t)nqt * nnt)) ||
+                   (r = ensure_buf(h, h->h1qcnt, (size_t)qc * H1_BSUB * H1_CSTRIDE)) || (r = ensure_buf(h, h->h1ovf, (size_t)qc)) ||
+                   (r = ensure_buf(h, h->h1bucket, (size_t)qc * H1_BSUB * scap)) || (r = ensure_buf(h, h->qerr, 1)) ||
+                   (r = ensure_buf(h, h->xsegd, (size_t)qc * sseg * J)) ||
+                   (r = ensure_buf(h, h->xsegi, (size_t)qc * sseg * J))))
             return r;
         if (split) {
             const int64_t plane = h->capn * h->pitch;
@@ -829,12 +895,14 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         // order of n-term f32 summation relative to the sum of magnitudes)
         const double u = std::ldexp(1.0, -24);
         auto gam = [&](double nn) { return nn * u / (1.0 - nn * u); };
-        // products per element: f32 1, bf16x3 3, fp16 2-product 2.  Split error: bf16x3
-        // drops ql.xl and the planes' tails (3.02 * 2^-16); fp16 2-product rounds the
-        // rows to fp16 (2^-11 |x|, Cauchy-Schwarz) and the queries to hi + lo (2^-21)
-        const double g_mfma = gam((h2 ? 2.0 : split ? 3.0 : 1.0) * h->pitch + 1);
-        // (fp16: the rows' part is the measured max |x' - x| / |x| <= 2^-11, added on the device)
-        const double e_split = h2 ? std::ldexp(1.0, -21) : split ? 3.02 * std::ldexp(1.0, -16) : 0.0;
+        // products per element: f32 1, bf16x3 3, fp16 2-product 2, fp16 1-product 1.  Split
+        // error: bf16x3 drops ql.xl and the planes' tails (3.02 * 2^-16); fp16 2-product
+        // rounds the rows to fp16 (2^-11 |x|, Cauchy-Schwarz) and the queries to hi + lo
+        // (2^-21); fp16 1-product rounds both once
+        const double g_mfma = gam((h1 ? 1.0 : h2 ? 2.0 : split ? 3.0 : 1.0) * h->pitch + 1);
+        // (fp16: the rows' part -- and the queries' in the 1-product -- is the measured
+        // max |x' - x| / |x| <= 2^-11, added on the device)
+        const double e_split = h1 ? 0.0 : h2 ? std::ldexp(1.0, -21) : split ? 3.02 * std::ldexp(1.0, -16) : 0.0;
         const double g_can = gam(4.0 * h->vpl + 8);  // canonical: 4*VPL fmaf per lane + 6 butterfly levels
         CertArgs cert{};
         cert.qnorm = h->qnorm.p;
@@ -847,6 +915,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         cert.nflag = h->xnflag.p;
         cert.stats = h->d_stats + 3;
         cert.xerr = h2 ? h->xerr.p : nullptr;
+        cert.qerr = h1 ? h->qerr.p : nullptr;
         if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
         if (split && h->xsplit_rows < h->n) {
             uint16_t* xh = h->xsplit.p;
@@ -897,7 +966,39 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
                 a.Qh = h->qsplit.p;
                 a.Ql = h->qsplit.p + (size_t)qc * h->pitch;
                 a.ldQs = qc;
-                if (h2) {
+                if (h1) {
+                    a.xinv = h->xinv.p;
+                    a.qinv = h->qinv.p;
+                    HIPCHK(h, hipMemsetAsync(h->qerr.p, 0, sizeof(float), s));
+                    LCHK(h, launch_split_h16(a.Q, 0, nb, h->pitch, qc, h->qsplit.p, nullptr, h->qinv.p, h->qerr.p, s));
+                    // 1. sample: every score of the sampled row tiles -> the kk-th best per query
+                    ExactArgs as = a;
+                    as.tile_stride = stride;
+                    as.nsample_tiles = nsamp;
+                    as.ldS = nsamp * H1_BN;
+                    LCHK(h, launch_h1_sample(as, h->exact_tile, s));
+                    as.N = nsamp * H1_BN;
+                    as.kk = J;
+                    as.nseg = sseg;
+                    as.seglen = sseglen;
+                    as.bound = h->h1thr.p;
+                    LCHK(h, launch_exact_select(as, s));
+                    // 2. the full GEMM keeps the pairs that can beat it; 3. per-query buckets; 4. top-kk
+                    LCHK(h, launch_ring_prep(h->h1thr.p, a.qnorm, a.qinv, nb, h->metric, h->h1c.p, h->h1s.p, s));
+                    HIPCHK(h, hipMemsetAsync(h->h1qcnt.p, 0, (size_t)nb * H1_BSUB * H1_CSTRIDE * 4, s));
+                    HIPCHK(h, hipMemsetAsync(h->h1ovf.p, 0, (size_t)nb, s));
+                    a.tile_stride = 1;
+                    a.ring_c = h->h1c.p;
+                    a.ring_s = h->h1s.p;
+                    a.region = h->h1region.p;
+                    a.region_cnt = h->h1rcnt.p;
+                    a.rcap = rcap;
+                    LCHK(h, launch_h1_filter(a, h->exact_tile, s));
+                    const int64_t bqt = (nb + bm - 1) / bm;
+                    LCHK(h, launch_bucket(h->h1region.p, h->h1rcnt.p, rcap, bqt * nnt, bqt, bm, H1_BN, nb, h->h1qcnt.p,
+                                          h->h1bucket.p, scap, h->h1ovf.p, s));
+                    LCHK(h, launch_select_bucket(a, h->h1qcnt.p, h->h1bucket.p, scap, h->h1ovf.p, h->h1thr.p, s));
+                } else if (h2) {
                     a.xinv = h->xinv.p;
                     a.qinv = h->qinv.p;
                     LCHK(h, launch_split_h16(a.Q, 0, nb, h->pitch, qc, h->qsplit.p, h->qsplit.p + (size_t)qc * h->pitch,
@@ -911,7 +1012,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             } else {
                 LCHK(h, launch_exact_scores(a, s));
             }
-            LCHK(h, launch_exact_select(a, s));
+            if (!h1) LCHK(h, launch_exact_select(a, s));
             HIPCHK(h, hipMemsetAsync(h->xnflag.p, 0, sizeof(int32_t), s));
             CertArgs c1 = cert;
             c1.bound = h->xbound.p;
@@ -1005,7 +1106,8 @@ int mhnsw_create(int metric, int M, double ml, int ef_search, uint64_t seed, mhn
         return fail(nullptr, MHNSW_EDEVICE, "no HIP device available");
     }
     if (hipMalloc(&h->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&h->d_err, 2 * sizeof(int)) != hipSuccess || hipMemset(h->d_err, 0, 2 * sizeof(int)) != hipSuccess || hipMalloc(&h->touched_cnt, 16) != hipSuccess ||
+        hipMalloc(&h->d_err, 2 * sizeof(int)) != hipSuccess || hipMemset(h->d_err, 0, 2 * sizeof(int)) != hipSuccess ||
+        hipMalloc(&h->h16err, sizeof(float)) != hipSuccess || hipMemset(h->h16err, 0, sizeof(float)) != hipSuccess || hipMalloc(&h->touched_cnt, 16) != hipSuccess ||
         hipMalloc(&h->d_layer_entry, MH_MAXL * 4) != hipSuccess ||
         hipMalloc(&h->d_layers, MH_MAXL * sizeof(LayerDev)) != hipSuccess || hipEventCreate(&h->ev0) != hipSuccess ||
         hipEventCreate(&h->ev1) != hipSuccess || hipEventCreateWithFlags(&h->scr_ev, hipEventDisableTiming) != hipSuccess ||
@@ -1029,8 +1131,6 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->norms);
     F(h->h16);
     F(h->h16aux);
-    F(h->i8);
-    F(h->i8aux);
     F(h->keys);
     F(h->levels);
     F(h->dead);
@@ -1044,6 +1144,7 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->d_layers);
     F(h->d_stats);
     F(h->d_err);
+    F(h->h16err);
     for (auto& L : h->layers) {
         F(L.deg);
         F(L.adj);
@@ -1072,6 +1173,15 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->xinv.p);
     F(h->qinv.p);
     F(h->xerr.p);
+    F(h->h1thr.p);
+    F(h->h1c.p);
+    F(h->h1s.p);
+    F(h->qerr.p);
+    F(h->h1region.p);
+    F(h->h1bucket.p);
+    F(h->h1rcnt.p);
+    F(h->h1qcnt.p);
+    F(h->h1ovf.p);
     F(h->qsplit.p);
     F(h->xbound.p);
     F(h->xsegd.p);
@@ -1084,6 +1194,7 @@ void mhnsw_destroy(mhnsw_index* h) {
     if (h->meta_ev) (void)hipEventDestroy(h->meta_ev);
     if (h->ord_ev) (void)hipEventDestroy(h->ord_ev);
     if (h->ord_pin) (void)hipHostFree(h->ord_pin);
+    for (auto e : h->tev) (void)hipEventDestroy(e);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1163,8 +1274,10 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "fuse_descent") {
         if (v != 0 && v != 1) return fail(h, MHNSW_EINVAL, "fuse_descent must be 0 or 1");
         h->fuse_descent = (int)v;
+    } else if (n == "time_build") {
+        h->time_build = (int)(v != 0);
     } else if (n == "screen") {
-        if (v < 0 || v > 3) return fail(h, MHNSW_EINVAL, "screen must be in [0, 3]");
+        if (v < 0 || v > 1) return fail(h, MHNSW_EINVAL, "screen must be 0 or 1");
         if ((int)v == h->screen) return MHNSW_OK;
         int r = drain(h);
         if (r) return r;
@@ -1175,14 +1288,10 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
         };
         F(h->h16);
         F(h->h16aux);
-        F(h->i8);
-        F(h->i8aux);
         h->h16_metric = -1;
         h->screen = (int)v;
-        if (v && h->capn > 0) {  // rewrite the selected copies
-            if (v & 1 && ((r = grow(h, h->h16, 0, h->capn * h->pitch, 0)) || (r = grow(h, h->h16aux, 0, h->capn, 0xFF))))
-                return r;
-            if (v & 2 && ((r = grow(h, h->i8, 0, h->capn * h->pitch, 0)) || (r = grow(h, h->i8aux, 0, h->capn, 0xFF))))
+        if (v && h->capn > 0) {  // rewrite the copy
+            if ((r = grow(h, h->h16, 0, h->capn * h->pitch, 0)) || (r = grow(h, h->h16aux, 0, h->capn, 0xFF)))
                 return r;
             if ((r = h16_rows(h, 0, h->n))) return r;
             HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -1191,8 +1300,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
         if (v != 1 && v != 8) return fail(h, MHNSW_EINVAL, "compat_waves must be 1 or 8");
         h->compat_waves = (int)v;
     } else if (n == "exact_precision") {
-        if (v < 0 || v > 2)
-            return fail(h, MHNSW_EINVAL, "exact_precision must be 0 (f32), 1 (bf16x3) or 2 (fp16 2-product)");
+        if (v < 0 || v > 3)
+            return fail(h, MHNSW_EINVAL,
+                        "exact_precision must be 0 (f32), 1 (bf16x3), 2 (fp16 2-product) or 3 (fp16 1-product, fused)");
         h->exact_precision = (int)v;
     } else {
         return fail(h, MHNSW_EINVAL, "unknown option '%s'", n.c_str());
@@ -1220,6 +1330,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "upper_ef") *v = h->upper_ef;
     else if (n == "screen") *v = h->screen;
     else if (n == "fuse_descent") *v = h->fuse_descent;
+    else if (n == "time_build") *v = h->time_build;
     else if (n == "strkey_relabels") *v = h->relabels;
     else if (n == "strkeys") *v = (int64_t)h->s2l.size();
     else if (n == "pitch") *v = h->pitch;
@@ -1396,8 +1507,6 @@ void reset_graph(mhnsw_index* h) {
     F(h->norms);
     F(h->h16);
     F(h->h16aux);
-    F(h->i8);
-    F(h->i8aux);
     F(h->keys);
     F(h->levels);
     F(h->dead);
@@ -2000,9 +2109,10 @@ int mhnsw_stats(const mhnsw_index* h, int64_t* out, int n) {
     HIPCHK(hh, hipMemcpy(err2, h->d_err, sizeof(err2), hipMemcpyDeviceToHost));
     const int err = err2[0] | err2[1];
     if (err & 4) return fail(hh, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
-    const int64_t v[11] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4], (int64_t)d[5], (int64_t)d[6],
-                           h->stats_host[6], (int64_t)d[3], (int64_t)d[8], (int64_t)d[9], (int64_t)d[10]};
-    for (int i = 0; i < n && i < 11; ++i) out[i] = v[i];
+    const int64_t v[13] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4], (int64_t)d[5], (int64_t)d[6],
+                           h->stats_host[6], (int64_t)d[3], (int64_t)d[8], (int64_t)d[9], (int64_t)d[10],
+                           (int64_t)d[11], (int64_t)h->build_search_us};
+    for (int i = 0; i < n && i < 13; ++i) out[i] = v[i];
     return 0;
 }
 
@@ -2010,6 +2120,7 @@ int mhnsw_reset_stats(mhnsw_index* h) {
     HIPCHK(h, hipDeviceSynchronize());
     HIPCHK(h, hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)));
     for (auto& v : h->stats_host) v = 0;
+    h->build_search_us = 0;
     return 0;
 }
 

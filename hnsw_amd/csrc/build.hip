@@ -590,6 +590,8 @@ __global__ __launch_bounds__(64) void k_batch_descend(BatchBuildArgs a) {
         a.cur_entry[u] = ep;
         atomicAdd(&a.stats[0], st.E);
         atomicAdd(&a.stats[1], st.X);
+        atomicAdd(&a.stats[6], st.S);
+        atomicAdd(&a.stats[7], st.F);
     }
 }
 
@@ -644,6 +646,7 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
                 load_query(qc, a.g.vecs + (size_t)c * a.g.pitch);
                 const float cn = a.g.norms[c];
                 st.E += nsel;
+                st.F += nsel + 1;  // the candidate's row and the kept rows, in f32
                 eval_list<C, G>(a.g, qc, cn, sel, nsel, a.g.metric, [&](float dcs, uint32_t) {
                     if (a.alpha * dcs < dc) good = false;
                 });
@@ -693,6 +696,8 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
     if (lane == 0) {
         atomicAdd(&a.stats[0], st.E);
         atomicAdd(&a.stats[1], st.X);
+        atomicAdd(&a.stats[6], st.S);
+        atomicAdd(&a.stats[7], st.F);
     }
 }
 
@@ -979,7 +984,7 @@ static int launch_batch_descend_t(const BatchBuildArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 << a.vis_log2;
     const int64_t n = a.n1 - a.n0;
     if (n <= 0) return 0;
-    if (a.g.h16 || a.g.i8)
+    if (a.g.h16)
         hipLaunchKernelGGL((k_batch_descend<C, G, true>), dim3((unsigned)n), dim3(64), lds, s, a);
     else
         hipLaunchKernelGGL((k_batch_descend<C, G, false>), dim3((unsigned)n), dim3(64), lds, s, a);
@@ -991,7 +996,7 @@ static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 << a.vis_log2;
     const int64_t n = a.order ? a.count : a.n1 - a.n0;
     if (n <= 0) return 0;
-    if (a.g.h16 || a.g.i8)  // fp16 screening: same graph, fewer bytes per candidate
+    if (a.g.h16)  // fp16 screening: same graph, fewer bytes per candidate
         hipLaunchKernelGGL((k_batch_search<C, R, G, true>), dim3((unsigned)n), dim3(64), lds, s, a);
     else
         hipLaunchKernelGGL((k_batch_search<C, R, G, false>), dim3((unsigned)n), dim3(64), lds, s, a);

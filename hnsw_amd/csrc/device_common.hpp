@@ -58,13 +58,9 @@ struct GraphDev {
     //           h16aux[r] = {2^-e, |x|}, NaN 2^-e marks a never-rejected row
     const uint16_t* h16;      // [cap_nodes * pitch]
     const float2* h16aux;     // [cap_nodes] (L2)
-    // int8 screening copy (nullptr = off), the first and cheapest screen
-    // ("The int8 screening copy"):
-    //   row r is q8 = round(y / s_r) with y = x / |x| (cosine) or x (L2), and
-    //   i8aux[r] = {s_r, e_r}: e_r >= |s_r q8 - y|_2 (an upper bound computed
-    //   when the row is written); NaN s_r marks a never-rejected row
-    const int8_t* i8;         // [cap_nodes * pitch]
-    const float2* i8aux;      // [cap_nodes]
+    // [1] max over the copy's rows of the measured relative rounding |y' - y| / |y|
+    // (<= 2^-11 by construction; replaces 2^-11 in the screening bounds)
+    const float* h16err;
 };
 
 __device__ __forceinline__ bool is_dead(const GraphDev& g, uint32_t id) { return g.dead && g.dead[id]; }
@@ -325,86 +321,16 @@ __device__ __forceinline__ float eval_rows_h16(const QReg<C>& q, const uint16_t*
     return reduce_rows<G, C::LPR>(p);
 }
 
-// Approximate sums from the int8 screening copy.  Its rows are stored
-// lane-contiguous: the 4*VPL bytes lane `sub` needs (elements sub*4 + v*LPR*4
-// + j, the same elements as in eval_rows) sit at bytes [sub*4*VPL, (sub+1)*4*VPL)
-// of the row, so one row is one dwordx{VPL} load per lane (i8_offset).
-// Dot: sum q_i * q8_i (the caller applies the row's scale).  L2: sum (q_i -
-// q8_i * sc_g)^2.
-__host__ __device__ constexpr int i8_vpl(int pitch) { return pitch >= 256 ? pitch / 256 : 1; }
-template <int VPL>
-__device__ __forceinline__ void load_i8(const int8_t* rp, int (&x)[VPL]) {
-    const int* p = reinterpret_cast<const int*>(rp);  // 4-byte aligned
-    if constexpr (VPL % 4 == 0) {
-#pragma unroll
-        for (int v = 0; v < VPL; v += 4) {
-            const int4 t = *reinterpret_cast<const int4*>(p + v);
-            x[v] = t.x, x[v + 1] = t.y, x[v + 2] = t.z, x[v + 3] = t.w;
-        }
-    } else if constexpr (VPL % 3 == 0) {
-        typedef int i3 __attribute__((ext_vector_type(3)));
-#pragma unroll
-        for (int v = 0; v < VPL; v += 3) {
-            const i3 t = *reinterpret_cast<const i3*>(p + v);
-            x[v] = t.x, x[v + 1] = t.y, x[v + 2] = t.z;
-        }
-    } else if constexpr (VPL % 2 == 0) {
-#pragma unroll
-        for (int v = 0; v < VPL; v += 2) {
-            const int2 t = *reinterpret_cast<const int2*>(p + v);
-            x[v] = t.x, x[v + 1] = t.y;
-        }
-    } else {
-#pragma unroll
-        for (int v = 0; v < VPL; ++v) x[v] = p[v];
-    }
-}
-template <class C, int G, bool L2>
-__device__ __forceinline__ float eval_rows_i8(const QReg<C>& q, const int8_t* __restrict__ I, int pitch,
-                                              const uint32_t (&ids)[G], const bool (&valid)[G],
-                                              const float (&sc)[G]) {
-    const int sub = lane_id() & (C::LPR - 1);
-    int x[G][C::VPL];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        if (valid[g]) {
-            load_i8<C::VPL>(I + (size_t)ids[g] * (size_t)pitch + sub * 4 * C::VPL, x[g]);
-        } else {
-#pragma unroll
-            for (int v = 0; v < C::VPL; ++v) x[g][v] = 0;
-        }
-    }
-    float p[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        float acc = 0.f;
-#pragma unroll
-        for (int v = 0; v < C::VPL; ++v) {
-            const int w = x[g][v];
-            const float x0 = (float)((w << 24) >> 24), x1 = (float)((w << 16) >> 24);
-            const float x2 = (float)((w << 8) >> 24), x3 = (float)(w >> 24);
-            if (L2) {
-                const float t0 = fmaf(x0, sc[g], -q.v[v].x), t1 = fmaf(x1, sc[g], -q.v[v].y);
-                const float t2 = fmaf(x2, sc[g], -q.v[v].z), t3 = fmaf(x3, sc[g], -q.v[v].w);
-                acc = fmaf(t0, t0, acc);
-                acc = fmaf(t1, t1, acc);
-                acc = fmaf(t2, t2, acc);
-                acc = fmaf(t3, t3, acc);
-            } else {
-                acc = fmaf(x0, q.v[v].x, acc);
-                acc = fmaf(x1, q.v[v].y, acc);
-                acc = fmaf(x2, q.v[v].z, acc);
-                acc = fmaf(x3, q.v[v].w, acc);
-            }
-        }
-        p[g] = acc;
-    }
-    return reduce_rows<G, C::LPR>(p);
-}
+// Lane-contiguous row copies (the fp16 screening copy, eval_rows_h16): the
+// 4*VPL elements lane `sub` needs (sub*4 + v*LPR*4 + j, the same elements as
+// in eval_rows) are adjacent, so a lane's part of a row is one or two loads.
+__host__ __device__ constexpr int lc_vpl(int pitch) { return pitch >= 256 ? pitch / 256 : 1; }
 
 // Screening bounds ("The fp16 screening copy"), with y the row the fp16 copy stands for
-// (x / |x|_f32 for cosine, x for L2) and |y' - y| <= 2^-11 |y| (+ 2u from the
-// cosine normalisation, + a subnormal term far below 2^-30 |y|):
+// (x / |x|_f32 for cosine, x for L2) and |y' - y| <= E |y|, E = the measured
+// maximum over the copy's rows (k_h16_rows, f64, rounded up; it includes the
+// cosine normalisation), at most 2^-11 (+ 2u) -- the bounds below are written
+// with 2^-11, the kernels use E:
 //   cosine: |S / |q|_f32 - (the f32 cosine term)| <= 2^-11 + 2 gamma + 8u
 //           (Cauchy-Schwarz; gamma = accumulation bound of one f32 dot,
 //           < 2^-18 for dim <= 4096), so approx > wd + 2^-11 + 2^-16 => f32 > wd
@@ -421,31 +347,16 @@ __device__ __forceinline__ bool h16_query_ok(float qn) {
     return qn >= 9.094947017729282e-13f && qn <= 1.099511627776e12f;  // [2^-40, 2^40]; false for NaN
 }
 // true when the f32 distance of this row is certainly > wd (s: eval_rows_h16 sum)
-__device__ __forceinline__ bool h16_rejects_cos(float s, float qn, float wd) {
+// margins for a measured E: cosine E + 2^-16, L2 E (1 + 2^-15)
+__device__ __forceinline__ float h16_margin_cos(float e) { return e + 0.0000152587890625f; }
+__device__ __forceinline__ float h16_margin_l2(float e) { return e * 1.000030517578125f; }
+__device__ __forceinline__ bool h16_rejects_cos(float s, float qn, float wd, float mcos) {
     const float da = 1.0f - (s * H16_COS_SCALE) / qn;
-    return da > wd + H16_DELTA_COS;
+    return da > wd + mcos;
 }
-__device__ __forceinline__ bool h16_rejects_l2(float s, float xn, float wd) {
+__device__ __forceinline__ bool h16_rejects_l2(float s, float xn, float wd, float ml2) {
     const float da = sqrtf(s);
-    return da >= H16_MIN_L2 && da * H16_REL_L2 - H16_ABS_L2 * xn > wd;
-}
-
-// int8 screen ("The int8 screening copy"): with y' = s q8 and
-// e >= |y' - y|_2 stored per row,
-//   cosine: |S/|q| - (the f32 cosine term)| <= e + 3 gamma + 10u < e + 2^-16
-//           (Cauchy-Schwarz on q.(y' - y); S = s * sum q_i q8_i in f32)
-//   L2:     | |q - y'| - |q - y| | <= e (triangle inequality), plus the
-//           relative rounding of both computed distances (< 2^-16)
-// e already carries (1 + 2^-10) relative and 2^-20 |y| absolute slack for the
-// rounding of its own computation.  A NaN scale or bound never rejects.
-constexpr float I8_SLACK_COS = 0.0000152587890625f;  // 2^-16
-__device__ __forceinline__ bool i8_rejects_cos(float s, float scale, float e, float qn, float wd) {
-    const float da = 1.0f - (s * scale) / qn;
-    return da > wd + e + I8_SLACK_COS;
-}
-__device__ __forceinline__ bool i8_rejects_l2(float s, float e, float wd) {
-    const float da = sqrtf(s);
-    return da >= H16_MIN_L2 && da * H16_REL_L2 - e > wd;
+    return da >= H16_MIN_L2 && da * H16_REL_L2 - ml2 * xn > wd;
 }
 
 // finalize a canonical sum into a distance (distance.go:15-23 semantics)

@@ -79,57 +79,6 @@ __device__ __forceinline__ uint32_t compact(uint32_t v, bool keep, int& cnt) {
     return push_to(v, dst);
 }
 
-// int8 stage of the screen: drops candidates whose int8 screening distance
-// proves the f32 distance exceeds wd; returns the compacted survivors (cnt
-// updated).  2G rows per pass, as the fp16 stage (register budget).
-template <class C, int G>
-__device__ __forceinline__ uint32_t screen_i8(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int& cnt,
-                                              int metric, float wd) {
-    constexpr int GI = (2 * G <= C::LPR) ? 2 * G : G;
-    using RM = RowMap<C, GI>;
-    const int lane = lane_id();
-    bool rej = false;  // lane t: candidate t is rejected
-    for (int base = 0; base < cnt; base += RM::T) {
-        uint32_t ids[GI];
-        bool valid[GI];
-        float sc[GI];
-#pragma unroll
-        for (int gg = 0; gg < GI; ++gg) {
-            const int t = base + RM::reg_row(gg, lane);
-            valid[gg] = t < cnt;
-            if constexpr (C::RPI == 1)
-                ids[gg] = rl_u(cid, (base + gg) & 63);
-            else
-                ids[gg] = shfl_u(cid, t & 63);
-            ids[gg] = valid[gg] ? guard_id(g, ids[gg]) : 0u;
-        }
-        // the owner lane of row town fetches that row's {scale, bound} only
-        const int town = base + RM::owned_row(lane);
-        const uint32_t oid = shfl_u(cid, town & 63);
-        const float2 ax = g.i8aux[town < cnt ? guard_id(g, oid) : 0u];
-        bool r = false;
-        if (metric == EUCLIDEAN) {
-#pragma unroll
-            for (int gg = 0; gg < GI; ++gg) sc[gg] = g.i8aux[ids[gg]].x;
-            const float s = eval_rows_i8<C, GI, true>(q, g.i8, g.pitch, ids, valid, sc);
-            if (town < cnt) r = i8_rejects_l2(s, ax.y, wd);
-        } else {
-#pragma unroll
-            for (int gg = 0; gg < GI; ++gg) sc[gg] = 1.f;
-            const float s = eval_rows_i8<C, GI, false>(q, g.i8, g.pitch, ids, valid, sc);
-            if (town < cnt) r = i8_rejects_cos(s, ax.x, ax.y, qn, wd);
-        }
-        const int t = lane - base;
-        const int src = (t >= 0 && t < RM::T) ? RM::owner(t) : lane;
-        const bool rt = __shfl((int)r, src, 64) != 0;
-        if (t >= 0 && t < RM::T) rej = rt;
-    }
-    int cnt2;
-    const uint32_t cid2 = compact(cid, lane < cnt && !rej, cnt2);
-    cnt = cnt2;
-    return cid2;
-}
-
 // Screened evaluation for the sorted-list searches: candidates whose fp16
 // screening distance proves the f32 distance exceeds `wd` (the list's worst
 // entry before this batch, which only decreases) are dropped; the rest go
@@ -138,16 +87,11 @@ __device__ __forceinline__ uint32_t screen_i8(const GraphDev& g, const QReg<C>& 
 // Returns the number of rows evaluated in f32.
 template <class C, int G, class Sink>
 __device__ __forceinline__ int eval_screened(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int cnt,
-                                             int metric, float wd, Sink&& sink, unsigned long long& s8,
-                                             unsigned long long& s16) {
+                                             int metric, float wd, Sink&& sink, unsigned long long& s16,
+                                             float margin) {
     constexpr int GH = (2 * G <= C::LPR) ? 2 * G : G;
     using RM = RowMap<C, GH>;
     const int lane = lane_id();
-    if (g.i8) {  // stage 1: int8 copy, compact the survivors
-        s8 += cnt;
-        cid = screen_i8<C, G>(g, q, qn, cid, cnt, metric, wd);
-        if (cnt == 0) return 0;
-    }
     if (!g.h16) {
         eval_list<C, G>(g, q, qn, cid, cnt, metric, sink);
         return cnt;
@@ -184,12 +128,12 @@ __device__ __forceinline__ int eval_screened(const GraphDev& g, const QReg<C>& q
 #pragma unroll
             for (int gg = 1; gg < GH; ++gg)
                 if (RM::reg_row(gg, lane) == town - base) xo = xn[gg];
-            if (town < cnt) r = h16_rejects_l2(s, xo, wd);
+            if (town < cnt) r = h16_rejects_l2(s, xo, wd, margin);
         } else {
 #pragma unroll
             for (int gg = 0; gg < GH; ++gg) inv[gg] = 1.f;
             const float s = eval_rows_h16<C, GH, false>(q, g.h16, g.pitch, ids, valid, inv);
-            if (town < cnt) r = h16_rejects_cos(s, qn, wd);
+            if (town < cnt) r = h16_rejects_cos(s, qn, wd, margin);
         }
         // hand row t's verdict from its owner lane to lane t
         const int t = lane - base;
@@ -206,8 +150,7 @@ __device__ __forceinline__ int eval_screened(const GraphDev& g, const QReg<C>& q
 
 struct WaveStats {
     unsigned long long E = 0, X = 0, resets = 0;
-    unsigned long long S = 0, F = 0;  // screened rows (fp16, or int8 when there is no fp16 copy) / rows evaluated in f32
-    unsigned long long S8 = 0;        // rows screened on the int8 copy
+    unsigned long long S = 0, F = 0;  // rows screened on the fp16 copy / rows evaluated in f32
 };
 
 // How the sequential (compat) walks evaluate distances and order their own
@@ -253,6 +196,11 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
     st.E += 1;
     st.F += 1;
     const bool screen = SCREEN && h16_query_ok(qn);
+    float margin = 0.f;  // the copy's measured rounding -> the metric's screening margin
+    if constexpr (SCREEN) {
+        const float e = g.h16err ? *g.h16err : 0.00048828125f;
+        margin = g.metric == EUCLIDEAN ? h16_margin_l2(e) : h16_margin_cos(e);
+    }
     const int32_t* degp = g.layers[layer].deg;
     const int32_t* adjp = g.layers[layer].adj;
     const int capl = g.layers[layer].cap;
@@ -286,7 +234,7 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
             bl_at(L, ef - 1, wd, wi);
         }
         if (SCREEN && screen && wd < __int_as_float(0x7f800000)) {
-            st.F += eval_screened<C, G>(g, q, qn, cid, cnt, g.metric, wd, sink, st.S8, st.S);
+            st.F += eval_screened<C, G>(g, q, qn, cid, cnt, g.metric, wd, sink, st.S, margin);
         } else {
             st.F += cnt;
             eval_list<C, G>(g, q, qn, cid, cnt, g.metric, sink);

@@ -66,10 +66,9 @@ constexpr int NEG_MAX_CAND = 256;
 int launch_negatives(const NegArgs& a, int lpr, int vpl, hipStream_t s);
 
 int launch_pad_rows(const float* src, int64_t n, int dim, float* dst, int pitch, hipStream_t s);
-int launch_i8_rows(const float* X, const float* norms, int64_t n0, int64_t n1, int pitch, int metric, int8_t* I,
-                   float2* aux, hipStream_t s);
+// err: running max of the rows' measured relative rounding (GraphDev::h16err)
 int launch_h16_rows(const float* X, const float* norms, int64_t n0, int64_t n1, int pitch, int metric, uint16_t* H,
-                    float2* aux, hipStream_t s);
+                    float2* aux, float* err, hipStream_t s);
 int launch_norms(const float* X, int64_t n0, int64_t n1, int pitch, int lpr, int vpl, float* out, hipStream_t s);
 int launch_sweep(const float* q, const float* X, int64_t n, int pitch, int lpr, int vpl, int metric, float* out,
                  hipStream_t s);
@@ -168,11 +167,33 @@ struct ExactArgs {
     int64_t ldQs;
     const float* xinv;    // fp16 2-product mode: per-row / per-query unscale 2^-e (NaN: outside the bound)
     const float* qinv;
+    // fp16 1-product ring (exact_precision 3)
+    int tile_stride;          // sample pass: score every tile_stride-th row tile (1: every tile)
+    int64_t nsample_tiles;    // ... how many (compact columns [0, nsample_tiles * BN) of scores)
+    const float* ring_c;      // [>= roundup(B, 256)] filter constants (k_ring_prep; +inf pads)
+    const float* ring_s;      // [same] L2: 1 / qi
+    uint2* region;            // [tiles * rcap] passing pairs {row off | query off << 16, acc}
+    int32_t* region_cnt;      // [tiles] pairs per tile (may exceed rcap: overflow)
+    int rcap;                 // entries per tile region
 };
 int launch_exact_scores(const ExactArgs& a, hipStream_t s);     // f32-input MFMA
 int launch_exact_scores_x3(const ExactArgs& a, int tile, hipStream_t s);  // bf16x3 split MFMA
 // fp16 2-product split: (qh + ql) . xh on v_mfma_f32_32x32x16_f16 (Xl unused)
 int launch_exact_scores_x2h(const ExactArgs& a, int tile, hipStream_t s);
+// fp16 1-product ring: every score of the sampled row tiles, or the fused filter into regions
+int launch_h1_sample(const ExactArgs& a, int variant, hipStream_t s);
+int launch_h1_filter(const ExactArgs& a, int variant, hipStream_t s);
+constexpr int H1_BN = 256;   // row tile of every launch_h1_* variant
+constexpr int H1_BSUB = 16;     // sub-buckets per query (k_bucket)
+constexpr int H1_CSTRIDE = 32;  // sub-bucket counters one 128-B line apart (no same-line atomics)
+int h1_tile_bm(int variant);  // query tile of a variant (128 or 256)
+int launch_ring_prep(const float* thr, const float* qnorm, const float* qinv, int64_t B, int metric, float* c,
+                     float* sq, hipStream_t s);
+// qcnt [B * H1_BSUB * H1_CSTRIDE], bucket [B * H1_BSUB * scap]
+int launch_bucket(const uint2* region, const int32_t* region_cnt, int rcap, int64_t ntiles, int64_t nqt, int BM,
+                  int BN, int64_t B, int32_t* qcnt, uint2* bucket, int scap, uint8_t* qovf, hipStream_t s);
+int launch_select_bucket(const ExactArgs& a, const int32_t* qcnt, const uint2* bucket, int scap, const uint8_t* qovf,
+                         const float* thr, hipStream_t s);
 // err (nullable): running max of the rows' relative fp16 rounding |x' - x| / |x|
 int launch_split_h16(const float* src, int64_t r0, int64_t r1, int pitch, int64_t rows, uint16_t* hi, uint16_t* lo,
                      float* inv, float* err, hipStream_t s);
@@ -194,6 +215,7 @@ struct CertArgs {
     unsigned long long* stats;   // [0] += uncertified queries
     const uint8_t* only;         // re-rank only rows with only[b] != 0 (nullable)
     const float* xerr;           // fp16 2-product scores: max relative row rounding, added to the bound (nullable)
+    const float* qerr;           // fp16 1-product scores: max relative query rounding of the batch (nullable)
 };
 int launch_rerank(const float* Q, const GraphDev& g, const uint32_t* cand, int kk, int64_t B, int lpr, int vpl, int k,
                   int64_t* out_keys, float* out_dist, int32_t* out_n, int32_t* out_ids, const CertArgs& c,

@@ -24,6 +24,7 @@
 //             oracle's brute force bit for bit.
 //  k_merge  : per query, merge S shard top-k lists by (distance, key).
 #include <algorithm>
+#include <type_traits>
 
 #include "device_search.hpp"
 #include "engine.hpp"
@@ -272,18 +273,28 @@ int launch_max_norm(const float* norms, int64_t n, float* out, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// Block tile BM (queries) x BN (rows) = (WAVES_M*TM*32) x (WAVES_N*TN*32); one
-// K-stage = 16 deep.  LDS image of one stage: [A hi][A lo][B hi][B lo], each
-// rows x 16 bf16 (two 16-B chunks per row); chunk c of row r sits at chunk
-// position c ^ ((r >> 3) & 1), so the 16 consecutive rows one quarter of a
-// ds_read_b128 touches land in 16 distinct 16-B slots of the 256-B bank window.
-template <int WAVES_M, int WAVES_N, int TM, int TN, bool H2 = false>
-struct X3Tile {
+// Split-operand GEMM modes (planes of A = queries, B = rows, all K-blocked by 16):
+//   RING_X3 bf16x3     q.x ~ ql.xh + qh.xl + qh.xh  (A hi+lo, B hi+lo)
+//   RING_H2 fp16 2-pr. q.x ~ ql.xh + qh.xh          (A hi+lo, B hi; rows rounded once)
+//   RING_H1 fp16 1-pr. q.x ~ qh.xh                  (A hi,    B hi; both rounded once)
+enum { RING_X3 = 0, RING_H2 = 1, RING_H1 = 2 };
+
+// Block tile BM (queries) x BN (rows) = (WAVES_M*TM*32) x (WAVES_N*TN*32).  One
+// ring stage = S K-blocks of 16.  LDS image of one K-block: [A hi][A lo][B hi]
+// [B lo] (planes the mode uses), each rows x 16 halves (two 16-B chunks per
+// row); chunk c of row r sits at chunk position c ^ ((r >> 3) & 1), so the 16
+// consecutive rows one quarter of a ds_read_b128 touches land in 16 distinct
+// 16-B slots of the 256-B bank window.
+template <int WAVES_M, int WAVES_N, int TM, int TN, int MODE, int S>
+struct RingTile {
     static constexpr int BM = WAVES_M * TM * 32, BN = WAVES_N * TN * 32;
     static constexpr int NT = 64 * WAVES_M * WAVES_N, NW = WAVES_M * WAVES_N;
-    static constexpr int XPLANES = H2 ? 1 : 2;                    // H2: the rows' hi plane only
-    static constexpr int STAGE = (2 * BM + XPLANES * BN) * X3K;  // 16-bit elements per stage
-    static constexpr int PIECES = STAGE * 2 / 1024;     // 1-KiB LDS-DMA pieces per stage
+    static constexpr int APL = MODE == RING_H1 ? 1 : 2;  // query planes
+    static constexpr int XPL = MODE == RING_X3 ? 2 : 1;  // row planes
+    static constexpr int KBE = (APL * BM + XPL * BN) * X3K;  // 16-bit elements of one K-block image
+    static constexpr int STAGE = KBE * S;
+    static constexpr int KB_PIECES = KBE * 2 / 1024;  // 1-KiB LDS-DMA pieces per K-block
+    static constexpr int PIECES = KB_PIECES * S;
     static_assert(PIECES % NW == 0, "DMA split");
     static constexpr int PER = PIECES / NW;
 };
@@ -295,85 +306,106 @@ __device__ __forceinline__ void x3_dma(const uint16_t* src, uint16_t* lds) {
                                      (__attribute__((address_space(3))) void*)(lds), 16, 0, 0);
 }
 
-// one 16-deep K-stage of a wave's TM x TN tiles: q.x += ql.xh + qh.xl + qh.xh
+// Fragments of one 16-deep K-block (base = the K-block's image) for a wave's
+// TM x TN tiles, and their MFMAs.  ring_stage reads every K-block of a stage
+// before the first MFMA, so the LDS latency of block s+1 hides behind the
+// MFMAs of block s (the compiler's lgkmcnt waits become partial).
 template <class T, int TM, int TN>
-__device__ __forceinline__ void x3_stage(const uint16_t* base, f32x16 (&acc)[TM][TN], int wm, int wn, int li,
-                                         int lh) {
+struct RingFrag {
+    u32x4 ah[TM], al[TM], bh[TN], bl[TN];
+};
+
+template <class T, int TM, int TN>
+__device__ __forceinline__ void ring_load(const uint16_t* base, RingFrag<T, TM, TN>& f, int wm, int wn, int li, int lh) {
     const uint16_t* Ah = base;
     const uint16_t* Al = base + T::BM * X3K;
-    const uint16_t* Bh = base + 2 * T::BM * X3K;
+    const uint16_t* Bh = base + T::APL * T::BM * X3K;
     const uint16_t* Bl = Bh + T::BN * X3K;
-    bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         const int r = wm * TM * 32 + i * 32 + li;
-        ah[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(Ah + swz16(r, lh)));
-        al[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(Al + swz16(r, lh)));
+        f.ah[i] = *reinterpret_cast<const u32x4*>(Ah + swz16(r, lh));
+        if constexpr (T::APL == 2) f.al[i] = *reinterpret_cast<const u32x4*>(Al + swz16(r, lh));
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int r = wn * TN * 32 + j * 32 + li;
-        bh[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(Bh + swz16(r, lh)));
-        bl[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(Bl + swz16(r, lh)));
+        f.bh[j] = *reinterpret_cast<const u32x4*>(Bh + swz16(r, lh));
+        if constexpr (T::XPL == 2) f.bl[j] = *reinterpret_cast<const u32x4*>(Bl + swz16(r, lh));
     }
-    // small cross terms first, the dominant hi*hi last (one f32 accumulator)
+}
+
+template <class T, int MODE, int TM, int TN>
+__device__ __forceinline__ void ring_mma(const RingFrag<T, TM, TN>& f, f32x16 (&acc)[TM][TN]) {
+    typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+            if constexpr (MODE == RING_X3) {  // small cross terms first, the dominant hi*hi last
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f.al[i]),
+                                                                    __builtin_bit_cast(bf16x8, f.bh[j]), acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f.ah[i]),
+                                                                    __builtin_bit_cast(bf16x8, f.bl[j]), acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, f.ah[i]),
+                                                                    __builtin_bit_cast(bf16x8, f.bh[j]), acc[i][j], 0, 0, 0);
+            } else {
+                if constexpr (MODE == RING_H2)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, f.al[i]),
+                                                                       __builtin_bit_cast(f16x8, f.bh[j]), acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, f.ah[i]),
+                                                                   __builtin_bit_cast(f16x8, f.bh[j]), acc[i][j], 0, 0, 0);
+            }
         }
 }
 
-// H2 (fp16): q.x 2^(eq+ex) += ql.xh + qh.xh (the rows' rounding is the error term)
-template <class T, int TM, int TN>
-__device__ __forceinline__ void x2_stage(const uint16_t* base, f32x16 (&acc)[TM][TN], int wm, int wn, int li,
-                                         int lh) {
-    typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-    const uint16_t* Ah = base;
-    const uint16_t* Al = base + T::BM * X3K;
-    const uint16_t* Bh = base + 2 * T::BM * X3K;
-    f16x8 ah[TM], al[TM], bh[TN];
+template <class T, int MODE, int TM, int TN, int S>
+__device__ __forceinline__ void ring_stage(const uint16_t* buf, f32x16 (&acc)[TM][TN], int wm, int wn, int li,
+                                           int lh) {
+    RingFrag<T, TM, TN> f[S];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-        const int r = wm * TM * 32 + i * 32 + li;
-        ah[i] = __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4*>(Ah + swz16(r, lh)));
-        al[i] = __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4*>(Al + swz16(r, lh)));
-    }
+    for (int sb = 0; sb < S; ++sb) ring_load<T, TM, TN>(buf + sb * T::KBE, f[sb], wm, wn, li, lh);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int r = wn * TN * 32 + j * 32 + li;
-        bh[j] = __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4*>(Bh + swz16(r, lh)));
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-        }
+    for (int sb = 0; sb < S; ++sb) ring_mma<T, MODE, TM, TN>(f[sb], acc);
+}
+
+// the score of one (query, row) pair from its accumulator -- the one formula
+// every consumer of split scores uses (write epilogue, candidate select), so
+// a score is the same float wherever it is computed.  Outside the fp16 bound
+// (NaN unscale): -inf, always preselected / never certified.
+__device__ __forceinline__ float split_score(int mode, int metric, float acc, float xi, float qi, float qn, float xn) {
+    const float dot = mode != RING_X3 ? acc * xi * qi : acc;
+    float sc = metric == COSINE ? 1.0f - dot / (qn * xn) : fmaf(-2.f, dot, qn * qn + xn * xn);
+    if (!(sc == sc)) sc = __int_as_float(0x7f800000);
+    if (mode != RING_X3 && !(xi == xi && qi == qi)) sc = -__int_as_float(0x7f800000);
+    return sc;
 }
 
 // Staged by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave instruction
 // straight into LDS -- no staging registers, no ds_write pass) into a ring of
-// four buffers, four separate __shared__ objects so the compiler's wait
-// counting can tell which buffer a pending DMA targets.  Stage t lives in
-// buffer t % 4.  Step t: wait for this wave's stage-t pieces (vmcnt leaves
-// stages t+1 and t+2 in flight), barrier (everyone's stage t landed, everyone
-// finished step t-1), issue stage t+3 into the buffer step t-1 read, multiply.
-// The loop is unrolled by four; DMA issue is unconditional (past the end it
-// re-reads the last K-block into a buffer nobody reads) so the in-flight count
-// is the same every step.  A lane's source chunk is pre-swizzled on the global
-// side so the linear LDS-DMA image matches swz16().
-template <int WAVES_M, int WAVES_N, int TM, int TN, bool H2>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_x3(ExactArgs a) {
-    using T = X3Tile<WAVES_M, WAVES_N, TM, TN, H2>;
-    __shared__ __attribute__((aligned(16))) uint16_t B0[T::STAGE];
+// R buffers, R separate __shared__ objects so the compiler's wait counting can
+// tell which buffer a pending DMA targets.  Stage t lives in buffer t % R.
+// Step t: wait for this wave's stage-t pieces (vmcnt leaves stages t+1 ..
+// t+R-2 in flight), barrier (everyone's stage t landed, everyone finished step
+// t-1), issue stage t+R-1 into the buffer step t-1 read, multiply.  The loop is
+// unrolled by R; DMA issue is unconditional (past the end it re-reads the last
+// K-blocks into a buffer nobody reads) so the in-flight count is the same
+// every step.  A lane's source chunk is pre-swizzled on the global side so the
+// linear LDS-DMA image matches swz16().
+//
+// Epilogues: EPI 0 writes every score (nsample_tiles > 0: only row tiles 0,
+// tile_stride, 2 tile_stride, ..., into a compact [B x ns] sample matrix); EPI 1 keeps
+// only the pairs that can beat the query's threshold (RingFilter, below) --
+// the fused top-k: no score matrix.
+template <int WAVES_M, int WAVES_N, int TM, int TN, int MODE, int S, int R, int EPI>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_ring(ExactArgs a) {
+    using T = RingTile<WAVES_M, WAVES_N, TM, TN, MODE, S>;
+    static_assert(R >= 2 && R <= 4, "ring depth");
+    // B0's tail: the tile's region counter (EPI 1)
+    __shared__ __attribute__((aligned(16))) uint16_t B0[T::STAGE + 8];
     __shared__ __attribute__((aligned(16))) uint16_t B1[T::STAGE];
-    __shared__ __attribute__((aligned(16))) uint16_t B2[T::STAGE];
-    __shared__ __attribute__((aligned(16))) uint16_t B3[T::STAGE];
+    __shared__ __attribute__((aligned(16))) uint16_t B2[R > 2 ? T::STAGE : 8];
+    __shared__ __attribute__((aligned(16))) uint16_t B3[R > 3 ? T::STAGE : 8];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
@@ -381,13 +413,16 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_x3(ExactArgs 
     // every XCD a contiguous run of logical tiles, query tiles fastest, so one
     // base tile is read into an XCD's L2 once and reused by all query tiles.
     const int64_t nqt = (a.B + T::BM - 1) / T::BM;
-    const int64_t nnt = (a.N + T::BN - 1) / T::BN;
+    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + T::BN - 1) / T::BN;
     const int64_t nblk = nqt * nnt;
     const int64_t per = nblk / 8, rem = nblk % 8;
     const int64_t xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
     const int64_t logical = xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
     const int64_t qt = logical % nqt, nt = logical / nqt;
-    const int64_t q0 = qt * T::BM, n0 = nt * T::BN;
+    const int64_t q0 = qt * T::BM;
+    const int64_t n0 = (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * T::BN;
+    int* const tile_ctr = reinterpret_cast<int*>(B0 + T::STAGE);
+    if (EPI == 1 && tid == 0) *tile_ctr = 0;  // ordered before the epilogue by the mainloop's barriers
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -397,29 +432,36 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_x3(ExactArgs 
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    // this wave's DMA pieces: lane source (K-block 0), K-block stride, LDS offset.
-    // A piece = 32 rows x 32 B of one plane.  Rows past B / N are clamped to
-    // the last row (valid loads; their products land in outputs never stored).
-    const uint16_t* gp[T::PER];
-    int64_t gks[T::PER];
+    // this wave's DMA pieces.  A piece = 32 rows x 32 B of one plane of one
+    // K-block.  Its source is a wave-uniform base (plane + first row of the
+    // tile + the stage's K-blocks: scalar registers, advanced by scalar adds)
+    // plus a per-lane 32-bit byte offset (row within the tile, chunk, K-block
+    // within the stage), so each piece is one global_load_lds with an SGPR base
+    // and no per-stage vector address arithmetic.  Rows past B / N are clamped
+    // to the last row (valid loads; their products land in outputs never stored).
+    const int wv = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform piece numbers
+    const char* pb[T::PER];
+    int64_t pstep[T::PER];  // bytes per ring stage (uniform)
+    uint32_t poff[T::PER];
     int lofs[T::PER];
 #pragma unroll
     for (int j = 0; j < T::PER; ++j) {
-        const int I = wave * T::PER + j;
-        const int apieces = T::BM / 16;  // 2 planes x BM/32 pieces
+        const int I = wv * T::PER + j;
+        const int sblk = I / T::KB_PIECES, Ik = I % T::KB_PIECES;
+        const int apieces = T::APL * T::BM / 32;
         int r;
         const uint16_t* base;
         int64_t row0, rmax, ld;
-        if (I < apieces) {
-            const int plane = I / (T::BM / 32);
-            r = (I % (T::BM / 32)) * 32 + (lane >> 1);
+        if (Ik < apieces) {
+            const int plane = Ik / (T::BM / 32);
+            r = (Ik % (T::BM / 32)) * 32 + (lane >> 1);
             base = plane ? a.Ql : a.Qh;
             row0 = q0;
             rmax = a.B - 1;
             ld = a.ldQs;
         } else {
-            const int I2 = I - apieces;
-            const int plane = I2 / (T::BN / 32);  // H2: always 0
+            const int I2 = Ik - apieces;
+            const int plane = I2 / (T::BN / 32);
             r = (I2 % (T::BN / 32)) * 32 + (lane >> 1);
             base = plane ? a.Xl : a.Xh;
             row0 = n0;
@@ -427,98 +469,422 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_x3(ExactArgs 
             ld = a.ldXs;
         }
         const int c = (lane & 1) ^ ((r >> 3) & 1);
-        gp[j] = base + min(row0 + r, rmax) * X3K + c * 8;
-        gks[j] = ld * X3K;
+        pb[j] = reinterpret_cast<const char*>(base + row0 * X3K);
+        pstep[j] = ld * X3K * S * 2;
+        poff[j] = (uint32_t)(((min(row0 + r, rmax) - row0) * X3K + c * 8 + (int64_t)sblk * ld * X3K) * 2);
         lofs[j] = I * 512;
     }
-    const int nk = a.pitch / X3K;
+    const int nst = a.pitch / (X3K * S);  // ring stages
     const int li = lane & 31, lh = lane >> 5;
-    auto issue = [&](uint16_t* buf, int k) {
-        const int64_t kb = min(k, nk - 1);
+    auto issue = [&](uint16_t* buf, int st) {
+        const int64_t kb = min(st, nst - 1);
 #pragma unroll
-        for (int j = 0; j < T::PER; ++j) x3_dma(gp[j] + kb * gks[j], buf + lofs[j]);
+        for (int j = 0; j < T::PER; ++j) {
+            // the stage's base in scalar registers, the lane's offset added last:
+            // global_load_lds with an SGPR base and a 32-bit VGPR offset
+            const uint64_t ub = reinterpret_cast<uint64_t>(pb[j] + kb * pstep[j]);
+            const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ub) |
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(ub >> 32)) << 32);
+            x3_dma(reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(sb) + poff[j]), buf + lofs[j]);
+        }
     };
-    auto stage = [&](const uint16_t* buf) {
-        if constexpr (H2)
-            x2_stage<T, TM, TN>(buf, acc, wm, wn, li, lh);
-        else
-            x3_stage<T, TM, TN>(buf, acc, wm, wn, li, lh);
-    };
-    // vmcnt(2*PER): this wave's pieces of the two newest stages stay in flight
-    constexpr int NW2 = 2 * T::PER;
-    constexpr int WAIT = (NW2 & 15) | ((NW2 >> 4) << 14) | (0x7 << 4) | (0xF << 8);
-    issue(B0, 0);
-    issue(B1, 1);
-    issue(B2, 2);
-    for (int kt = 0; kt < nk; kt += 4) {
-        __builtin_amdgcn_s_waitcnt(WAIT);
-        __builtin_amdgcn_s_barrier();
-        issue(B3, kt + 3);
-        stage(B0);
-        __builtin_amdgcn_s_waitcnt(WAIT);
-        __builtin_amdgcn_s_barrier();
-        issue(B0, kt + 4);
-        if (kt + 1 < nk) stage(B1);
-        __builtin_amdgcn_s_waitcnt(WAIT);
-        __builtin_amdgcn_s_barrier();
-        issue(B1, kt + 5);
-        if (kt + 2 < nk) stage(B2);
-        __builtin_amdgcn_s_waitcnt(WAIT);
-        __builtin_amdgcn_s_barrier();
-        issue(B2, kt + 6);
-        if (kt + 3 < nk) stage(B3);
+    auto stage = [&](const uint16_t* buf) { ring_stage<T, MODE, TM, TN, S>(buf, acc, wm, wn, li, lh); };
+    // vmcnt(PER * (R - 2)): this wave's pieces of the R-2 newest stages stay in flight
+    constexpr int NWT = T::PER * (R - 2);
+    constexpr int WAIT = (NWT & 15) | ((NWT >> 4) << 14) | (0x7 << 4) | (0xF << 8);
+    uint16_t* const bufs[4] = {B0, B1, B2, B3};
+#pragma unroll
+    for (int p = 0; p < R - 1; ++p) issue(bufs[p], p);
+    for (int kt = 0; kt < nst; kt += R) {
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            __builtin_amdgcn_s_waitcnt(WAIT);
+            __builtin_amdgcn_s_barrier();
+            issue(bufs[(u + R - 1) % R], kt + u + R - 1);
+            if (u == 0 || kt + u < nst) stage(bufs[u]);
+        }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no DMA may land after the workgroup ends
-    // epilogue: D col = lane&31 (base row), row = (r&3) + 8*(r>>2) + 4*(lane>>5) (query)
-    const float inf = __int_as_float(0x7f800000);
+    // accumulator layout: D col = lane&31 (base row), row = (r&3) + 8*(r>>2) + 4*(lane>>5) (query)
+    if constexpr (EPI == 0) {
+        const int64_t col0 = EPI == 0 && a.nsample_tiles > 0 ? nt * T::BN : n0;  // sample: compact columns
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int64_t xr = n0 + wn * TN * 32 + j * 32 + li;
-        if (xr >= a.N) continue;
-        const bool xok = !(a.dead && a.dead[xr]);
-        const float xn = a.xnorm[xr];
-        const float xi = H2 ? a.xinv[xr] : 1.f;
+        for (int j = 0; j < TN; ++j) {
+            const int64_t xr = n0 + wn * TN * 32 + j * 32 + li;
+            if (xr >= a.N) continue;
+            const bool xok = !(a.dead && a.dead[xr]);
+            const float xn = a.xnorm[xr];
+            const float xi = MODE != RING_X3 ? a.xinv[xr] : 1.f;
+            const int64_t col = col0 + wn * TN * 32 + j * 32 + li;
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
+            for (int i = 0; i < TM; ++i) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int64_t qr = q0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (qr >= a.B) continue;
-                const float qi = H2 ? a.qinv[qr] : 1.f;
-                const float dot = H2 ? acc[i][j][r] * xi * qi : acc[i][j][r];
-                const float qn = a.qnorm[qr];
-                float sc = a.metric == COSINE ? 1.0f - dot / (qn * xn) : fmaf(-2.f, dot, qn * qn + xn * xn);
-                if (!(sc == sc)) sc = inf;
-                if (H2 && !(xi == xi && qi == qi)) sc = -inf;  // outside the bound: always preselected / uncertified
-                if (!xok) sc = inf;
-                a.scores[(size_t)qr * a.ldS + xr] = sc;
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t qr = q0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (qr >= a.B) continue;
+                    const float qi = MODE != RING_X3 ? a.qinv[qr] : 1.f;
+                    float sc = split_score(MODE, a.metric, acc[i][j][r], xi, qi, a.qnorm[qr], xn);
+                    if (!xok) sc = __int_as_float(0x7f800000);
+                    a.scores[(size_t)qr * a.ldS + col] = sc;
+                }
             }
         }
+    } else {
+        // Fused preselection.  A pair can matter only if its score is <= the
+        // query's threshold t_q (an upper bound on the query's kk-th best
+        // score, from the sample pass).  The test is done on the accumulator:
+        //   cosine: score <= t  <=>  acc >= (1 - t) |q| |x| / (xi qi) = c_q w_r
+        //   L2:     score <= t  <=>  acc >= a_q / xi + b_r / qi
+        // with c_q, a_q lowered and b_r scaled down by 2^-19..2^-20 relative
+        // (k_ring_prep), far more than the roundings of either side, so a pair
+        // whose exact score is <= t always passes; extra passes are harmless
+        // (k_select_bucket recomputes split_score).  Passing pairs go to this
+        // wave's slice of the tile's region: {row offset | query offset << 16, acc}.
+        bool rok[TN];
+        float w0[TN], w1[TN], rxi[TN], rxn[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int64_t xr = n0 + wn * TN * 32 + j * 32 + li;
+            rok[j] = xr < a.N && !(a.dead && a.dead[xr]);
+            const int64_t xc = xr < a.N ? xr : a.N - 1;
+            const float xi = a.xinv[xc], xn = a.xnorm[xc];
+            rxi[j] = xi;
+            rxn[j] = xn;
+            if (a.metric == COSINE) {
+                w0[j] = xn / xi;  // xi is a power of two (or NaN: every query passes the row)
+                w1[j] = 0.f;
+            } else {
+                w0[j] = 1.f / xi;
+                w1[j] = xn * xn * 0.5f * (1.0f - 0x1p-20f) / xi;
+            }
+        }
+        // Passing pairs go to the tile's region {row off | query off << 16, score}
+        // (split_score, the exact float the sample pass and k_select use).  One
+        // pass, per element an fma and a compare (t = acc - bound; !(t < 0) keeps
+        // NaN bounds, rows outside the fp16 bound, passing) and a wave-uniform
+        // branch on the ballot; only a ballot with passes (a few per wave-tile)
+        // takes an LDS add for its slots.
+        uint2* reg = a.region + logical * (int64_t)a.rcap;
+        unsigned long long rokm[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) rokm[j] = __builtin_amdgcn_ballot_w64(rok[j]);
+        auto epi = [&](auto cos_tag) {
+            constexpr bool COS = decltype(cos_tag)::value;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+#pragma unroll
+                for (int r4 = 0; r4 < 4; ++r4) {
+                    const int64_t qb = q0 + wm * TM * 32 + i * 32 + 8 * r4 + 4 * lh;  // 4 consecutive queries
+                    const float4 c4 = *reinterpret_cast<const float4*>(a.ring_c + qb);
+                    const float cq[4] = {c4.x, c4.y, c4.z, c4.w};
+                    float sq[4] = {0.f, 0.f, 0.f, 0.f};
+                    if constexpr (!COS) {
+                        const float4 s4 = *reinterpret_cast<const float4*>(a.ring_s + qb);
+                        sq[0] = s4.x, sq[1] = s4.y, sq[2] = s4.z, sq[3] = s4.w;
+                    }
+#pragma unroll
+                    for (int r1 = 0; r1 < 4; ++r1) {
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) {
+                            const int r = r4 * 4 + r1;
+                            const float v = acc[i][j][r];
+                            float t;
+                            if constexpr (COS)
+                                t = fmaf(-cq[r1], w0[j], v);
+                            else
+                                t = v - fmaf(cq[r1], w0[j], w1[j] * sq[r1]);
+                            const unsigned long long m = __builtin_amdgcn_ballot_w64(!(t < 0.f)) & rokm[j];
+                            if (m) {
+                                const bool pass = (m >> lane) & 1ull;
+                                const int first = __ffsll((long long)m) - 1;
+                                int base = 0;
+                                if (lane == first) base = atomicAdd(tile_ctr, __popcll(m));
+                                base = __shfl(base, first, 64);
+                                const int qo = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                                // every counted slot is written: a padded query (q >= B, bound
+                                // +inf) can still pass on a NaN bound (zero row) and is stored
+                                // with score +inf, which the bucket pass skips
+                                if (pass) {
+                                    const int e = base + __builtin_amdgcn_mbcnt_hi(
+                                                             (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                                    const int ro = wn * TN * 32 + j * 32 + li;
+                                    const float sc = q0 + qo < a.B
+                                                         ? split_score(MODE, a.metric, v, rxi[j], a.qinv[q0 + qo],
+                                                                       a.qnorm[q0 + qo], rxn[j])
+                                                         : __builtin_inff();
+                                    if (e < a.rcap)
+                                        reg[e] = make_uint2((uint32_t)ro | ((uint32_t)qo << 16), __float_as_uint(sc));
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        };
+        if (a.metric == COSINE)
+            epi(std::true_type{});
+        else
+            epi(std::false_type{});
+        __syncthreads();
+        if (tid == 0) a.region_cnt[logical] = *tile_ctr;
     }
 }
 
-template <int WM_, int WN_, int TM_, int TN_, bool H2>
-static int launch_x3_t(const ExactArgs& a, hipStream_t s) {
-    using T = X3Tile<WM_, WN_, TM_, TN_, H2>;
-    const int64_t nqt = (a.B + T::BM - 1) / T::BM, nnt = (a.N + T::BN - 1) / T::BN;
-    hipLaunchKernelGGL((k_scores_x3<WM_, WN_, TM_, TN_, H2>), dim3((unsigned)(nqt * nnt)), dim3(T::NT), 0, s, a);
+template <int WM_, int WN_, int TM_, int TN_, int MODE, int S, int R, int EPI>
+static int launch_ring_t(const ExactArgs& a, hipStream_t s) {
+    using T = RingTile<WM_, WN_, TM_, TN_, MODE, S>;
+    if (a.pitch % (X3K * S)) return -5;
+    const int64_t nqt = (a.B + T::BM - 1) / T::BM;
+    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + T::BN - 1) / T::BN;
+    hipLaunchKernelGGL((k_scores_ring<WM_, WN_, TM_, TN_, MODE, S, R, EPI>), dim3((unsigned)(nqt * nnt)), dim3(T::NT),
+                       0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <bool H2>
+template <int MODE>
 static int launch_split_scores(const ExactArgs& a, int tile, hipStream_t s) {
     if (a.B <= 0 || a.N <= 0) return 0;
     if (a.pitch % X3K) return -5;
     // tile 0: the measured best per split (config 5: bf16x3 256 x 256, fp16 128 x 256)
-    if (tile == 0) tile = H2 ? 1 : 3;
+    if (tile == 0) tile = MODE == RING_H2 ? 1 : 3;
     switch (tile) {
-        case 1: return launch_x3_t<2, 4, 2, 2, H2>(a, s);  // 128 x 256, 8 waves of 64 x 64
-        case 2: return launch_x3_t<2, 2, 2, 2, H2>(a, s);  // 128 x 128, 4 waves of 64 x 64
-        default: return launch_x3_t<2, 4, 4, 2, H2>(a, s);  // 256 x 256, 8 waves of 128 x 64
+        case 1: return launch_ring_t<2, 4, 2, 2, MODE, 1, 4, 0>(a, s);  // 128 x 256, 8 waves of 64 x 64
+        case 2: return launch_ring_t<2, 2, 2, 2, MODE, 1, 4, 0>(a, s);  // 128 x 128, 4 waves of 64 x 64
+        default: return launch_ring_t<2, 4, 4, 2, MODE, 1, 4, 0>(a, s);  // 256 x 256, 8 waves of 128 x 64
     }
 }
-int launch_exact_scores_x3(const ExactArgs& a, int tile, hipStream_t s) { return launch_split_scores<false>(a, tile, s); }
-int launch_exact_scores_x2h(const ExactArgs& a, int tile, hipStream_t s) { return launch_split_scores<true>(a, tile, s); }
+int launch_exact_scores_x3(const ExactArgs& a, int tile, hipStream_t s) { return launch_split_scores<RING_X3>(a, tile, s); }
+int launch_exact_scores_x2h(const ExactArgs& a, int tile, hipStream_t s) { return launch_split_scores<RING_H2>(a, tile, s); }
+
+// ---------------------------------------------------------------------------
+// fp16 1-product path with the fused preselection (exact_precision 3)
+// ---------------------------------------------------------------------------
+// ring variants (exact_tile for precision 3; 0 = 5): 1 = 256 x 256, 32-deep stages,
+// 4 buffers; 2 = 256 x 256, 64-deep stages, 2 buffers; 3 = 256 x 256, 16-deep
+// stages, 4 buffers; 4 = 128 x 256, 32-deep, 4 buffers; 5 = 128 x 256, 32-deep, 3 buffers
+// (two workgroups per CU); 6 = 128 x 256 on 4 waves of 128 x 64, 32-deep, 3 buffers
+template <int EPI>
+static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
+    if (a.B <= 0 || a.N <= 0) return 0;
+    if (variant == 0) variant = 5;  // measured best on config 5 (profiles/r02_cfg5_*)
+    switch (variant) {
+        case 2: return launch_ring_t<2, 4, 4, 2, RING_H1, 4, 2, EPI>(a, s);
+        case 3: return launch_ring_t<2, 4, 4, 2, RING_H1, 1, 4, EPI>(a, s);
+        case 4: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 4, EPI>(a, s);
+        case 5: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 3, EPI>(a, s);
+        case 6: return launch_ring_t<1, 4, 4, 2, RING_H1, 2, 3, EPI>(a, s);
+        default: return launch_ring_t<2, 4, 4, 2, RING_H1, 2, 4, EPI>(a, s);
+    }
+}
+int h1_tile_bm(int variant) { return variant == 0 || (variant >= 4 && variant <= 6) ? 128 : 256; }
+int launch_h1_sample(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<0>(a, variant, s); }
+int launch_h1_filter(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<1>(a, variant, s); }
+
+// Per query: the epilogue filter's constants from the sample threshold t_q (the
+// kk-th best sample score; the sample is a subset of the rows scored with the
+// same arithmetic, so t_q bounds the query's kk-th best score from above).
+//   cosine: c = ((1 - t) - 2^-19) |q| / qi, then scaled by (1 -+ 2^-20) toward -inf
+//   L2:     c = a = (|q|^2 - t - 2^-20 (|q|^2 + |t|)) / (2 qi), s = 1 / qi
+// A query the bound does not cover (NaN qi, t not finite) gets c = +inf: no row
+// passes for it except rows outside the bound; k_select_bucket sends it to the
+// canonical fallback.
+__global__ void k_ring_prep(const float* thr, const float* qnorm, const float* qinv, int64_t B, int64_t Bpad,
+                            int metric, float* c, float* sq) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= Bpad) return;
+    if (b >= B) {  // pads of the last query tile: nothing passes
+        c[b] = __int_as_float(0x7f800000);
+        sq[b] = 0.f;
+        return;
+    }
+    const float t = thr[b], qn = qnorm[b], qi = qinv[b];
+    const bool ok = isfinite(t) && qi == qi;
+    float cv, sv = 0.f;
+    if (metric == COSINE) {
+        const double v = ((1.0 - (double)t) - 0x1p-19) * (double)qn / (double)qi;
+        cv = (float)(v >= 0 ? v * (1.0 - 0x1p-20) : v * (1.0 + 0x1p-20));
+    } else {
+        const double q2 = (double)qn * (double)qn;
+        cv = (float)((q2 - (double)t - 0x1p-20 * (q2 + fabs((double)t))) * 0.5 / (double)qi);
+        sv = 1.f / qi;
+    }
+    c[b] = ok ? cv : __int_as_float(0x7f800000);
+    sq[b] = ok ? sv : 0.f;
+}
+
+int launch_ring_prep(const float* thr, const float* qnorm, const float* qinv, int64_t B, int metric, float* c,
+                     float* sq, hipStream_t s) {
+    if (B <= 0) return 0;
+    const int64_t Bpad = (B + 255) / 256 * 256;  // covers every variant's query tile
+    hipLaunchKernelGGL(k_ring_prep, dim3((unsigned)((Bpad + 255) / 256)), dim3(256), 0, s, thr, qnorm, qinv, B, Bpad,
+                       metric, c, sq);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Regions -> per-query buckets: one wave per row/query tile.  A query's
+// bucket is split in H1_BSUB sub-buckets (row tile nt goes to nt % H1_BSUB), each with
+// its own counter, so the appends of the ~N/256 tiles that feed one query do
+// not all serialise on one address.  A region (or sub-bucket) whose count
+// exceeds its capacity lost pairs: every query of the tile (or that query) is
+// marked, and k_select_bucket sends it to the canonical fallback.
+__global__ __launch_bounds__(64) void k_bucket(const uint2* region, const int32_t* region_cnt, int rcap, int64_t ntiles,
+                                               int64_t nqt, int BM, int BN, int64_t B, int32_t* qcnt, uint2* bucket,
+                                               int scap, uint8_t* qovf) {
+    const int64_t t = blockIdx.x;
+    if (t >= ntiles) return;
+    const int lane = lane_id();
+    const int64_t nt = t / nqt;
+    const int64_t q0 = (t % nqt) * BM, n0 = nt * BN;
+    const int sub = (int)(nt % H1_BSUB);
+    const int n = region_cnt[t];
+    if (n > rcap) {
+        for (int64_t q = q0 + lane; q < q0 + BM && q < B; q += 64) qovf[q] = 1;
+    }
+    const int m = min(n, rcap);
+    const uint2* reg = region + t * (int64_t)rcap;
+    for (int e = lane; e < m; e += 64) {
+        const uint2 v = reg[e];
+        const int64_t q = q0 + (v.x >> 16);
+        if (q >= B) continue;
+        const uint32_t row = (uint32_t)(n0 + (v.x & 0xFFFFu));
+        const int pos = atomicAdd(&qcnt[(q * H1_BSUB + sub) * H1_CSTRIDE], 1);
+        if (pos < scap) bucket[(q * H1_BSUB + sub) * scap + pos] = make_uint2(row, v.y);
+    }
+}
+
+int launch_bucket(const uint2* region, const int32_t* region_cnt, int rcap, int64_t ntiles, int64_t nqt, int BM,
+                  int BN, int64_t B, int32_t* qcnt, uint2* bucket, int scap, uint8_t* qovf, hipStream_t s) {
+    if (ntiles <= 0) return 0;
+    hipLaunchKernelGGL(k_bucket, dim3((unsigned)ntiles), dim3(64), 0, s, region, region_cnt, rcap, ntiles, nqt, BM, BN,
+                       B, qcnt, bucket, scap, qovf);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// One wave per query: the best kk (score, row) of its sub-buckets (scores as
+// the epilogue computed them with split_score).  Bound t: every row outside
+// the bucket scored above t_q (the filter passes every score <= t_q), every
+// bucket row past the best kk scored >= the kk-th, so t = min(t_q, kk-th best)
+// (t_q alone when the bucket holds fewer than kk).  A query with an overflowed
+// region or sub-bucket, or an unusable threshold, gets t = -inf: its
+// certificate fails and the canonical fallback recomputes it.
+template <int R>
+__global__ __launch_bounds__(256) void k_select_bucket(ExactArgs a, const int32_t* qcnt, const uint2* bucket, int scap,
+                                                       const uint8_t* qovf, const float* thr) {
+    // four waves per query, wave w takes sub-buckets w, w+4, ...; wave 0 merges
+    __shared__ float md[4 * 64 * R];
+    __shared__ uint32_t mi[4 * 64 * R];
+    __shared__ int mbad;
+    const int64_t b = blockIdx.x;
+    if (b >= a.B) return;
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const float inf = __int_as_float(0x7f800000);
+    const float tq = thr[b], qi = a.qinv[b];
+    const bool usable0 = !qovf[b] && isfinite(tq) && qi == qi;
+    if (threadIdx.x == 0) mbad = 0;
+    __syncthreads();
+    const int kk = a.kk;
+    auto scan = [&](BList<R>& L, const uint2* bk, int m) {
+        float worst;
+        {
+            float wd;
+            uint32_t wi;
+            bl_at(L, kk - 1, wd, wi);
+            worst = wi == EMPTY_ID ? inf : wd;
+        }
+        for (int base = 0; base < m; base += 64) {
+            const int e = base + lane;
+            float x = inf;
+            uint32_t row = 0;
+            if (e < m) {
+                const uint2 v = bk[e];
+                row = v.x;
+                x = __uint_as_float(v.y);
+            }
+            unsigned long long msk = __ballot(x <= worst && x < inf);
+            while (msk) {
+                const int src = __ffsll((long long)msk) - 1;
+                msk &= msk - 1;
+                const float d = rl_f(x, src);
+                const uint32_t id = (uint32_t)__shfl((int)row, src, 64);
+                if (bl_insert(L, kk, d, id)) {
+                    float wd;
+                    uint32_t wi;
+                    bl_at(L, kk - 1, wd, wi);
+                    worst = wi == EMPTY_ID ? inf : wd;
+                }
+            }
+        }
+    };
+    BList<R> L;
+    bl_init(L);
+    if (usable0) {
+        for (int sb = wave; sb < H1_BSUB; sb += 4) {
+            const int n = qcnt[(b * H1_BSUB + sb) * H1_CSTRIDE];
+            if (n > scap) {
+                if (lane == 0) mbad = 1;
+                break;
+            }
+            scan(L, bucket + (b * H1_BSUB + sb) * (int64_t)scap, n);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        md[(wave * R + r) * 64 + lane] = L.d[r];
+        mi[(wave * R + r) * 64 + lane] = L.i[r] == EMPTY_ID ? EMPTY_ID : (L.i[r] & ID_MASK);
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    const bool usable = usable0 && !mbad;
+    // merge the other three lists into wave 0's
+    for (int w = 1; w < 4 && usable; ++w) {
+        float worst;
+        {
+            float wd;
+            uint32_t wi;
+            bl_at(L, kk - 1, wd, wi);
+            worst = wi == EMPTY_ID ? inf : wd;
+        }
+        for (int r = 0; r < R; ++r) {
+            const float x = md[(w * R + r) * 64 + lane];
+            const uint32_t row = mi[(w * R + r) * 64 + lane];
+            unsigned long long msk = __ballot(row != EMPTY_ID && x <= worst);
+            while (msk) {
+                const int src = __ffsll((long long)msk) - 1;
+                msk &= msk - 1;
+                const float d = rl_f(x, src);
+                const uint32_t id = (uint32_t)__shfl((int)row, src, 64);
+                if (bl_insert(L, kk, d, id)) {
+                    float wd;
+                    uint32_t wi;
+                    bl_at(L, kk - 1, wd, wi);
+                    worst = wi == EMPTY_ID ? inf : wd;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int idx = r * 64 + lane;
+        if (idx < kk) a.cand[b * kk + idx] = (!usable || L.i[r] == EMPTY_ID) ? EMPTY_ID : (L.i[r] & ID_MASK);
+    }
+    float kd;
+    uint32_t ki;
+    bl_at(L, kk - 1, kd, ki);
+    if (lane == 0) a.bound[b] = !usable ? -inf : (ki != EMPTY_ID ? fminf(kd, tq) : tq);
+}
+
+int launch_select_bucket(const ExactArgs& a, const int32_t* qcnt, const uint2* bucket, int scap, const uint8_t* qovf,
+                         const float* thr, hipStream_t s) {
+    if (a.B <= 0) return 0;
+    if (a.kk < 1 || a.kk > 256) return -4;
+    if (a.kk <= 64)
+        hipLaunchKernelGGL(k_select_bucket<1>, dim3((unsigned)a.B), dim3(256), 0, s, a, qcnt, bucket, scap, qovf, thr);
+    else if (a.kk <= 128)
+        hipLaunchKernelGGL(k_select_bucket<2>, dim3((unsigned)a.B), dim3(256), 0, s, a, qcnt, bucket, scap, qovf, thr);
+    else
+        hipLaunchKernelGGL(k_select_bucket<4>, dim3((unsigned)a.B), dim3(256), 0, s, a, qcnt, bucket, scap, qovf, thr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 // ---------------------------------------------------------------------------
 // top-kk preselect per query row (one wave per query)
@@ -682,11 +1048,15 @@ __global__ __launch_bounds__(64) void k_rerank(const float* __restrict__ Q, Grap
             if (ik == EMPTY_ID) {
                 cert = false;
             } else if (g.metric == COSINE) {
-                const double ex = c.xerr ? 1.01 * (1.0 + 1e-4) * (double)*c.xerr : 0.0;
+                // measured roundings: rows' ex (and queries' eq, 1-product) ->
+                // |q'.x' - q.x| <= (ex + eq + ex eq) |q| |x|
+                const double xe = c.xerr ? (double)*c.xerr : 0.0, qe = c.qerr ? (double)*c.qerr : 0.0;
+                const double ex = 1.01 * (1.0 + 1e-4) * (xe + qe + xe * qe);
                 cert = (double)dk < (double)t - (double)c.eps_cos - ex;
             } else {
                 const double qnd = c.qnorm[b], xm = *c.xmax;
-                const double ed = c.eps_dot + (c.xerr ? 1.01 * (double)*c.xerr : 0.0);
+                const double xe = c.xerr ? (double)*c.xerr : 0.0, qe = c.qerr ? (double)*c.qerr : 0.0;
+                const double ed = c.eps_dot + 1.01 * (xe + qe + xe * qe);
                 const double delta = 2.0 * ed * qnd * xm + c.c_l2 * (qnd + xm) * (qnd + xm);
                 cert = (double)dk * (double)dk < (double)t - delta;
             }

@@ -139,8 +139,91 @@ __global__ __launch_bounds__(256) void k_sweep_raw(const float* __restrict__ q, 
     if (lane == 0) out[row] = finalize(metric, acc, sqrtf(xx), sqrtf(qq));
 }
 
+// The same sweep for 16-B aligned rows with dim % 4 == 0 (the common case):
+// lane l loads its elements as float4 (one 1-KiB wave instruction per 256
+// elements), the query and its canonical |q| stay in registers for every row
+// of a grid-stride loop, two rows in flight per step.  Identical arithmetic
+// order, so identical bits.  HBM-bound: n * dim * 4 bytes per query.
+template <int VPL>
+__global__ __launch_bounds__(256) void k_sweep_raw4(const float* __restrict__ q, const float* __restrict__ X,
+                                                    int64_t n, int dim, int metric, float* __restrict__ out) {
+    const int lane = lane_id();
+    const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    float4 qv[VPL];
+    float qq = 0.f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+        const int e = v * 256 + 4 * lane;
+        qv[v] = e < dim ? *reinterpret_cast<const float4*>(q + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < dim) {
+            qq = fmaf(qv[v].x, qv[v].x, qq);
+            qq = fmaf(qv[v].y, qv[v].y, qq);
+            qq = fmaf(qv[v].z, qv[v].z, qq);
+            qq = fmaf(qv[v].w, qv[v].w, qq);
+        }
+    }
+    const float qn = metric == COSINE ? sqrtf(seg_allreduce<64>(qq)) : 1.f;
+    for (int64_t r0 = gw * 2; r0 < n; r0 += nw * 2) {
+        float4 xv[2][VPL];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t row = r0 + h < n ? r0 + h : r0;
+            const float* x = X + (size_t)row * dim;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) {
+                const int e = v * 256 + 4 * lane;
+                xv[h][v] = e < dim ? *reinterpret_cast<const float4*>(x + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            float acc = 0.f, xx = 0.f;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) {
+                if (v * 256 + 4 * lane >= dim) continue;
+                const float4 a = xv[h][v], b = qv[v];
+                if (metric == EUCLIDEAN) {
+                    float t = a.x - b.x;
+                    acc = fmaf(t, t, acc);
+                    t = a.y - b.y;
+                    acc = fmaf(t, t, acc);
+                    t = a.z - b.z;
+                    acc = fmaf(t, t, acc);
+                    t = a.w - b.w;
+                    acc = fmaf(t, t, acc);
+                } else {
+                    acc = fmaf(a.x, b.x, acc);
+                    xx = fmaf(a.x, a.x, xx);
+                    acc = fmaf(a.y, b.y, acc);
+                    xx = fmaf(a.y, a.y, xx);
+                    acc = fmaf(a.z, b.z, acc);
+                    xx = fmaf(a.z, a.z, xx);
+                    acc = fmaf(a.w, b.w, acc);
+                    xx = fmaf(a.w, a.w, xx);
+                }
+            }
+            acc = seg_allreduce<64>(acc);
+            if (metric == COSINE) xx = seg_allreduce<64>(xx);
+            if (lane == 0 && r0 + h < n) out[r0 + h] = finalize(metric, acc, sqrtf(xx), qn);
+        }
+    }
+}
+
 int launch_sweep_raw(const float* q, const float* X, int64_t n, int dim, int metric, float* out, hipStream_t s) {
     if (n <= 0) return 0;
+    const bool vec = dim % 4 == 0 && dim <= 4096 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)X & 15) == 0;
+    if (vec) {
+        const int vpl = (dim + 255) / 256;
+        const int grid = (int)std::min<int64_t>((n + 7) / 8, 4096);
+#define SW_(V)                                                                                            \
+    if (vpl <= V) {                                                                                       \
+        hipLaunchKernelGGL(k_sweep_raw4<V>, dim3((unsigned)grid), dim3(256), 0, s, q, X, n, dim, metric, out); \
+        return hipGetLastError() == hipSuccess ? 0 : -1;                                                  \
+    }
+        SW_(1) SW_(2) SW_(3) SW_(4) SW_(6) SW_(8) SW_(12) SW_(16)
+#undef SW_
+    }
     hipLaunchKernelGGL(k_sweep_raw, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, q, X, n, dim, metric, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -178,7 +261,8 @@ static int launch_sweep_t(const float* q, const float* X, int64_t n, int pitch, 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_h16_rows(const float* __restrict__ X, const float* __restrict__ norms,
                                                   int64_t n0, int64_t n1, int pitch, int metric,
-                                                  uint16_t* __restrict__ H, float2* __restrict__ aux) {
+                                                  uint16_t* __restrict__ H, float2* __restrict__ aux,
+                                                  float* __restrict__ err) {
     const int lane = lane_id();
     const int64_t r = n0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n1) return;
@@ -202,6 +286,9 @@ __global__ __launch_bounds__(256) void k_h16_rows(const float* __restrict__ X, c
     if (ok) (void)frexpf(m, &k);  // m = f * 2^k, f in [0.5, 1)
     const int ex = 15 - k;        // m * 2^ex in [2^14, 2^15)
     const float rx = ok ? 16384.0f / xn : 0.f;
+    // the row's measured rounding against y = x / |x|_f32 (cosine) or x (L2), in f64
+    double e2 = 0.0, y2 = 0.0;
+    const double inx = ok ? 1.0 / (double)xn : 0.0;
     for (int e = lane * 4; e < pitch; e += 256) {
         const float4 v = *reinterpret_cast<const float4*>(xp + e);
         h4 o;
@@ -212,88 +299,43 @@ __global__ __launch_bounds__(256) void k_h16_rows(const float* __restrict__ X, c
         else
             o = h4{(_Float16)ldexpf(v.x, ex), (_Float16)ldexpf(v.y, ex), (_Float16)ldexpf(v.z, ex),
                    (_Float16)ldexpf(v.w, ex)};
-        // lane-contiguous layout (eval_rows_h16), as the int8 copy
-        *reinterpret_cast<h4*>(H + (size_t)r * pitch + lane * 4 * i8_vpl(pitch) + (e >> 8) * 4) = o;
+        if (ok) {
+            const float xv[4] = {v.x, v.y, v.z, v.w};
+            const _Float16 ov[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const double y = metric == COSINE ? (double)xv[c] * inx : (double)xv[c];
+                const double yq = metric == COSINE ? (double)(float)ov[c] * 0x1p-14 : ldexp((double)(float)ov[c], -ex);
+                e2 = fma(yq - y, yq - y, e2);
+                y2 = fma(y, y, y2);
+            }
+        }
+        // lane-contiguous layout (eval_rows_h16)
+        *reinterpret_cast<h4*>(H + (size_t)r * pitch + lane * 4 * lc_vpl(pitch) + (e >> 8) * 4) = o;
     }
     if (lane == 0) aux[r] = make_float2(ok ? ldexpf(1.f, -ex) : __int_as_float(0x7fc00000), xn);
+    if (err && ok) {  // rows outside the range never reject: they do not count
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            e2 += __shfl_xor(e2, o, 64);
+            y2 += __shfl_xor(y2, o, 64);
+        }
+        // relative to |y| (cosine: |y| = |x| / |x|_f32 ~ 1), padded for the f64 sums and the rounding to f32
+        const float rel = y2 > 0.0 ? (float)(sqrt(e2 / y2) * (1.0 + 1e-6)) : 0.f;
+        if (lane == 0) atomicMax(reinterpret_cast<unsigned int*>(err), __float_as_uint(rel));
+    }
 }
 
 int launch_h16_rows(const float* X, const float* norms, int64_t n0, int64_t n1, int pitch, int metric, uint16_t* H,
-                    float2* aux, hipStream_t s) {
+                    float2* aux, float* err, hipStream_t s) {
     const int64_t rows = n1 - n0;
     if (rows <= 0) return 0;
     hipLaunchKernelGGL(k_h16_rows, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, X, norms, n0, n1, pitch, metric,
-                       H, aux);
+                       H, aux, err);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // ---------------------------------------------------------------------------
-// int8 screening copy of rows [n0, n1) (device_common.hpp GraphDev::i8), one
-// wave per row; norms[r] (canonical |x|) must already be written.
-//   y = x * (1/|x|) (cosine) or x (L2);  s = max|y_i| / 127;
-//   q8_i = round(y_i / s) in [-127, 127];  aux[r] = {s, e} with
-//   e = |s q8 - y|_2 (1 + 2^-10) + 2^-20 |y|  (covers the rounding of e itself
-//   and of y for cosine); rows outside the screen's validity range (as for
-//   the fp16 copy) get s = NaN and zero bytes.  Rows are stored
-//   lane-contiguous (device_common.hpp eval_rows_i8).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_i8_rows(const float* __restrict__ X, const float* __restrict__ norms,
-                                                 int64_t n0, int64_t n1, int pitch, int metric,
-                                                 int8_t* __restrict__ I, float2* __restrict__ aux) {
-    const int lane = lane_id();
-    const int64_t r = n0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= n1) return;
-    const float* xp = X + (size_t)r * pitch;
-    float m = 0.f;
-    bool fin = true;
-    for (int e = lane * 4; e < pitch; e += 256) {
-        const float4 v = *reinterpret_cast<const float4*>(xp + e);
-        fin = fin && isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w);
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    fin = __ballot(!fin) == 0ull;
-    const float xn = norms[r];
-    const bool ok = fin && m >= 8.881784197001252e-16f && m <= 1.125899906842624e15f &&  // [2^-50, 2^50]
-                    xn > 0.f && isfinite(xn);
-    const bool cos = metric == COSINE;
-    const float rx = cos ? 1.0f / xn : 1.0f;
-    const float my = cos ? m * rx : m;  // max|y_i| (rounding is monotone)
-    const float inv = ok ? 127.0f / my : 0.f;
-    const float sc = my / 127.0f;
-    float e2 = 0.f;
-    for (int e = lane * 4; e < pitch; e += 256) {
-        const float4 v = *reinterpret_cast<const float4*>(xp + e);
-        const float y[4] = {v.x * rx, v.y * rx, v.z * rx, v.w * rx};
-        uint32_t w = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float t = fminf(fmaxf(rintf(y[j] * inv), -127.f), 127.f);
-            const float d = fmaf(t, sc, -y[j]);
-            e2 = fmaf(d, d, e2);
-            w |= (uint32_t)(uint8_t)(int8_t)(int)t << (8 * j);
-        }
-        // lane-contiguous layout (device_common.hpp eval_rows_i8): element e
-        // = l*4 + v*256 + j (l = lane, v = e / 256) lands at byte l*4*VPL + v*4 + j
-        const int vpl = i8_vpl(pitch);
-        *reinterpret_cast<uint32_t*>(I + (size_t)r * pitch + lane * 4 * vpl + (e >> 8) * 4) = ok ? w : 0u;
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) e2 += __shfl_xor(e2, o, 64);
-    const float eb = sqrtf(e2) * 1.0009765625f + 9.5367431640625e-07f * (cos ? 1.0f : xn);
-    if (lane == 0) aux[r] = make_float2(ok ? sc : __int_as_float(0x7fc00000), eb);
-}
-
-int launch_i8_rows(const float* X, const float* norms, int64_t n0, int64_t n1, int pitch, int metric, int8_t* I,
-                   float2* aux, hipStream_t s) {
-    const int64_t rows = n1 - n0;
-    if (rows <= 0) return 0;
-    hipLaunchKernelGGL(k_i8_rows, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, X, norms, n0, n1, pitch, metric,
-                       I, aux);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 // ---------------------------------------------------------------------------
 // batched search: one wave per query
 // ---------------------------------------------------------------------------
@@ -357,7 +399,6 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
         if (st.resets) atomicAdd(&a.stats[2], st.resets);
         atomicAdd(&a.stats[8], st.S);
         atomicAdd(&a.stats[9], st.F);
-        if (st.S8) atomicAdd(&a.stats[10], st.S8);
     }
 }
 
@@ -494,7 +535,7 @@ __global__ __launch_bounds__(64) void k_negatives(NegArgs a) {
 template <class C, int R, int G>
 static int launch_beam_t(const SearchArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 << a.vis_log2;
-    if (a.g.h16 || a.g.i8)
+    if (a.g.h16)
         hipLaunchKernelGGL((k_search_beam<C, R, G, true>), dim3((unsigned)a.B), dim3(64), lds, s, a);
     else
         hipLaunchKernelGGL((k_search_beam<C, R, G, false>), dim3((unsigned)a.B), dim3(64), lds, s, a);

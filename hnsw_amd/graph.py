@@ -547,11 +547,11 @@ class Graph:
         return out
 
     def stats(self) -> dict:
-        o = np.zeros(11, np.int64)
-        self._check(load().mhnsw_stats(self._h, _ptr(o, C.c_int64), 11))
+        o = np.zeros(13, np.int64)
+        self._check(load().mhnsw_stats(self._h, _ptr(o, C.c_int64), 13))
         names = ["search_dist_evals", "search_expansions", "visited_resets", "build_dist_evals",
                  "build_expansions", "dropped_proposals", "searches", "exact_uncertified",
-                 "search_screened", "search_f32_evals", "search_screened_i8"]
+                 "search_screened", "search_f32_evals", "build_screened", "build_f32_rows", "build_search_us"]
         return dict(zip(names, o.tolist()))
 
     def reset_stats(self):
@@ -666,6 +666,13 @@ def NewGraphWithConfig(m: int, ml: float, efSearch: int, distance) -> Graph:  # 
     check(load().mhnsw_create(_metric_of(distance), int(m), float(ml), int(efSearch), seed & (2**64 - 1),
                               C.byref(h)))  # validates before touching the device
     return Graph(M=m, Ml=ml, EfSearch=efSearch, Distance=distance, Rng=seed, _handle=h)
+
+
+def sweep_device(metric: int, q_ptr, X_ptr, n: int, dim: int, out_ptr, stream=0):
+    """DistanceFunc batched sweep on device buffers (mhnsw_distance_device):
+    out[i] = distance(X[i], q) for n rows of dim contiguous floats."""
+    check(load().mhnsw_distance_device(metric, C.c_void_p(q_ptr), C.c_void_p(X_ptr), n, dim, C.c_void_p(out_ptr),
+                                       C.c_void_p(stream)))
 
 
 def merge_topk_device(keys_ptr, dist_ptr, n_ptr, shards, B, k, out_keys, out_dist, out_n, stream=0):

@@ -74,15 +74,15 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * (heuristic slack x100: c is dropped when alpha*d(c,kept) < d(u,c); 100 = HNSW
  * Alg. 4), "batch_min", "batch_max", "batch_ratio_pct", "vis_log2", "exact_kk",
  * "exact_precision" (exact-mode scoring: 0 f32-input MFMA, 1 bf16x3 split MFMA,
- * 2 fp16 2-product split MFMA (default); all preselect, re-rank canonically and
- * certify, so results are identical),
+ * 2 fp16 2-product split MFMA, 3 (default) fp16 1-product MFMA with the top-kk
+ * preselection fused into the GEMM epilogue; all preselect, re-rank canonically
+ * and certify, so results are identical),
  * "exact_tile" (split GEMM tile: 0 best measured per split, 1 128x256, 2 128x128,
  * 3 256x256), "compat_waves" (1 or 8 waves scoring the compat insert's
  * distance batches), "upper_ef" (beam mode: upper-layer descent width, 1 =
- * greedy), "screen" (beam mode and batched insert, bit set, default 1: bit 0
- * keeps an fp16 copy of the rows, bit 1 an int8 copy screened first; a
- * candidate is skipped only when a copy proves the f32 distance rejects it,
- * so results are unchanged);
+ * greedy), "screen" (beam mode and batched insert, default 1: keep an fp16
+ * copy of the rows; a candidate is skipped only when the copy proves the f32
+ * distance rejects it, so results are unchanged);
  * read-only: "pitch", "capacity", "strkeys", "strkey_relabels" */
 int mhnsw_set_option(mhnsw_index *h, const char *name, int64_t value);
 int mhnsw_get_option(const mhnsw_index *h, const char *name, int64_t *value);
@@ -186,7 +186,10 @@ int mhnsw_preview_levels(mhnsw_index *h, int64_t n, int32_t *out);
  * proposals, [6] searches issued, [7] exact-mode queries whose preselection
  * could not be certified and were redone by a full canonical sweep, [8] beam
  * candidates screened on the fp16 copy, [9] beam candidates evaluated in f32,
- * [10] beam candidates screened on the int8 copy */
+ * [10] batched-insert candidates screened on the fp16 copy, [11] batched-insert
+ * rows read in f32 (search evaluations + neighbour-selection rows), [12]
+ * device time of the batched insert's search kernels in microseconds (option
+ * "time_build" = 1: HIP events around each launch) */
 int mhnsw_stats(const mhnsw_index *h, int64_t *out, int n);
 int mhnsw_reset_stats(mhnsw_index *h);
 /* device time of the last search's main kernel (HIP events on its stream) */

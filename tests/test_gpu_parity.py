@@ -362,7 +362,7 @@ def _exact_inputs(rng, n, d, nq, metric):
     return X, Q
 
 
-@pytest.mark.parametrize("precision", [0, 1, 2])
+@pytest.mark.parametrize("precision", [0, 1, 2, 3])
 @pytest.mark.parametrize("metric,d", [(0, 24), (1, 24), (0, 768), (1, 768), (0, 1536), (1, 4096)])
 def test_exact_precision_parity(H, O, metric, d, precision):
     """Exact mode with f32-input MFMA scores (0), bf16x3 split scores (1) and
@@ -405,7 +405,7 @@ def test_exact_large_k(H, O, k):
     o = O.Graph(metric=0, order=O.ORDER_DEV, M=8, M0=16, Ml=0.25, EfSearch=32)
     o.import_graph(**g.export())
     rk, rd, rn = o.search(Q, k, mode=O.MODE_EXACT)
-    for precision in (2, 1, 0):
+    for precision in (3, 2, 1, 0):
         g.set_option("exact_precision", precision)
         gk, gd, gn = g.search_arrays(Q, k, mode=H.MODE_EXACT)
         _same_results(gk, gd, gn, rk, rd, rn)
@@ -427,7 +427,7 @@ def test_exact_certificate_fallback(H, O, metric):
                 ef_construction=32)
     g.add_arrays(np.arange(n), X)
     g.set_option("exact_kk", 10)
-    for precision in (2, 1, 0):
+    for precision in (3, 2, 1, 0):
         g.set_option("exact_precision", precision)
         g.reset_stats()
         gk, gd, gn = g.search_arrays(Q, 10, mode=H.MODE_EXACT)
@@ -463,7 +463,7 @@ def test_exact_h16_outside_bound(H, O, metric):
     rk, rd, rn = o.search(Q, 10, mode=O.MODE_EXACT)
     # every precision; the huge query's L2 distances all tie in f32, so its top-k
     # is decided by ids alone (the preselection must admit rows tying its bound)
-    for precision in (2, 1, 0):
+    for precision in (3, 2, 1, 0):
         g.set_option("exact_precision", precision)
         g.reset_stats()
         gk, gd, gn = g.search_arrays(Q, 10, mode=H.MODE_EXACT)

@@ -1,5 +1,5 @@
-"""GPU: the screening copies (option "screen": bit 0 fp16, bit 1 int8; DESIGN.md §6, "The fp16
-screening copy" and "The int8 screening copy") never change a beam search.  Every result (keys, f32 distance bits, counts) with the screen
+"""GPU: the fp16 screening copy (option "screen"; DESIGN.md §6, "The fp16
+screening copy") never changes a beam search or a batched build.  Every result (keys, f32 distance bits, counts) with the screen
 on must equal the screen-off search and the oracle's beam search, on data built
 to sit at the screen's edges: exact distance ties (integer-valued rows),
 duplicates, rows and queries outside the screen's validity range (huge, tiny,
@@ -38,7 +38,7 @@ def _search(g, Q, ef, H):
     return g.search_arrays(Q, 10, mode=H.MODE_BEAM, ef=ef)
 
 
-# dims cover every int8 row-load width (VPL 1, 2, 3, 4, 6 dwords per lane)
+# dims cover every lane-contiguous row-load width (VPL 1, 2, 3, 4, 6)
 @pytest.mark.parametrize("metric,d,n", [(0, 64, 20000), (1, 64, 20000), (0, 768, 6000), (1, 200, 8000),
                                         (1, 512, 4000), (0, 1024, 3000), (1, 1536, 2500)])
 def test_screen_identical_to_f32(H, O, metric, d, n):
@@ -56,22 +56,19 @@ def test_screen_identical_to_f32(H, O, metric, d, n):
         off = _search(g, Q, ef, H)
         st = g.stats()
         assert st["search_screened"] == 0 and st["search_f32_evals"] == st["search_dist_evals"]
-        assert st["search_screened_i8"] == 0
         _same_results(*off, *o.search(Q, 10, mode=O.MODE_BEAM, ef=ef))
-        for screen in (1, 2, 3):
-            g.set_option("screen", screen)
-            g.reset_stats()
-            on = _search(g, Q, ef, H)
-            st = g.stats()
-            assert (st["search_screened_i8"] > 0) == bool(screen & 2), (screen, st)
-            assert (st["search_screened"] > 0) == bool(screen & 1), (screen, st)
-            assert st["search_f32_evals"] < st["search_dist_evals"]
-            _same_results(*on, *off)
+        g.set_option("screen", 1)
+        g.reset_stats()
+        on = _search(g, Q, ef, H)
+        st = g.stats()
+        assert st["search_screened"] > 0, st
+        assert st["search_f32_evals"] < st["search_dist_evals"]
+        _same_results(*on, *off)
     g.close()
 
 
-@pytest.mark.parametrize("screen", [1, 3])
-def test_screen_follows_adds_and_import(H, O, screen):
+def test_screen_follows_adds_and_import(H, O):
+    screen = 1
     rng = np.random.default_rng(7)
     n, d = 6000, 96
     X, Q = _adversarial(rng, n, d, 0)
@@ -90,32 +87,31 @@ def test_screen_follows_adds_and_import(H, O, screen):
     g2.import_graph(**g.export())
     g2.reset_stats()
     _same_results(*on, *_search(g2, Q, 48, H))
-    assert g2.stats()["search_screened" if screen == 1 else "search_screened_i8"] > 0
+    assert g2.stats()["search_screened"] > 0
     g.close()
     g2.close()
 
 
-@pytest.mark.parametrize("screen", [1, 2])
-def test_screen_follows_metric_change(H, O, screen):
+def test_screen_follows_metric_change(H, O):
     """Distance is a public field (graph.go:309): switching it rewrites the
     screening copy in the new metric's format."""
     rng = np.random.default_rng(8)
     n, d = 5000, 128
     X, Q = _adversarial(rng, n, d, 1)
     g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=H.CosineDistance, Rng=3, build_mode=H.BUILD_BATCH,
-                ef_construction=64, heuristic=2, screen=screen)
+                ef_construction=64, heuristic=2, screen=1)
     g.add_arrays(np.arange(n), X)
     for dist, metric in ((H.EuclideanDistance, 1), (H.CosineDistance, 0)):
         g.Distance = dist
         g.reset_stats()
         on = _search(g, Q, 48, H)
-        assert g.stats()["search_screened" if screen == 1 else "search_screened_i8"] > 0
+        assert g.stats()["search_screened"] > 0
         o = O.Graph(metric=metric, order=O.ORDER_DEV, M=12, M0=24, Ml=0.3, EfSearch=48)
         o.import_graph(**g.export())
         _same_results(*on, *o.search(Q, 10, mode=O.MODE_BEAM, ef=48))
         g.set_option("screen", 0)
         _same_results(*on, *_search(g, Q, 48, H))
-        g.set_option("screen", screen)
+        g.set_option("screen", 1)
     g.close()
 
 
@@ -130,7 +126,7 @@ def test_screened_batch_build_identical(H, metric):
     n, d = 12000, 96
     X, _ = _adversarial(rng, n, d, metric)
     ex = {}
-    for screen, fuse in ((0, 0), (1, 0), (0, 1), (1, 1), (2, 1), (3, 1)):
+    for screen, fuse in ((0, 0), (1, 0), (0, 1), (1, 1)):
         g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
                     ef_construction=80, heuristic=2, keep_pruned=1, screen=screen, fuse_descent=fuse)
         g.add_arrays(np.arange(n // 3), X[: n // 3])   # two calls: later batches descend a multi-layer graph
@@ -138,5 +134,5 @@ def test_screened_batch_build_identical(H, metric):
         assert g.stats()["dropped_proposals"] == 0
         ex[(screen, fuse)] = g.export()
         g.close()
-    for key in ((1, 0), (0, 1), (1, 1), (2, 1), (3, 1)):
+    for key in ((1, 0), (0, 1), (1, 1)):
         _same_graph(ex[(0, 0)], ex[key])

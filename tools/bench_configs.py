@@ -92,14 +92,13 @@ if "5" in which:
     n, d, B = 1_000_000, 1536, 1024
     X = gen_vectors(n, d, 55, 12, 1000, dev, "cosine")
     Q = gen_vectors(B, d, 56, 12, 1000, dev, "cosine")
-    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_BATCH, m0=32,
-                ef_construction=64)
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_FLAT)
     g.reserve(n, d)
     g.add_device(np.arange(n), X.data_ptr(), n, d)
     S = Searcher(g, B, 10, d, dev)
     flops = 2.0 * B * n * d
     res = {}
-    for prec, name in ((0, "f32"), (1, "bf16x3"), (2, "fp16x2")):
+    for prec, name in ((3, "fp16x1_fused"), (2, "fp16x2"), (1, "bf16x3"), (0, "f32")):
         g.set_option("exact_precision", prec)
         S.run(Q, H.MODE_EXACT, 0)
         g.reset_stats()
@@ -113,8 +112,10 @@ if "5" in which:
                           "fp32_equiv_tflops_end_to_end": round(flops / dt / 1e12, 1),
                           "uncertified_per_batch": unc, "mfma_f32_peak_tflops": 157.3,
                           "mfma_bf16_dense_peak_tflops": 2500.0, "recall": 1.0}), flush=True)
-    same = all(torch.equal(a_, b_) for other in ("bf16x3", "fp16x2") for a_, b_ in zip(res["f32"], res[other]))
-    print(json.dumps({"config": "configs[4] exact: f32 vs bf16x3 vs fp16x2 results", "identical": same}), flush=True)
+    same = all(torch.equal(a_, b_) for other in ("bf16x3", "fp16x2", "fp16x1_fused")
+               for a_, b_ in zip(res["f32"], res[other]))
+    print(json.dumps({"config": "configs[4] exact: f32 vs bf16x3 vs fp16x2 vs fp16x1_fused results", "identical": same}),
+          flush=True)
     g.close()
     del X
 
@@ -123,14 +124,13 @@ if "5t" in which:  # bf16x3 GEMM tile variants (exact_tile option), same workloa
     n, d, B = 1_000_000, 1536, 1024
     X = gen_vectors(n, d, 55, 12, 1000, dev, "cosine")
     Q = gen_vectors(B, d, 56, 12, 1000, dev, "cosine")
-    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_BATCH, m0=16,
-                ef_construction=16)
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_FLAT)
     g.reserve(n, d)
     g.add_device(np.arange(n), X.data_ptr(), n, d)
     S = Searcher(g, B, 10, d, dev)
-    for prec in (1, 2):
+    for prec in (3, 1, 2):
         g.set_option("exact_precision", prec)
-        for tile in (1, 2, 3):
+        for tile in ((1, 2, 3, 4, 5, 6) if prec == 3 else (1, 2, 3)):
             g.set_option("exact_tile", tile)
             S.run(Q, H.MODE_EXACT, 0)
             dt, _ = timed(lambda: S.run(Q, H.MODE_EXACT, 0), reps=5)

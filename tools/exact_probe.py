@@ -1,5 +1,5 @@
 """Config-5 exact-path probe for kernel profiling: 1M x 1536 cosine, batch 1024,
-a minimal graph (the exact path ignores it), `reps` exact searches.
+a flat index (vector store only), `reps` exact searches.
 Usage: python tools/exact_probe.py [precision=1] [tile=0] [reps=3]"""
 import os
 import sys
@@ -19,8 +19,7 @@ dev = torch.device("cuda")
 n, d, B = 1_000_000, 1536, 1024
 X = gen_vectors(n, d, 55, 12, 1000, dev, "cosine")
 Q = gen_vectors(B, d, 56, 12, 1000, dev, "cosine")
-g = H.Graph(M=4, Ml=0.25, EfSearch=8, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_BATCH, m0=4,
-            ef_construction=4)
+g = H.Graph(M=4, Ml=0.25, EfSearch=8, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_FLAT)
 g.reserve(n, d)
 g.add_device(np.arange(n), X.data_ptr(), n, d)
 del X
