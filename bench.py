@@ -75,7 +75,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline time box (0 disables)")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
     p.add_argument("--one-gpu", action="store_true", help="map every rank to cuda:0 (multi-rank rehearsal)")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_search.json"))
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02_pmc_search.json"))
+    p.add_argument("--pmc-build-json", default=os.path.join(ROOT, "profiles", "r02_pmc_build.json"))
     return p.parse_args()
 
 
@@ -306,6 +307,17 @@ def main():
         byts = F * (4 * a.dim + 4) + Sc * (2 * a.dim + aux) + Xp * 4 * (a.M0 + 1) + a.nbase * (4 * a.dim + 16 * a.M0)
         us = bs["build_search_us"]
         gbs = byts / (us * 1e-6) / 1e9 if us > 0 else None
+        # HBM bytes of k_batch_search from a separate rocprofv3 --pmc pass of this
+        # same configuration (tools/profile_round.sh), when one is recorded
+        traffic = None
+        try:
+            pm = json.load(open(a.pmc_build_json))
+            want = dict(n=a.nbase, dim=a.dim, efc=a.efc, m0=a.M0, keep_pruned=a.keep_pruned, alpha=a.alpha,
+                        screen=a.screen)
+            if all(pm.get(k) == v for k, v in want.items()):
+                traffic = pm.get("hbm_bytes_total")
+        except (OSError, ValueError):
+            traffic = None
         return {"inserts_per_s": round(a.nbase / secs, 1), "seconds": round(secs, 2),
                 "dist_evals_per_insert": round(bs["build_dist_evals"] / a.nbase, 1),
                 "f32_rows_per_insert": round(F / a.nbase, 1), "screened_per_insert": round(Sc / a.nbase, 1),
@@ -313,7 +325,8 @@ def main():
                 "roofline": {"bound": "hbm", "kernel": "k_batch_search + k_batch_descend",
                              "kernel_ms_total": round(us / 1e3, 2), "alg_bytes": int(byts),
                              "achieved": round(gbs, 1) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None}}
+                             "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None,
+                             "traffic": traffic, "traffic_kernel": "k_batch_search"}}
 
     shard = shard_only
     queries_done = a.batch * a.steps * (1 if shard else world)
@@ -398,6 +411,9 @@ def main():
             "parallelism": f"{'shard' if shard else 'replica'}{world}",
         },
         "recall_at_10": round(recall, 4),
+        "parity": ("results bit-identical to oracle/, a C restatement of graph.go/distance.go (the Go toolchain "
+                   "is absent, so parity is to the restatement, pinned by the reference's own test vectors: "
+                   "tests/golden/reference_goldens.json); checked by pytest -m gpu, not inside this run"),
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -405,6 +421,7 @@ def main():
             "alg_bytes_per_launch": int(alg_bytes),
             "dist_evals_per_query": round(E / a.batch, 1), "expansions_per_query": round(Xp / a.batch, 1),
             "screened_per_query": round(Sc / a.batch, 1), "f32_evals_per_query": round(F / a.batch, 1),
+            "screen_margin": (g.get_option("screen_err_ppb") * 1e-9) if (g is not None and a.screen) else None,
         },
         "build": build_roofline(bstats, build_s),
         "sweep": sweep,

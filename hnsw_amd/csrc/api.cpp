@@ -996,7 +996,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
                     LCHK(h, launch_h1_filter(a, h->exact_tile, s));
                     const int64_t bqt = (nb + bm - 1) / bm;
                     LCHK(h, launch_bucket(h->h1region.p, h->h1rcnt.p, rcap, bqt * nnt, bqt, bm, H1_BN, nb, h->h1qcnt.p,
-                                          h->h1bucket.p, scap, h->h1ovf.p, s));
+                                          h->h1bucket.p, scap, h->h1ovf.p, a, s));
                     LCHK(h, launch_select_bucket(a, h->h1qcnt.p, h->h1bucket.p, scap, h->h1ovf.p, h->h1thr.p, s));
                 } else if (h2) {
                     a.xinv = h->xinv.p;
@@ -1267,6 +1267,7 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "exact_kk") {
         h->exact_kk = (int)v;
     } else if (n == "exact_tile") {
+        if (v < 0 || v > 6) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 6]");
         h->exact_tile = (int)v;
     } else if (n == "upper_ef") {
         if (v < 1 || v > 64) return fail(h, MHNSW_EINVAL, "upper_ef must be in [1, 64]");
@@ -1335,6 +1336,13 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "strkeys") *v = (int64_t)h->s2l.size();
     else if (n == "pitch") *v = h->pitch;
     else if (n == "capacity") *v = h->capn;
+    else if (n == "screen_err_ppb") {  // read-only: the fp16 copy's measured margin E, parts per 1e9
+        float e = 0.f;
+        if (h->h16err && (hipMemcpyAsync(&e, h->h16err, sizeof(float), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+                          hipStreamSynchronize(h->stream) != hipSuccess))
+            return MHNSW_EDEVICE;
+        *v = (int64_t)std::llround((double)e * 1e9);
+    }
     else return MHNSW_EINVAL;
     return MHNSW_OK;
 }

@@ -191,7 +191,8 @@ int launch_ring_prep(const float* thr, const float* qnorm, const float* qinv, in
                      float* sq, hipStream_t s);
 // qcnt [B * H1_BSUB * H1_CSTRIDE], bucket [B * H1_BSUB * scap]
 int launch_bucket(const uint2* region, const int32_t* region_cnt, int rcap, int64_t ntiles, int64_t nqt, int BM,
-                  int BN, int64_t B, int32_t* qcnt, uint2* bucket, int scap, uint8_t* qovf, hipStream_t s);
+                  int BN, int64_t B, int32_t* qcnt, uint2* bucket, int scap, uint8_t* qovf, const ExactArgs& a,
+                  hipStream_t s);
 int launch_select_bucket(const ExactArgs& a, const int32_t* qcnt, const uint2* bucket, int scap, const uint8_t* qovf,
                          const float* thr, hipStream_t s);
 // err (nullable): running max of the rows' relative fp16 rounding |x' - x| / |x|

@@ -365,8 +365,12 @@ __device__ __forceinline__ void ring_stage(const uint16_t* buf, f32x16 (&acc)[TM
     RingFrag<T, TM, TN> f[S];
 #pragma unroll
     for (int sb = 0; sb < S; ++sb) ring_load<T, TM, TN>(buf + sb * T::KBE, f[sb], wm, wn, li, lh);
+    // priority 1 while this wave's MFMA cluster issues (cdna_hip_programming.md T5:
+    // keeps the cluster between the barriers instead of among the DMA issues)
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int sb = 0; sb < S; ++sb) ring_mma<T, MODE, TM, TN>(f[sb], acc);
+    __builtin_amdgcn_s_setprio(0);
 }
 
 // the score of one (query, row) pair from its accumulator -- the one formula
@@ -476,13 +480,20 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_ring(ExactArg
     }
     const int nst = a.pitch / (X3K * S);  // ring stages
     const int li = lane & 31, lh = lane >> 5;
+    // issue() is called for stages 0, 1, 2, ... in order: each piece's base
+    // advances by one stage per call and stops at the last stage (past the end
+    // the DMA re-reads it), a scalar add instead of a 64-bit multiply per piece
+    int next_st = 0;
     auto issue = [&](uint16_t* buf, int st) {
-        const int64_t kb = min(st, nst - 1);
+        (void)st;
+        const bool adv = next_st < nst - 1;
+        ++next_st;
 #pragma unroll
         for (int j = 0; j < T::PER; ++j) {
             // the stage's base in scalar registers, the lane's offset added last:
             // global_load_lds with an SGPR base and a 32-bit VGPR offset
-            const uint64_t ub = reinterpret_cast<uint64_t>(pb[j] + kb * pstep[j]);
+            const uint64_t ub = reinterpret_cast<uint64_t>(pb[j]);
+            if (adv) pb[j] += pstep[j];
             const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ub) |
                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(ub >> 32)) << 32);
             x3_dma(reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(sb) + poff[j]), buf + lofs[j]);
@@ -541,15 +552,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_ring(ExactArg
         // (k_select_bucket recomputes split_score).  Passing pairs go to this
         // wave's slice of the tile's region: {row offset | query offset << 16, acc}.
         bool rok[TN];
-        float w0[TN], w1[TN], rxi[TN], rxn[TN];
+        float w0[TN], w1[TN];
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int64_t xr = n0 + wn * TN * 32 + j * 32 + li;
             rok[j] = xr < a.N && !(a.dead && a.dead[xr]);
             const int64_t xc = xr < a.N ? xr : a.N - 1;
             const float xi = a.xinv[xc], xn = a.xnorm[xc];
-            rxi[j] = xi;
-            rxn[j] = xn;
             if (a.metric == COSINE) {
                 w0[j] = xn / xi;  // xi is a power of two (or NaN: every query passes the row)
                 w1[j] = 0.f;
@@ -601,19 +610,15 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_ring(ExactArg
                                 if (lane == first) base = atomicAdd(tile_ctr, __popcll(m));
                                 base = __shfl(base, first, 64);
                                 const int qo = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                                // every counted slot is written: a padded query (q >= B, bound
-                                // +inf) can still pass on a NaN bound (zero row) and is stored
-                                // with score +inf, which the bucket pass skips
+                                // every counted slot is written (a padded query, q >= B, can pass
+                                // on a NaN bound; k_bucket skips it).  The raw accumulator is
+                                // stored: k_bucket turns it into split_score's float.
                                 if (pass) {
                                     const int e = base + __builtin_amdgcn_mbcnt_hi(
                                                              (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
                                     const int ro = wn * TN * 32 + j * 32 + li;
-                                    const float sc = q0 + qo < a.B
-                                                         ? split_score(MODE, a.metric, v, rxi[j], a.qinv[q0 + qo],
-                                                                       a.qnorm[q0 + qo], rxn[j])
-                                                         : __builtin_inff();
                                     if (e < a.rcap)
-                                        reg[e] = make_uint2((uint32_t)ro | ((uint32_t)qo << 16), __float_as_uint(sc));
+                                        reg[e] = make_uint2((uint32_t)ro | ((uint32_t)qo << 16), __float_as_uint(v));
                                 }
                             }
                         }
@@ -729,7 +734,7 @@ int launch_ring_prep(const float* thr, const float* qnorm, const float* qinv, in
 // marked, and k_select_bucket sends it to the canonical fallback.
 __global__ __launch_bounds__(64) void k_bucket(const uint2* region, const int32_t* region_cnt, int rcap, int64_t ntiles,
                                                int64_t nqt, int BM, int BN, int64_t B, int32_t* qcnt, uint2* bucket,
-                                               int scap, uint8_t* qovf) {
+                                               int scap, uint8_t* qovf, ExactArgs a) {
     const int64_t t = blockIdx.x;
     if (t >= ntiles) return;
     const int lane = lane_id();
@@ -747,16 +752,20 @@ __global__ __launch_bounds__(64) void k_bucket(const uint2* region, const int32_
         const int64_t q = q0 + (v.x >> 16);
         if (q >= B) continue;
         const uint32_t row = (uint32_t)(n0 + (v.x & 0xFFFFu));
+        // the epilogue stored the raw accumulator: its score, split_score's float
+        const float sc = split_score(RING_H1, a.metric, __uint_as_float(v.y), a.xinv[row], a.qinv[q], a.qnorm[q],
+                                     a.xnorm[row]);
         const int pos = atomicAdd(&qcnt[(q * H1_BSUB + sub) * H1_CSTRIDE], 1);
-        if (pos < scap) bucket[(q * H1_BSUB + sub) * scap + pos] = make_uint2(row, v.y);
+        if (pos < scap) bucket[(q * H1_BSUB + sub) * scap + pos] = make_uint2(row, __float_as_uint(sc));
     }
 }
 
 int launch_bucket(const uint2* region, const int32_t* region_cnt, int rcap, int64_t ntiles, int64_t nqt, int BM,
-                  int BN, int64_t B, int32_t* qcnt, uint2* bucket, int scap, uint8_t* qovf, hipStream_t s) {
+                  int BN, int64_t B, int32_t* qcnt, uint2* bucket, int scap, uint8_t* qovf, const ExactArgs& a,
+                  hipStream_t s) {
     if (ntiles <= 0) return 0;
     hipLaunchKernelGGL(k_bucket, dim3((unsigned)ntiles), dim3(64), 0, s, region, region_cnt, rcap, ntiles, nqt, BM, BN,
-                       B, qcnt, bucket, scap, qovf);
+                       B, qcnt, bucket, scap, qovf, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -77,13 +77,18 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * 2 fp16 2-product split MFMA, 3 (default) fp16 1-product MFMA with the top-kk
  * preselection fused into the GEMM epilogue; all preselect, re-rank canonically
  * and certify, so results are identical),
- * "exact_tile" (split GEMM tile: 0 best measured per split, 1 128x256, 2 128x128,
- * 3 256x256), "compat_waves" (1 or 8 waves scoring the compat insert's
+ * "exact_tile" (GEMM tile, 0 = the measured best per precision; precisions 1/2:
+ * 1 128x256, 2 128x128, 3-6 256x256; precision 3: 1 256x256 S2 R4, 2 256x256
+ * S4 R2, 3 256x256 S1 R4, 4 128x256 S2 R4, 5 128x256 S2 R3 (the default),
+ * 6 128x256 on 4 waves S2 R3 -- S = 16-deep K-blocks per stage, R = ring
+ * buffers), "compat_waves" (1 or 8 waves scoring the compat insert's
  * distance batches), "upper_ef" (beam mode: upper-layer descent width, 1 =
  * greedy), "screen" (beam mode and batched insert, default 1: keep an fp16
  * copy of the rows; a candidate is skipped only when the copy proves the f32
  * distance rejects it, so results are unchanged);
- * read-only: "pitch", "capacity", "strkeys", "strkey_relabels" */
+ * read-only: "pitch", "capacity", "strkeys", "strkey_relabels",
+ *            "screen_err_ppb" (the fp16 screening copy's measured max relative
+ *            rounding E, the margin its rejects use, in parts per 1e9) */
 int mhnsw_set_option(mhnsw_index *h, const char *name, int64_t value);
 int mhnsw_get_option(const mhnsw_index *h, const char *name, int64_t *value);
 /* Graph.Validate (graph.go:916-937) */
