@@ -40,6 +40,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import hnsw_amd as H  # noqa: E402
+
+# revision of the search/build kernels the recorded PMC passes (profiles/*_pmc_*.json)
+# were taken on; a pass recorded on another revision is not attached as `traffic`
+KERNEL_REV = "r02-screened-selection"
 from hnsw_amd.shard import engine_local_search, shard_range, sharded_search  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -313,7 +317,7 @@ def main():
         try:
             pm = json.load(open(a.pmc_build_json))
             want = dict(n=a.nbase, dim=a.dim, efc=a.efc, m0=a.M0, keep_pruned=a.keep_pruned, alpha=a.alpha,
-                        screen=a.screen)
+                        screen=a.screen, rev=KERNEL_REV)
             if all(pm.get(k) == v for k, v in want.items()):
                 traffic = pm.get("hbm_bytes_total")
         except (OSError, ValueError):
@@ -376,7 +380,7 @@ def main():
         try:
             pm = json.load(open(a.pmc_json))
             want = dict(n=a.nbase, dim=a.dim, batch=a.batch, ef=a.ef, efc=a.efc, m0=a.M0, keep_pruned=a.keep_pruned,
-                        alpha=a.alpha, screen=a.screen)
+                        alpha=a.alpha, screen=a.screen, rev=KERNEL_REV)
             if all(pm.get(k) == v for k, v in want.items()):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:

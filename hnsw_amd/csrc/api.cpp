@@ -1013,6 +1013,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
                 LCHK(h, launch_exact_scores(a, s));
             }
             if (!h1) LCHK(h, launch_exact_select(a, s));
+            if (h1 && h->exact_tile >= 7) continue;  // timing diagnostic: no re-rank, no results
             HIPCHK(h, hipMemsetAsync(h->xnflag.p, 0, sizeof(int32_t), s));
             CertArgs c1 = cert;
             c1.bound = h->xbound.p;
@@ -1029,6 +1030,8 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             LCHK(h, launch_rerank(a.Q, g, h->cand.p, kk, nb, h->lpr, h->vpl, k, ok_, od_, on_, oi_, c2, s));
         }
         if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));
+        if (h->exact_precision == 3 && h->n >= H1_BN && h->exact_tile >= 7)
+            return fail(h, MHNSW_EUNSUPPORTED, "exact_tile %d is a timing diagnostic: no results", h->exact_tile);
     } else {
         if ((r = sync_layer_entries(h))) return r;
         if ((r = sync_layer_table(h)) || (r = order_meta(h, s))) return r;
@@ -1267,7 +1270,7 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "exact_kk") {
         h->exact_kk = (int)v;
     } else if (n == "exact_tile") {
-        if (v < 0 || v > 6) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 6]");
+        if (v < 0 || v > 9) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 9]");
         h->exact_tile = (int)v;
     } else if (n == "upper_ef") {
         if (v < 1 || v > 64) return fail(h, MHNSW_EINVAL, "upper_ef must be in [1, 64]");

@@ -629,6 +629,13 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
         bl_at(L, 0, d0, i0);
         if (lane == 0 && i0 != EMPTY_ID) a.cur_entry[u] = i0 & ID_MASK;
         // neighbour selection
+        bool sel_screen = false;
+        float margin = 0.f;
+        if constexpr (SCREEN) {
+            sel_screen = a.g.h16 != nullptr && a.alpha > 0.f;
+            const float e = a.g.h16err ? *a.g.h16err : 0.00048828125f;
+            margin = a.g.metric == EUCLIDEAN ? h16_margin_l2(e) : h16_margin_cos(e);
+        }
         uint32_t sel = 0;
         float seld = 0.f;
         int nsel = 0;
@@ -646,10 +653,32 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
                 load_query(qc, a.g.vecs + (size_t)c * a.g.pitch);
                 const float cn = a.g.norms[c];
                 st.E += nsel;
-                st.F += nsel + 1;  // the candidate's row and the kept rows, in f32
-                eval_list<C, G>(a.g, qc, cn, sel, nsel, a.g.metric, [&](float dcs, uint32_t) {
+                auto rule = [&](float dcs, uint32_t) {
                     if (a.alpha * dcs < dc) good = false;
-                });
+                };
+                // Screened (fp16 copy): a kept row r whose distance to c is
+                // certainly above hi cannot drop c, one certainly below lo does;
+                // only the undecided rows are evaluated in f32.  hi / lo bracket
+                // dc / alpha so that fl(alpha * d) >= dc for every d > hi and
+                // < dc for every d < lo, hence the same decision.
+                if (SCREEN && sel_screen && dc > 0.f && h16_query_ok(cn)) {
+                    const float t = dc / a.alpha;
+                    const float hi = t * (1.0f + 0x1p-20f), lo = t * (1.0f - 0x1p-20f);
+                    const int cls = screen_pairs<C, G>(a.g, qc, cn, sel, nsel, a.g.metric, lo, hi, margin);
+                    st.S += nsel;
+                    st.F += 1;  // the candidate's row
+                    if (__ballot(lane < nsel && cls < 0)) {
+                        good = false;
+                    } else {
+                        int nu;
+                        const uint32_t und = compact(sel, lane < nsel && cls == 0, nu);
+                        st.F += nu;
+                        if (nu > 0) eval_list<C, G>(a.g, qc, cn, und, nu, a.g.metric, rule);
+                    }
+                } else {
+                    st.F += nsel + 1;  // the candidate's row and the kept rows, in f32
+                    eval_list<C, G>(a.g, qc, cn, sel, nsel, a.g.metric, rule);
+                }
             }
             if (good) {
                 if (lane == nsel) {

@@ -359,6 +359,18 @@ __device__ __forceinline__ bool h16_rejects_l2(float s, float xn, float wd, floa
     return da >= H16_MIN_L2 && da * H16_REL_L2 - ml2 * xn > wd;
 }
 
+// The other side, for the neighbour-selection screen: true when the f32
+// distance is certainly < lo (same bounds as the rejects, mirrored, with the
+// relative slack doubled for the rounding of the upper bound itself).
+__device__ __forceinline__ bool h16_below_cos(float s, float qn, float lo, float mcos) {
+    const float da = 1.0f - (s * H16_COS_SCALE) / qn;
+    return da < lo - mcos;
+}
+__device__ __forceinline__ bool h16_below_l2(float s, float xn, float lo, float ml2) {
+    const float da = sqrtf(s);
+    return da >= H16_MIN_L2 && da * (2.0f - H16_REL_L2 * H16_REL_L2) + ml2 * xn * (2.0f - H16_REL_L2) < lo;
+}
+
 // finalize a canonical sum into a distance (distance.go:15-23 semantics)
 __device__ __forceinline__ float finalize(int metric, float s, float xn, float qn) {
     if (metric == COSINE) return 1.0f - s / (xn * qn);

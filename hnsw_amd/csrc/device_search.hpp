@@ -147,6 +147,61 @@ __device__ __forceinline__ int eval_screened(const GraphDev& g, const QReg<C>& q
     return cnt2;
 }
 
+// Two-sided screen of the rows cid[0, cnt) against a stored row held as the
+// "query" q (norm qn), for the selection rule "r drops c when alpha d(c, r) <
+// d(u, c)": lane t gets +1 when row t's f32 distance is certainly > hi, -1
+// when it is certainly < lo, 0 when the fp16 estimate cannot tell (those go
+// to the canonical f32 path).  Rows outside the copy's range are always 0.
+template <class C, int G>
+__device__ __forceinline__ int screen_pairs(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int cnt,
+                                            int metric, float lo, float hi, float margin) {
+    constexpr int GH = (2 * G <= C::LPR) ? 2 * G : G;
+    using RM = RowMap<C, GH>;
+    const int lane = lane_id();
+    int cls = 0;
+    for (int base = 0; base < cnt; base += RM::T) {
+        uint32_t ids[GH];
+        bool valid[GH];
+        float inv[GH];
+#pragma unroll
+        for (int gg = 0; gg < GH; ++gg) {
+            const int t = base + RM::reg_row(gg, lane);
+            valid[gg] = t < cnt;
+            if constexpr (C::RPI == 1)
+                ids[gg] = rl_u(cid, (base + gg) & 63);
+            else
+                ids[gg] = shfl_u(cid, t & 63);
+            ids[gg] = valid[gg] ? guard_id(g, ids[gg]) : 0u;
+        }
+        const int town = base + RM::owned_row(lane);
+        int c = 0;
+        if (metric == EUCLIDEAN) {
+            float xn[GH];
+#pragma unroll
+            for (int gg = 0; gg < GH; ++gg) {
+                const float2 ax = g.h16aux[ids[gg]];
+                inv[gg] = ax.x;
+                xn[gg] = ax.y;
+            }
+            const float s = eval_rows_h16<C, GH, true>(q, g.h16, g.pitch, ids, valid, inv);
+            float xo = xn[0];
+#pragma unroll
+            for (int gg = 1; gg < GH; ++gg)
+                if (RM::reg_row(gg, lane) == town - base) xo = xn[gg];
+            if (town < cnt) c = h16_rejects_l2(s, xo, hi, margin) ? 1 : h16_below_l2(s, xo, lo, margin) ? -1 : 0;
+        } else {
+#pragma unroll
+            for (int gg = 0; gg < GH; ++gg) inv[gg] = 1.f;
+            const float s = eval_rows_h16<C, GH, false>(q, g.h16, g.pitch, ids, valid, inv);
+            if (town < cnt) c = h16_rejects_cos(s, qn, hi, margin) ? 1 : h16_below_cos(s, qn, lo, margin) ? -1 : 0;
+        }
+        const int t = lane - base;
+        const int src = (t >= 0 && t < RM::T) ? RM::owner(t) : lane;
+        const int ct = __shfl(c, src, 64);
+        if (t >= 0 && t < RM::T) cls = ct;
+    }
+    return cls;
+}
 
 struct WaveStats {
     unsigned long long E = 0, X = 0, resets = 0;

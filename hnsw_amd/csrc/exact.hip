@@ -401,7 +401,10 @@ __device__ __forceinline__ float split_score(int mode, int metric, float acc, fl
 // tile_stride, 2 tile_stride, ..., into a compact [B x ns] sample matrix); EPI 1 keeps
 // only the pairs that can beat the query's threshold (RingFilter, below) --
 // the fused top-k: no score matrix.
-template <int WAVES_M, int WAVES_N, int TM, int TN, int MODE, int S, int R, int EPI>
+// DIAG (timing diagnostics, exact_tile 7-9; no pair passes, so every query
+// goes to the canonical fallback and results stay exact): 1 no epilogue, 2 also
+// no waits / barriers in the main loop, 3 also no DMA.
+template <int WAVES_M, int WAVES_N, int TM, int TN, int MODE, int S, int R, int EPI, int DIAG = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_ring(ExactArgs a) {
     using T = RingTile<WAVES_M, WAVES_N, TM, TN, MODE, S>;
     static_assert(R >= 2 && R <= 4, "ring depth");
@@ -505,17 +508,32 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_ring(ExactArg
     constexpr int WAIT = (NWT & 15) | ((NWT >> 4) << 14) | (0x7 << 4) | (0xF << 8);
     uint16_t* const bufs[4] = {B0, B1, B2, B3};
 #pragma unroll
-    for (int p = 0; p < R - 1; ++p) issue(bufs[p], p);
+    for (int p = 0; p < R - 1; ++p)
+        if (DIAG < 3) issue(bufs[p], p);
     for (int kt = 0; kt < nst; kt += R) {
 #pragma unroll
         for (int u = 0; u < R; ++u) {
-            __builtin_amdgcn_s_waitcnt(WAIT);
-            __builtin_amdgcn_s_barrier();
-            issue(bufs[(u + R - 1) % R], kt + u + R - 1);
+            if (DIAG < 2) {
+                __builtin_amdgcn_s_waitcnt(WAIT);
+                __builtin_amdgcn_s_barrier();
+            }
+            if (DIAG < 3) issue(bufs[(u + R - 1) % R], kt + u + R - 1);
             if (u == 0 || kt + u < nst) stage(bufs[u]);
         }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no DMA may land after the workgroup ends
+    if constexpr (DIAG > 0) {
+        float keep = 0.f;  // keeps the MFMAs live
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) keep += acc[i][j][r];
+        __syncthreads();
+        if (tid == 0) a.region_cnt[logical] = keep == -1.0e38f ? 1 : 0;
+        return;
+    }
     // accumulator layout: D col = lane&31 (base row), row = (r&3) + 8*(r>>2) + 4*(lane>>5) (query)
     if constexpr (EPI == 0) {
         const int64_t col0 = EPI == 0 && a.nsample_tiles > 0 ? nt * T::BN : n0;  // sample: compact columns
@@ -635,13 +653,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_ring(ExactArg
     }
 }
 
-template <int WM_, int WN_, int TM_, int TN_, int MODE, int S, int R, int EPI>
+template <int WM_, int WN_, int TM_, int TN_, int MODE, int S, int R, int EPI, int DIAG = 0>
 static int launch_ring_t(const ExactArgs& a, hipStream_t s) {
     using T = RingTile<WM_, WN_, TM_, TN_, MODE, S>;
     if (a.pitch % (X3K * S)) return -5;
     const int64_t nqt = (a.B + T::BM - 1) / T::BM;
     const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + T::BN - 1) / T::BN;
-    hipLaunchKernelGGL((k_scores_ring<WM_, WN_, TM_, TN_, MODE, S, R, EPI>), dim3((unsigned)(nqt * nnt)), dim3(T::NT),
+    hipLaunchKernelGGL((k_scores_ring<WM_, WN_, TM_, TN_, MODE, S, R, EPI, DIAG>), dim3((unsigned)(nqt * nnt)), dim3(T::NT),
                        0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -678,10 +696,13 @@ static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
         case 4: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 4, EPI>(a, s);
         case 5: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 3, EPI>(a, s);
         case 6: return launch_ring_t<1, 4, 4, 2, RING_H1, 2, 3, EPI>(a, s);
+        case 7: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 3, EPI, EPI ? 1 : 0>(a, s);
+        case 8: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 3, EPI, EPI ? 2 : 0>(a, s);
+        case 9: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 3, EPI, EPI ? 3 : 0>(a, s);
         default: return launch_ring_t<2, 4, 4, 2, RING_H1, 2, 4, EPI>(a, s);
     }
 }
-int h1_tile_bm(int variant) { return variant == 0 || (variant >= 4 && variant <= 6) ? 128 : 256; }
+int h1_tile_bm(int variant) { return variant == 0 || (variant >= 4 && variant <= 9) ? 128 : 256; }
 int launch_h1_sample(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<0>(a, variant, s); }
 int launch_h1_filter(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<1>(a, variant, s); }
 

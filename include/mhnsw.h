@@ -81,7 +81,9 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * 1 128x256, 2 128x128, 3-6 256x256; precision 3: 1 256x256 S2 R4, 2 256x256
  * S4 R2, 3 256x256 S1 R4, 4 128x256 S2 R4, 5 128x256 S2 R3 (the default),
  * 6 128x256 on 4 waves S2 R3 -- S = 16-deep K-blocks per stage, R = ring
- * buffers), "compat_waves" (1 or 8 waves scoring the compat insert's
+ * buffers; 7-9 timing diagnostics of 5 that let no pair pass, so every query
+ * takes the canonical fallback: 7 no epilogue, 8 also no waits/barriers,
+ * 9 also no DMA), "compat_waves" (1 or 8 waves scoring the compat insert's
  * distance batches), "upper_ef" (beam mode: upper-layer descent width, 1 =
  * greedy), "screen" (beam mode and batched insert, default 1: keep an fp16
  * copy of the rows; a candidate is skipped only when the copy proves the f32
