@@ -50,6 +50,7 @@ SIGNATURES = {
     "mhnsw_layer_count": (C.c_int64, [_vp, C.c_int]),
     "mhnsw_connectivity": (C.c_int, [_vp, _P(C.c_double), C.c_int]),
     "mhnsw_delete": (C.c_int, [_vp, _i64p, C.c_int64, _u8p]),
+    "mhnsw_replace": (C.c_int, [_vp, _i64p, _f32p, C.c_int64, C.c_int, _u8p]),
     "mhnsw_distance": (C.c_int, [C.c_int, _f32p, _f32p, C.c_int64, C.c_int, _f32p]),
     "mhnsw_distance_device": (C.c_int, [C.c_int, _vp, _vp, C.c_int64, C.c_int, _vp, _vp]),
     "mhnsw_export_sizes": (C.c_int, [_vp, _i64p, _P(C.c_int), _P(C.c_int), _P(C.c_int)]),

@@ -47,10 +47,19 @@ class ExactIndex:
             return
         latest = {}
         for k, v in zip(keys, vectors):  # later entries of one batch win, like successive map stores
-            latest[k] = v
+            latest[k] = np.asarray(v, np.float32).ravel()
         ks = list(latest)
-        self._g.BatchDelete(ks)  # replacement = map assignment
-        self._g.BatchAdd([Node(k, np.asarray(latest[k], np.float32)) for k in ks])
+        # validate the whole batch first, so a failing batch changes nothing
+        d0 = self._g.Dims() or latest[ks[0]].size
+        for k in ks:
+            if latest[k].size != d0:
+                raise HnswError(-2, f"embedding dimension mismatch: {d0} != {latest[k].size}")
+        # replacement = map assignment: present keys are overwritten in place
+        # (the store does not grow), the others are added
+        present = self._g.Replace([Node(k, latest[k]) for k in ks]) if self._g.Len() else [False] * len(ks)
+        new = [Node(k, latest[k]) for k, p in zip(ks, present) if not p]
+        if new:
+            self._g.BatchAdd(new)
 
     def Search(self, query, k: int) -> List[Node]:  # exact.go:62-109
         if self.Len() == 0:

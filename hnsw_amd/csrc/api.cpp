@@ -2022,6 +2022,60 @@ int mhnsw_search_negatives(mhnsw_index* h, const float* queries, int64_t B, int 
 }
 
 // graph.go:843-895 Delete / BatchDelete
+// ExactIndex replace-on-Add (hybrid/exact.go:28-59) on a FLAT handle: rows of
+// present keys are overwritten in place, so repeated Adds of one key neither
+// grow the store nor leave dead rows for the exact path to scan.
+int mhnsw_replace(mhnsw_index* h, const int64_t* keys, const float* vecs, int64_t n, int dim, uint8_t* out) {
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    if (int r0 = drain(h)) return r0;
+    if (n > 0 && (!keys || !vecs || !out)) return fail(h, MHNSW_EINVAL, "keys, vecs and out must be non-NULL");
+    if (h->build_mode != MHNSW_BUILD_FLAT) return fail(h, MHNSW_EUNSUPPORTED, "replace needs a flat (build_mode 2) handle");
+    for (int64_t i = 0; i < n; ++i) out[i] = 0;
+    if (n <= 0 || !h->layers_exist) return 0;
+    if (dim != h->dim) return fail(h, MHNSW_EDIM, "embedding dimension mismatch: %d != %d", h->dim, dim);
+    std::vector<int32_t> ids;
+    std::vector<int64_t> src;
+    {
+        std::unordered_map<int64_t, int> seen;
+        for (int64_t i = 0; i < n; ++i) {
+            if (seen.count(keys[i])) return fail(h, MHNSW_EINVAL, "duplicate key %lld in replace", (long long)keys[i]);
+            seen[keys[i]] = 1;
+        }
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        auto it = h->key2id.find(keys[i]);
+        if (it == h->key2id.end()) continue;
+        out[i] = 1;
+        ids.push_back(it->second);
+        src.push_back(i);
+    }
+    if (ids.empty()) return 0;
+    const int64_t m = (int64_t)ids.size();
+    int r;
+    // the present keys' vectors, compacted on the host, padded on the device
+    std::vector<float> hv((size_t)m * dim);
+    for (int64_t j = 0; j < m; ++j) std::memcpy(&hv[(size_t)j * dim], vecs + (size_t)src[j] * dim, (size_t)dim * 4);
+    if ((r = ensure_buf(h, h->tmp, (size_t)m * dim + (size_t)m * h->pitch + (size_t)m))) return r;
+    float* staged = h->tmp.p;
+    float* padded = h->tmp.p + (size_t)m * dim;
+    int32_t* dids = reinterpret_cast<int32_t*>(padded + (size_t)m * h->pitch);
+    HIPCHK(h, hipMemcpyAsync(staged, hv.data(), hv.size() * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(dids, ids.data(), (size_t)m * 4, hipMemcpyHostToDevice, h->stream));
+    LCHK(h, launch_pad_rows(staged, m, dim, padded, h->pitch, h->stream));
+    LCHK(h, launch_scatter_rows(padded, dids, m, h->pitch, h->vecs, h->stream));
+    // norms, the screening copy and the exact path's planes of the touched range
+    // (rows in between are recomputed to the same values; the copies' measured
+    // error maxima only grow, so their margins stay valid)
+    const int64_t lo = *std::min_element(ids.begin(), ids.end()), hi = *std::max_element(ids.begin(), ids.end()) + 1;
+    LCHK(h, launch_norms(h->vecs, lo, hi, h->pitch, h->lpr, h->vpl, h->norms, h->stream));
+    if (h->screen & 1 && h->h16 && h->h16_metric == h->metric)
+        LCHK(h, launch_h16_rows(h->vecs, h->norms, lo, hi, h->pitch, h->metric, h->h16, h->h16aux, h->h16err,
+                                h->stream));
+    h->xsplit_rows = std::min(h->xsplit_rows, lo);
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
 int mhnsw_delete(mhnsw_index* h, const int64_t* keys, int64_t n, uint8_t* out) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
     if (int r0 = drain(h)) return r0;

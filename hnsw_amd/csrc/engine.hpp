@@ -66,6 +66,7 @@ constexpr int NEG_MAX_CAND = 256;
 int launch_negatives(const NegArgs& a, int lpr, int vpl, hipStream_t s);
 
 int launch_pad_rows(const float* src, int64_t n, int dim, float* dst, int pitch, hipStream_t s);
+int launch_scatter_rows(const float* src, const int32_t* ids, int64_t n, int pitch, float* dst, hipStream_t s);
 // err: running max of the rows' measured relative rounding (GraphDev::h16err)
 int launch_h16_rows(const float* X, const float* norms, int64_t n0, int64_t n1, int pitch, int metric, uint16_t* H,
                     float2* aux, float* err, hipStream_t s);

@@ -28,6 +28,25 @@ int launch_pad_rows(const float* src, int64_t n, int dim, float* dst, int pitch,
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// dst row ids[i] <- padded row i of src (rows already padded to pitch)
+__global__ void k_scatter_rows(const float* __restrict__ src, const int32_t* __restrict__ ids, int64_t n, int pitch,
+                               float* __restrict__ dst) {
+    const int64_t total = n * (int64_t)pitch;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / pitch;
+        dst[(size_t)ids[r] * pitch + (i - r * pitch)] = src[i];
+    }
+}
+
+int launch_scatter_rows(const float* src, const int32_t* ids, int64_t n, int pitch, float* dst, hipStream_t s) {
+    if (n <= 0) return 0;
+    int64_t total = n * pitch;
+    int64_t grid = (total + 255) / 256;
+    if (grid > 65536) grid = 65536;
+    hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)grid), dim3(256), 0, s, src, ids, n, pitch, dst);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // canonical |x| per row: one wave handles RPI rows per step
 template <class C>
 __global__ __launch_bounds__(256) void k_norms(const float* __restrict__ X, int64_t n0, int64_t n1, int pitch,

@@ -336,6 +336,30 @@ class Graph:
         self._check(load().mhnsw_add_device(self._h, _ptr(keys, C.c_int64), C.c_void_p(vecs_dev_ptr), n, dim,
                                             None if lv is None else _ptr(lv, C.c_int32)))
 
+    def Replace(self, nodes: Sequence[Node]) -> List[bool]:
+        """Flat handles (build_mode 2): overwrite the vectors of present keys in
+        place (hybrid/exact.go:28-59 map assignment); -> which keys were present."""
+        if not nodes:
+            return []
+        vecs = [np.asarray(n.Value, dtype=np.float32).ravel() for n in nodes]
+        self._sync()
+        imgs = np.ascontiguousarray(self.encode_keys([n.Key for n in nodes]), np.int64)
+        out = self.replace_arrays(imgs, np.stack(vecs))
+        for n, v, ok in zip(nodes, vecs, out):
+            if ok:
+                self._values[n.Key] = v
+        return [bool(x) for x in out]
+
+    def replace_arrays(self, keys, vecs) -> np.ndarray:
+        """Array form of Replace: keys int64[n] (engine images), vecs float32[n, dim]."""
+        self._sync()
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        vecs = _f32(vecs).reshape(len(keys), -1)
+        out = np.zeros(max(len(keys), 1), np.uint8)
+        self._check(load().mhnsw_replace(self._h, _ptr(keys, C.c_int64), _ptr(vecs, C.c_float), len(keys),
+                                         vecs.shape[1], _ptr(out, C.c_uint8)))
+        return out[: len(keys)].astype(bool)
+
     def reserve(self, n: int, dim: int):
         self._check(load().mhnsw_reserve(self._h, n, dim))
 

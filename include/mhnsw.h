@@ -153,6 +153,15 @@ int mhnsw_connectivity(mhnsw_index *h, double *out, int max_layers);
  * Deleted rows are never returned by BEAM or EXACT searches. */
 int mhnsw_delete(mhnsw_index *h, const int64_t *keys, int64_t n, uint8_t *out);
 
+/* ---- ExactIndex replace-on-Add (hnsw-extensions/hybrid/exact.go:28-59: Add of
+ * a present key is a map assignment) ----
+ * FLAT build mode only (a vector store without links).  For every key present,
+ * its row's vector is overwritten in place (norms, the fp16 screening copy and
+ * the exact path's split planes follow); out[i] = 1 when keys[i] was present,
+ * 0 otherwise (the caller adds those).  Keys must be distinct.  Nothing is
+ * written unless every argument is valid. */
+int mhnsw_replace(mhnsw_index *h, const int64_t *keys, const float *vecs, int64_t n, int dim, uint8_t *out);
+
 /* ---- DistanceFunc (distance.go:12-23): batched sweep of one query over n rows ---- */
 int mhnsw_distance(int metric, const float *q, const float *X, int64_t n, int dim, float *out);
 int mhnsw_distance_device(int metric, const float *d_q, const float *d_X, int64_t n, int dim, float *d_out,

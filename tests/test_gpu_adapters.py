@@ -30,16 +30,24 @@ def test_exact_index_matches_brute_force(H, O, metric):
     for i in range(1500, n):
         idx.Add(keys[i], X[i])
     assert idx.Len() == n
-    # replace-on-Add (a map assignment): 30 keys get new vectors, Len unchanged
-    newv = _clustered(rng, 30, d)
-    idx.BatchAdd(keys[100:130], newv)
-    assert idx.Len() == n
-    X2 = X.copy()
-    X2[100:130] = newv
-    order = [i for i in range(n) if not 100 <= i < 130] + list(range(100, 130))  # replaced rows re-inserted last
+    # replace-on-Add (a map assignment): 30 keys get new vectors in place, plus
+    # 2 new keys in the same batch; Len grows by 2, the store by 2 rows only
+    rows0 = idx._g.export()["keys"].shape[0]
+    newv = _clustered(rng, 32, d)
+    idx.BatchAdd(keys[100:130] + [1, 4], newv)
+    assert idx.Len() == n + 2
+    assert idx._g.export()["keys"].shape[0] == rows0 + 2
+    X2 = np.concatenate([X, newv[30:]])
+    X2[100:130] = newv[:30]
+    keys2 = keys + [1, 4]
+    order = list(range(n + 2))  # replaced rows keep their place (ties: insertion order)
     assert idx.BatchDelete([keys[5], keys[5], -7]) == [True, False, False]
     order.remove(5)
-    rk, rd, rn = _oracle_exact(O, metric, [keys[i] for i in order], X2[order], Q, k)
+    # a batch that fails validation changes nothing
+    with pytest.raises(H.HnswError, match="dimension mismatch"):
+        idx.BatchAdd([keys[7], 99999], [np.ones(d, np.float32), np.ones(d + 1, np.float32)])
+    assert idx.Len() == n + 1
+    rk, rd, rn = _oracle_exact(O, metric, [keys2[i] for i in order], X2[order], Q, k)
     ks, od, on = idx.search_batch(Q, k)
     assert np.array_equal(on, rn)
     for b in range(len(Q)):
@@ -47,7 +55,7 @@ def test_exact_index_matches_brute_force(H, O, metric):
         assert _bit_equal(od[b, : on[b]], rd[b, : rn[b]]), b
     nodes = idx.Search(Q[3], k)
     assert [nd.Key for nd in nodes] == rk[3, : rn[3]].tolist()
-    i0 = keys.index(nodes[0].Key)
+    i0 = keys2.index(nodes[0].Key)
     assert np.array_equal(nodes[0].Value, X2[i0])
     with pytest.raises(H.HnswError) as e:
         idx.BatchAdd([1, 2], [X[0]])
@@ -75,6 +83,8 @@ def test_adapters(H, O):
             # the reference recomputes a.distance(query, node.Value) (adapter.go:62-64): same canonical value
             assert ok and np.float32(dist) == H.CosineDistance(q, v)
     assert a.Delete("k3") and a.BatchDelete(["k4", "nope"]) == [True, False] and a.Len() == n - 2
+    with pytest.raises(H.HnswError, match="flat"):  # in-place replacement is for vector stores only
+        g.Replace([H.Node("k5", X[0])])
     e = H.ExactAdapter(H.ExactIndex(H.CosineDistance))
     assert e.Search(Q[0], 3) == ([], [])
     assert e.BatchAdd(list(range(n)), X) == [None] * n

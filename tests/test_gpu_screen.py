@@ -115,24 +115,29 @@ def test_screen_follows_metric_change(H, O):
     g.close()
 
 
-@pytest.mark.parametrize("metric", [0, 1])
-def test_screened_batch_build_identical(H, metric):
-    """The batched insert's searches screen too, and its greedy descents run
-    in one launch per batch (fuse_descent): every combination builds the same
-    graph as the plain per-layer, unscreened insert."""
+@pytest.mark.parametrize("metric,alpha", [(0, 100), (1, 100), (0, 115), (1, 130)])
+def test_screened_batch_build_identical(H, metric, alpha):
+    """The batched insert's searches and its neighbour selection (the diversity
+    rule with slack alpha, screened two-sided) screen too, and its greedy
+    descents run in one launch per batch (fuse_descent): every combination
+    builds the same graph as the plain per-layer, unscreened insert."""
     from tests.test_gpu_parity import _same_graph
 
     rng = np.random.default_rng(21 + metric)
     n, d = 12000, 96
     X, _ = _adversarial(rng, n, d, metric)
-    ex = {}
+    ex, f32 = {}, {}
     for screen, fuse in ((0, 0), (1, 0), (0, 1), (1, 1)):
         g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
-                    ef_construction=80, heuristic=2, keep_pruned=1, screen=screen, fuse_descent=fuse)
+                    ef_construction=80, heuristic=2, keep_pruned=1, screen=screen, fuse_descent=fuse,
+                    prune_alpha_pct=alpha)
         g.add_arrays(np.arange(n // 3), X[: n // 3])   # two calls: later batches descend a multi-layer graph
         g.add_arrays(np.arange(n // 3, n), X[n // 3:])
-        assert g.stats()["dropped_proposals"] == 0
+        st = g.stats()
+        assert st["dropped_proposals"] == 0
+        f32[(screen, fuse)] = st["build_f32_rows"]
         ex[(screen, fuse)] = g.export()
         g.close()
     for key in ((1, 0), (0, 1), (1, 1)):
         _same_graph(ex[(0, 0)], ex[key])
+    assert f32[(1, 0)] < 0.6 * f32[(0, 0)]  # the selection's rows were mostly decided on the copy

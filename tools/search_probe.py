@@ -1,6 +1,7 @@
 """Headline-search knob probe on the bench graph (1M x 768 cosine, bench.py
 defaults): QPS / recall / distance evals / visited resets per setting.
-Usage: python tools/search_probe.py [name=value ...]  (default: the knob list below)"""
+Usage: python tools/search_probe.py [name=value ...]  (default: the knob list below)
+Env: PROBE_BATCH (16384), PROBE_LATENT (12: the bench data), PROBE_EFS ("56,64")."""
 import os
 import sys
 import time
@@ -14,8 +15,10 @@ from bench import Searcher, gen_vectors, recall_at_k  # noqa: E402
 
 dev = torch.device("cuda")
 n, d, B = 1_000_000, 768, int(os.environ.get("PROBE_BATCH", 16384))
-X = gen_vectors(n, d, 1234, 12, 1000, dev, "cosine")
-Q = gen_vectors(B, d, 1234 + 7777, 12, 1000, dev, "cosine")
+lat = int(os.environ.get("PROBE_LATENT", 12))
+efs = [int(x) for x in os.environ.get("PROBE_EFS", "56,64").split(",")]
+X = gen_vectors(n, d, 1234, lat, 1000, dev, "cosine")
+Q = gen_vectors(B, d, 1234 + 7777, lat, 1000, dev, "cosine")
 g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=1234, build_mode=H.BUILD_BATCH, m0=40,
             ef_construction=400, heuristic=2, keep_pruned=1, prune_alpha_pct=115)
 g.reserve(n, d)
@@ -30,7 +33,7 @@ if sys.argv[1:]:
 for name, val in knobs:
     g.set_option(name, val)
     vl = f"{name}={val}"
-    for ef in (56, 64):
+    for ef in efs:
         S.run(Q, H.MODE_BEAM, ef)
         g.reset_stats()
         torch.cuda.synchronize()
