@@ -160,3 +160,51 @@ def test_sharded_engine_gloo_world2(H, O):
         _same_results(r0[0], r0[1], r0[2], rk, rd, rn)
         if name == "exact":  # = the single-index exact top-k
             _same_results(r0[0], r0[1], r0[2], fk, fd, fn)
+
+
+def test_config3_layout_tenth_scale(H):
+    """BASELINE configs[3]'s layout (8 node-ID range shards of 768-d cosine,
+    every query on every shard, per-shard top-k merged) at 1/10 of its 10M rows,
+    on one GPU: 8 x 125k rows built by the batched insert with the bench's graph
+    recipe.  Sharded exact == the exact top-k of one flat index over all rows;
+    sharded beam (ef 64) recall@10 >= 0.99 against it."""
+    torch = pytest.importorskip("torch")
+    from bench import gen_vectors
+    from hnsw_amd.shard import engine_local_search, merge_topk, shard_range
+
+    S, n, d, B, k = 8, 1_000_000, 768, 4096, 10
+    dev = torch.device("cuda:0")
+    X = gen_vectors(n, d, 1234, 12, 1000, dev, "cosine")
+    Q = gen_vectors(B, d, 9011, 12, 1000, dev, "cosine")
+    keys = np.arange(n, dtype=np.int64)
+    torch.cuda.synchronize()  # the handles read X on their own streams
+    shards = []
+    for s in range(S):
+        lo, hi = shard_range(n, S, s)
+        g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=1234 + s, build_mode=H.BUILD_BATCH,
+                    m0=40, ef_construction=400, heuristic=2, keep_pruned=1, prune_alpha_pct=115)
+        g.reserve(hi - lo, d)
+        g.add_device(keys[lo:hi], X[lo:hi].contiguous().data_ptr(), hi - lo, d)
+        shards.append(g)
+    full = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, build_mode=H.BUILD_FLAT)
+    full.reserve(n, d)
+    full.add_device(keys, X.data_ptr(), n, d)
+    del X
+    fk, fd, fn = engine_local_search(full, k, H.MODE_EXACT, 0)(Q)
+    full.device_status()
+    fk, fd, fn = fk.cpu().numpy(), fd.cpu().numpy(), fn.cpu().numpy()
+    full.close()
+    res = {}
+    for name, mode, ef in (("exact", H.MODE_EXACT, 0), ("beam", H.MODE_BEAM, 64)):
+        lists = [engine_local_search(g, k, mode, ef)(Q) for g in shards]
+        for g in shards:
+            g.device_status()
+        mk, md, mn = merge_topk(torch.stack([x[0] for x in lists]), torch.stack([x[1] for x in lists]),
+                                torch.stack([x[2] for x in lists]), k)
+        res[name] = (mk.cpu().numpy(), md.cpu().numpy(), mn.cpu().numpy())
+    _same_results(*res["exact"], fk, fd, fn)
+    mk, _, mn = res["beam"]
+    rec = np.mean([len(set(mk[b, : mn[b]]) & set(fk[b, : fn[b]])) / k for b in range(B)])
+    assert rec >= 0.99, rec
+    for g in shards:
+        g.close()

@@ -21,6 +21,7 @@ X = gen_vectors(n, d, 55, 12, 1000, dev, "cosine")
 Q = gen_vectors(B, d, 56, 12, 1000, dev, "cosine")
 g = H.Graph(M=4, Ml=0.25, EfSearch=8, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_FLAT)
 g.reserve(n, d)
+torch.cuda.synchronize()
 g.add_device(np.arange(n), X.data_ptr(), n, d)
 del X
 g.set_option("exact_precision", prec)
