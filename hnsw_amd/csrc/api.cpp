@@ -66,6 +66,7 @@ struct mhnsw_index {
     int alpha_pct = 100;
     int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
     int vis_log2 = 12;
+    int vis_entries = 0;      // beam search's visited set; 0 = 1.25 * 2^vis_log2 (beam_vis_entries)
     int exact_kk = 0;
     int exact_precision = 3;  // scores: 0 f32-input MFMA, 1 bf16x3 split, 2 fp16 2-product split,
                               // 3 fp16 1-product with the fused preselection (all certified, same results)
@@ -728,6 +729,14 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
 
 // Mutations (Add / Delete / Reserve / Import) first let every enqueued
 // search finish: they rewrite or reallocate what those kernels read.
+// The beam search kernel is held to 2 waves per SIMD by its VGPRs (8 per CU),
+// which leaves 20 KiB of the CU's 160 KiB LDS per wave: its visited set takes
+// 1.25 * 2^vis_log2 entries (5,120 at the default), fewer resets at large ef.
+int beam_vis_entries(const mhnsw_index* h) {
+    if (h->vis_entries > 0) return h->vis_entries;
+    return std::min(32768, 5 << (h->vis_log2 - 2));
+}
+
 int drain(mhnsw_index* h) {
     if (h->scr_valid) HIPCHK(h, hipEventSynchronize(h->scr_ev));
     h->scr_valid = false;
@@ -1052,6 +1061,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         a.stats = h->d_stats;
         a.err = errw;
         a.vis_log2 = h->vis_log2;
+        a.vis_n = beam_vis_entries(h);
         a.upper_ef = h->upper_ef;
         if (mode == MHNSW_MODE_BEAM) {
             if (std::max(ef, k) > 512) return fail(h, MHNSW_EUNSUPPORTED, "beam mode supports max(ef,k) <= 512");
@@ -1264,6 +1274,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
         h->batch_max = (int)std::max<int64_t>(1, v);
     } else if (n == "batch_ratio_pct") {
         h->batch_ratio_pct = (int)std::max<int64_t>(0, v);
+    } else if (n == "vis_entries") {
+        if (v != 0 && (v < 64 || v > 32768)) return fail(h, MHNSW_EINVAL, "vis_entries must be 0 or in [64, 32768]");
+        h->vis_entries = (int)v;
     } else if (n == "vis_log2") {
         if (v < 6 || v > 15) return fail(h, MHNSW_EINVAL, "vis_log2 must be in [6, 15]");
         h->vis_log2 = (int)v;
@@ -1327,6 +1340,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "batch_max") *v = h->batch_max;
     else if (n == "batch_ratio_pct") *v = h->batch_ratio_pct;
     else if (n == "vis_log2") *v = h->vis_log2;
+    else if (n == "vis_entries") *v = beam_vis_entries(h);
     else if (n == "exact_kk") *v = h->exact_kk;
     else if (n == "exact_precision") *v = h->exact_precision;
     else if (n == "exact_tile") *v = h->exact_tile;

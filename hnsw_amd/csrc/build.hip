@@ -580,7 +580,7 @@ __global__ __launch_bounds__(64) void k_batch_descend(BatchBuildArgs a) {
     uint32_t ep = a.cur_entry[u];
     for (int l = a.layer; l > lv; --l) {
         BList<1> L1;
-        beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, 1, q, qn, L1, smem, a.vis_log2, st);
+        beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, 1, q, qn, L1, smem, 1 << a.vis_log2, st);
         float d;
         uint32_t id;
         bl_at(L1, 0, d, id);
@@ -616,14 +616,14 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
     const uint32_t ep = a.cur_entry[u];
     if (a.levels[u] < l) {  // above the node's level: greedy descent only
         BList<1> L1;
-        beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, 1, q, qn, L1, smem, a.vis_log2, st);
+        beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, 1, q, qn, L1, smem, 1 << a.vis_log2, st);
         float d;
         uint32_t id;
         bl_at(L1, 0, d, id);
         if (lane == 0 && id != EMPTY_ID) a.cur_entry[u] = id & ID_MASK;
     } else {
         BList<R> L;
-        beam_layer<C, R, G, false, SCREEN>(a.g, l, ep, a.ef, q, qn, L, smem, a.vis_log2, st);
+        beam_layer<C, R, G, false, SCREEN>(a.g, l, ep, a.ef, q, qn, L, smem, 1 << a.vis_log2, st);
         float d0;
         uint32_t i0;
         bl_at(L, 0, d0, i0);

@@ -400,6 +400,20 @@ __device__ __forceinline__ int vis_probe(uint32_t* tab, int mask, uint32_t id) {
     return 2;
 }
 
+// The same set over any size (the beam search sizes it to the LDS its
+// occupancy leaves): multiply-high range reduction, linear probing with wrap.
+__device__ __forceinline__ int vis_probe_n(uint32_t* tab, uint32_t size, uint32_t id) {
+    uint32_t h = __umulhi((id * 0x9E3779B1u) ^ (id >> 15), size);
+#pragma unroll 1
+    for (int p = 0; p < 48; ++p) {
+        uint32_t old = atomicCAS(&tab[h], VIS_EMPTY, id);
+        if (old == VIS_EMPTY) return 1;
+        if (old == id) return 0;
+        h = h + 1 == size ? 0u : h + 1;
+    }
+    return 2;
+}
+
 // ---------------------------------------------------------------------------
 // sorted list across lanes: entry index i = r*64 + lane, ordered by (d, id)
 // ---------------------------------------------------------------------------

@@ -238,14 +238,13 @@ struct WaveEval {
 // ---------------------------------------------------------------------------
 template <class C, int R, int G, bool COH = false, bool SCREEN = false>
 __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_t entry, int ef, const QReg<C>& q, float qn,
-                           BList<R>& L, uint32_t* vis, int vlog2, WaveStats& st) {
+                           BList<R>& L, uint32_t* vis, int vsize, WaveStats& st) {
     const int lane = lane_id();
-    const int vsize = 1 << vlog2, vmask = vsize - 1;
     bl_init(L);
     if (entry == EMPTY_ID) return;
     vis_clear(vis, vsize);
     __syncthreads();
-    if (lane == 0) vis_probe(vis, vmask, entry);
+    if (lane == 0) vis_probe_n(vis, (uint32_t)vsize, entry);
     int vcount = 1;
     eval_list<C, G>(g, q, qn, entry, 1, g.metric, [&](float d, uint32_t u) { bl_insert(L, ef, d, u); });
     st.E += 1;
@@ -275,7 +274,7 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
         int pr = 0;
         if (have && nb != 0xFFFFFFFFu) {
             nb = guard_id(g, nb);
-            pr = vis_probe(vis, vmask, nb);
+            pr = vis_probe_n(vis, (uint32_t)vsize, nb);
         }
         vcount += __popcll(__ballot(pr == 1));
         int cnt;
@@ -304,7 +303,7 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const uint32_t id = L.i[r];
-                const bool ins = id != EMPTY_ID && vis_probe(vis, vmask, id & ID_MASK) == 1;
+                const bool ins = id != EMPTY_ID && vis_probe_n(vis, (uint32_t)vsize, id & ID_MASK) == 1;
                 seeded += __popcll(__ballot(ins));
             }
             __syncthreads();

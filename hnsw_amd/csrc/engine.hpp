@@ -42,7 +42,8 @@ struct SearchArgs {
     unsigned long long* stats;    // [0]=dist evals [1]=expansions [2]=visited resets
                                   // [8]=rows screened in fp16 [9]=rows evaluated in f32 (beam)
     int* err;                     // set to nonzero on visited overflow (compat)
-    int vis_log2;
+    int vis_log2;                 // compat: 2^vis_log2-entry visited set
+    int vis_n;                    // beam: visited-set entries
     int upper_ef;                 // beam: width of the upper-layer descent (1 = greedy, the reference's k = 1)
 };
 

@@ -377,7 +377,7 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
                 if (e < 0) continue;
                 ep = (uint32_t)e;
             }
-            beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, a.upper_ef, q, qn, L1, smem, a.vis_log2, st);
+            beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, a.upper_ef, q, qn, L1, smem, a.vis_n, st);
             float d;
             uint32_t id;
             bl_at(L1, 0, d, id);
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
     BList<R> L;
     const int efl = a.ef > a.k ? a.ef : a.k;
     if (a.g.layers[0].deg[ep] == -2) ep = (uint32_t)a.layer_entry[0];
-    beam_layer<C, R, G, false, SCREEN>(a.g, 0, ep, efl, q, qn, L, smem, a.vis_log2, st);
+    beam_layer<C, R, G, false, SCREEN>(a.g, 0, ep, efl, q, qn, L, smem, a.vis_n, st);
     // compact the sorted list into the first k live entries (deleted rows
     // route the search but are never returned)
     int nvalid = 0;
@@ -553,7 +553,7 @@ __global__ __launch_bounds__(64) void k_negatives(NegArgs a) {
 
 template <class C, int R, int G>
 static int launch_beam_t(const SearchArgs& a, hipStream_t s) {
-    const size_t lds = (size_t)4 << a.vis_log2;
+    const size_t lds = (size_t)4 * (size_t)a.vis_n;
     if (a.g.h16)
         hipLaunchKernelGGL((k_search_beam<C, R, G, true>), dim3((unsigned)a.B), dim3(64), lds, s, a);
     else
