@@ -1,0 +1,125 @@
+// beam.hpp -- the batched beam search kernel (k_search_beam) and the
+// dimension-configuration list, shared by search.hip (dispatch) and the
+// beam_*.hip translation units that instantiate it per configuration (split
+// so that the kernel's 4 list widths x 2 screen modes x 10 configurations
+// compile in parallel).
+#pragma once
+#include "device_search.hpp"
+#include "engine.hpp"
+
+namespace mh {
+
+// group width per configuration (rows in flight per wave step)
+#define MH_FOR_EACH_CFG(X)      \
+    X(16, 1, 2)                 \
+    X(32, 1, 4)                 \
+    X(64, 1, 8)                 \
+    X(64, 2, 8)                 \
+    X(64, 3, 8)                 \
+    X(64, 4, 4)                 \
+    X(64, 6, 4)                 \
+    X(64, 8, 2)            \
+    X(64, 12, 1)           \
+    X(64, 16, 1)
+
+template <int L, int V>
+int launch_beam_cfg(const SearchArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// batched search: one wave per query
+// ---------------------------------------------------------------------------
+template <class C, int R, int G, bool SCREEN>
+__global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int64_t b = blockIdx.x;
+    if (b >= a.B) return;
+    const int lane = lane_id();
+    QReg<C> q;
+    load_query(q, a.q + (size_t)b * C::PITCH);
+    const float qn = query_norm(q);
+    WaveStats st;
+    uint32_t ep = a.entry;
+    {
+        BList<1> L1;
+        for (int l = a.top; l >= 1; --l) {  // greedy descent, ef = 1
+            if (a.g.layers[l].deg[ep] == -2) {  // not in this layer: restart at its entry
+                const int32_t e = a.layer_entry[l];
+                if (e < 0) continue;
+                ep = (uint32_t)e;
+            }
+            beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, a.upper_ef, q, qn, L1, smem, a.vis_n, st);
+            float d;
+            uint32_t id;
+            bl_at(L1, 0, d, id);
+            if (id != EMPTY_ID) ep = id & ID_MASK;
+        }
+    }
+    BList<R> L;
+    const int efl = a.ef > a.k ? a.ef : a.k;
+    if (a.g.layers[0].deg[ep] == -2) ep = (uint32_t)a.layer_entry[0];
+    beam_layer<C, R, G, false, SCREEN>(a.g, 0, ep, efl, q, qn, L, smem, a.vis_n, st);
+    // compact the sorted list into the first k live entries (deleted rows
+    // route the search but are never returned)
+    int nvalid = 0;
+    const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t id = L.i[r] & ID_MASK;
+        const bool ok = L.i[r] != EMPTY_ID && !is_dead(a.g, id);
+        const unsigned long long m = __ballot(ok);
+        const int pos = nvalid + __popcll(m & below);
+        if (ok && pos < a.k) {
+            a.out_keys[b * a.k + pos] = a.g.keys[id];
+            a.out_dist[b * a.k + pos] = L.d[r];
+            if (a.out_ids) a.out_ids[b * a.k + pos] = (int32_t)id;
+        }
+        nvalid += __popcll(m);
+    }
+    nvalid = min(nvalid, a.k);
+    for (int i = nvalid + lane; i < a.k; i += 64) {
+        a.out_keys[b * a.k + i] = (int64_t)-1;
+        a.out_dist[b * a.k + i] = __int_as_float(0x7f800000);
+        if (a.out_ids) a.out_ids[b * a.k + i] = -1;
+    }
+    if (lane == 0) {
+        a.out_n[b] = nvalid;
+        atomicAdd(&a.stats[0], st.E);
+        atomicAdd(&a.stats[1], st.X);
+        if (st.resets) atomicAdd(&a.stats[2], st.resets);
+        atomicAdd(&a.stats[8], st.S);
+        atomicAdd(&a.stats[9], st.F);
+    }
+}
+
+template <class C, int R, int G>
+static int launch_beam_t(const SearchArgs& a, hipStream_t s) {
+    const size_t lds = (size_t)4 * (size_t)a.vis_n;
+    if (a.g.h16)
+        hipLaunchKernelGGL((k_search_beam<C, R, G, true>), dim3((unsigned)a.B), dim3(64), lds, s, a);
+    else
+        hipLaunchKernelGGL((k_search_beam<C, R, G, false>), dim3((unsigned)a.B), dim3(64), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// group width G of configuration (L, V), from MH_FOR_EACH_CFG
+template <int L, int V>
+constexpr int beam_group() {
+#define X_(L_, V_, G_) \
+    if (L == L_ && V == V_) return G_;
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return 0;
+}
+
+template <int L, int V>
+int launch_beam_cfg(const SearchArgs& a, hipStream_t s) {
+    constexpr int G = beam_group<L, V>();
+    const int efl = a.ef > a.k ? a.ef : a.k;
+    if (efl <= 64) return launch_beam_t<Cfg<L, V>, 1, G>(a, s);
+    if (efl <= 128) return launch_beam_t<Cfg<L, V>, 2, G>(a, s);
+    if (efl <= 256) return launch_beam_t<Cfg<L, V>, 4, G>(a, s);
+    if (efl <= 512) return launch_beam_t<Cfg<L, V>, 8, G>(a, s);
+    return -4;
+}
+
+}  // namespace mh

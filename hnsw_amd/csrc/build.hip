@@ -1032,19 +1032,41 @@ static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-#define MH_FOR_EACH_CFG(X) \
-    X(16, 1, 2)            \
-    X(32, 1, 4)            \
-    X(64, 1, 8)            \
-    X(64, 2, 8)            \
-    X(64, 3, 8)            \
-    X(64, 4, 4)            \
-    X(64, 6, 4)            \
-    X(64, 8, 2)            \
-    X(64, 12, 1)           \
-    X(64, 16, 1)
+// build.hip is compiled once per part (MH_PART 0-3, Makefile) so that the
+// configurations' kernels compile in parallel; each part instantiates its
+// share of the configurations, and part 0 also holds the dispatchers, which
+// ask each part in turn (-3: configuration not in that part).
+#ifndef MH_PART
+#define MH_PART 0
+#endif
+#if MH_PART == 0
+#define MH_FOR_EACH_CFG(X) X(16, 1, 2) X(32, 1, 4) X(64, 1, 8)
+#elif MH_PART == 1
+#define MH_FOR_EACH_CFG(X) X(64, 2, 8) X(64, 3, 8)
+#elif MH_PART == 2
+#define MH_FOR_EACH_CFG(X) X(64, 4, 4) X(64, 6, 4)
+#else
+#define MH_FOR_EACH_CFG(X) X(64, 8, 2) X(64, 12, 1) X(64, 16, 1)
+#endif
+#define MH_CAT2(a, b) a##b
+#define MH_CAT(a, b) MH_CAT2(a, b)
+#define MH_PARTFN(f) MH_CAT(f##_part, MH_PART)
 
-int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, int waves, hipStream_t s) {
+// every part's entry points (defined below, one set per part)
+#define MH_DECL_PARTS(P)                                                                           \
+    int launch_build_compat_part##P(const CompatBuildArgs& a, int lpr, int vpl, int waves, hipStream_t s); \
+    int launch_build_batch_descend_part##P(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s); \
+    int launch_build_batch_search_part##P(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s);  \
+    int launch_build_batch_commit_part##P(const BatchBuildArgs& a, int lpr, int vpl, int64_t mt, hipStream_t s); \
+    int launch_delete_compat_part##P(const DeleteArgs& a, int lpr, int vpl, hipStream_t s);           \
+    int launch_delete_repair_part##P(const DeleteArgs& a, int lpr, int vpl, hipStream_t s);
+MH_DECL_PARTS(0)
+MH_DECL_PARTS(1)
+MH_DECL_PARTS(2)
+MH_DECL_PARTS(3)
+#undef MH_DECL_PARTS
+
+int MH_PARTFN(launch_build_compat)(const CompatBuildArgs& a, int lpr, int vpl, int waves, hipStream_t s) {
     // the sequential build keeps three query rows live (search / addNeighbor /
     // replenish): two rows in flight per group keeps it spill-free
 #define X_(L, V, G) \
@@ -1054,7 +1076,7 @@ int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, int waves, h
     return -3;
 }
 
-int launch_build_batch_descend(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s) {
+int MH_PARTFN(launch_build_batch_descend)(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s) {
 #define X_(L, V, G) \
     if (lpr == L && vpl == V) return launch_batch_descend_t<Cfg<L, V>, G>(a, s);
     MH_FOR_EACH_CFG(X_)
@@ -1062,7 +1084,7 @@ int launch_build_batch_descend(const BatchBuildArgs& a, int lpr, int vpl, hipStr
     return -3;
 }
 
-int launch_build_batch_search(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s) {
+int MH_PARTFN(launch_build_batch_search)(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s) {
 #define X_(L, V, G)                                                          \
     if (lpr == L && vpl == V) {                                              \
         if (a.ef <= 64) return launch_batch_search_t<Cfg<L, V>, 1, G>(a, s); \
@@ -1076,7 +1098,7 @@ int launch_build_batch_search(const BatchBuildArgs& a, int lpr, int vpl, hipStre
     return -3;
 }
 
-int launch_build_batch_commit(const BatchBuildArgs& a, int lpr, int vpl, int64_t max_touched, hipStream_t s) {
+int MH_PARTFN(launch_build_batch_commit)(const BatchBuildArgs& a, int lpr, int vpl, int64_t max_touched, hipStream_t s) {
     if (max_touched <= 0) return 0;
 #define X_(L, V, G)                                                                                   \
     if (lpr == L && vpl == V) {                                                                       \
@@ -1089,7 +1111,7 @@ int launch_build_batch_commit(const BatchBuildArgs& a, int lpr, int vpl, int64_t
     return -3;
 }
 
-int launch_delete_compat(const DeleteArgs& a, int lpr, int vpl, hipStream_t s) {
+int MH_PARTFN(launch_delete_compat)(const DeleteArgs& a, int lpr, int vpl, hipStream_t s) {
     if (a.nids <= 0) return 0;
 #define X_(L, V, G) \
     if (lpr == L && vpl == V) return launch_delete_compat_t<Cfg<L, V>, (G < 2 ? G : 2)>(a, s);
@@ -1098,7 +1120,7 @@ int launch_delete_compat(const DeleteArgs& a, int lpr, int vpl, hipStream_t s) {
     return -3;
 }
 
-int launch_delete_repair(const DeleteArgs& a, int lpr, int vpl, hipStream_t s) {
+int MH_PARTFN(launch_delete_repair)(const DeleteArgs& a, int lpr, int vpl, hipStream_t s) {
     if (a.n <= 0) return 0;
 #define X_(L, V, G)                                                                                      \
     if (lpr == L && vpl == V) {                                                                          \
@@ -1110,5 +1132,47 @@ int launch_delete_repair(const DeleteArgs& a, int lpr, int vpl, hipStream_t s) {
 #undef X_
     return -3;
 }
+
+#if MH_PART == 0
+#define MH_ASK_PARTS(call)                       \
+    {                                            \
+        int r_;                                  \
+        if ((r_ = call(0)) != -3) return r_;     \
+        if ((r_ = call(1)) != -3) return r_;     \
+        if ((r_ = call(2)) != -3) return r_;     \
+        return call(3);                          \
+    }
+int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, int waves, hipStream_t s) {
+#define C_(P) launch_build_compat_part##P(a, lpr, vpl, waves, s)
+    MH_ASK_PARTS(C_)
+#undef C_
+}
+int launch_build_batch_descend(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s) {
+#define C_(P) launch_build_batch_descend_part##P(a, lpr, vpl, s)
+    MH_ASK_PARTS(C_)
+#undef C_
+}
+int launch_build_batch_search(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s) {
+#define C_(P) launch_build_batch_search_part##P(a, lpr, vpl, s)
+    MH_ASK_PARTS(C_)
+#undef C_
+}
+int launch_build_batch_commit(const BatchBuildArgs& a, int lpr, int vpl, int64_t max_touched, hipStream_t s) {
+#define C_(P) launch_build_batch_commit_part##P(a, lpr, vpl, max_touched, s)
+    MH_ASK_PARTS(C_)
+#undef C_
+}
+int launch_delete_compat(const DeleteArgs& a, int lpr, int vpl, hipStream_t s) {
+#define C_(P) launch_delete_compat_part##P(a, lpr, vpl, s)
+    MH_ASK_PARTS(C_)
+#undef C_
+}
+int launch_delete_repair(const DeleteArgs& a, int lpr, int vpl, hipStream_t s) {
+#define C_(P) launch_delete_repair_part##P(a, lpr, vpl, s)
+    MH_ASK_PARTS(C_)
+#undef C_
+}
+#undef MH_ASK_PARTS
+#endif
 
 }  // namespace mh

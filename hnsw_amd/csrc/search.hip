@@ -5,8 +5,18 @@
 // query lives in VGPRs, the visited set in LDS, the candidate list in VGPRs
 // across lanes; candidate rows are gathered from HBM with 1-KiB coalesced
 // wave loads.
-#include "device_search.hpp"
-#include "engine.hpp"
+#include "beam.hpp"
+#include "walks.hpp"
+
+namespace mh {
+// instantiated in beam_*.hip / walks_*.hip
+#define X_(L, V, G)                                                                    \
+    extern template int launch_beam_cfg<L, V>(const SearchArgs&, hipStream_t);       \
+    extern template int launch_compat_cfg<L, V>(const SearchArgs&, hipStream_t);     \
+    extern template int launch_negatives_cfg<L, V>(const NegArgs&, hipStream_t);
+MH_FOR_EACH_CFG(X_)
+#undef X_
+}  // namespace mh
 
 namespace mh {
 
@@ -354,234 +364,6 @@ int launch_h16_rows(const float* X, const float* norms, int64_t n0, int64_t n1, 
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// ---------------------------------------------------------------------------
-// ---------------------------------------------------------------------------
-// batched search: one wave per query
-// ---------------------------------------------------------------------------
-template <class C, int R, int G, bool SCREEN>
-__global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const int64_t b = blockIdx.x;
-    if (b >= a.B) return;
-    const int lane = lane_id();
-    QReg<C> q;
-    load_query(q, a.q + (size_t)b * C::PITCH);
-    const float qn = query_norm(q);
-    WaveStats st;
-    uint32_t ep = a.entry;
-    {
-        BList<1> L1;
-        for (int l = a.top; l >= 1; --l) {  // greedy descent, ef = 1
-            if (a.g.layers[l].deg[ep] == -2) {  // not in this layer: restart at its entry
-                const int32_t e = a.layer_entry[l];
-                if (e < 0) continue;
-                ep = (uint32_t)e;
-            }
-            beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, a.upper_ef, q, qn, L1, smem, a.vis_n, st);
-            float d;
-            uint32_t id;
-            bl_at(L1, 0, d, id);
-            if (id != EMPTY_ID) ep = id & ID_MASK;
-        }
-    }
-    BList<R> L;
-    const int efl = a.ef > a.k ? a.ef : a.k;
-    if (a.g.layers[0].deg[ep] == -2) ep = (uint32_t)a.layer_entry[0];
-    beam_layer<C, R, G, false, SCREEN>(a.g, 0, ep, efl, q, qn, L, smem, a.vis_n, st);
-    // compact the sorted list into the first k live entries (deleted rows
-    // route the search but are never returned)
-    int nvalid = 0;
-    const unsigned long long below = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const uint32_t id = L.i[r] & ID_MASK;
-        const bool ok = L.i[r] != EMPTY_ID && !is_dead(a.g, id);
-        const unsigned long long m = __ballot(ok);
-        const int pos = nvalid + __popcll(m & below);
-        if (ok && pos < a.k) {
-            a.out_keys[b * a.k + pos] = a.g.keys[id];
-            a.out_dist[b * a.k + pos] = L.d[r];
-            if (a.out_ids) a.out_ids[b * a.k + pos] = (int32_t)id;
-        }
-        nvalid += __popcll(m);
-    }
-    nvalid = min(nvalid, a.k);
-    for (int i = nvalid + lane; i < a.k; i += 64) {
-        a.out_keys[b * a.k + i] = (int64_t)-1;
-        a.out_dist[b * a.k + i] = __int_as_float(0x7f800000);
-        if (a.out_ids) a.out_ids[b * a.k + i] = -1;
-    }
-    if (lane == 0) {
-        a.out_n[b] = nvalid;
-        atomicAdd(&a.stats[0], st.E);
-        atomicAdd(&a.stats[1], st.X);
-        if (st.resets) atomicAdd(&a.stats[2], st.resets);
-        atomicAdd(&a.stats[8], st.S);
-        atomicAdd(&a.stats[9], st.F);
-    }
-}
-
-template <class C, int G>
-__global__ __launch_bounds__(64) void k_search_compat(SearchArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const int64_t b = blockIdx.x;
-    if (b >= a.B) return;
-    const int lane = lane_id();
-    const int vsize = 1 << a.vis_log2;
-    CompatSmem S;
-    S.vis = smem;
-    S.vlog2 = a.vis_log2;
-    S.cd = reinterpret_cast<float*>(smem + vsize);
-    S.ci = smem + vsize + (a.ef + 2);
-    S.rd = reinterpret_cast<float*>(smem + vsize + 2 * (a.ef + 2));
-    S.ri = smem + vsize + 2 * (a.ef + 2) + (a.k + 2);
-    QReg<C> q;
-    load_query(q, a.q + (size_t)b * C::PITCH);
-    const float qn = query_norm(q);
-    WaveStats st;
-    int err = 0;
-    uint32_t elevator = EMPTY_ID;
-    int nres = 0;
-    for (int l = a.top; l >= 0; --l) {  // graph.go:571-622
-        // searchPoint: layers[l].nodes[*elevator] (nil once deleted) or entry() (nil when empty)
-        uint32_t p;
-        if (elevator != EMPTY_ID)
-            p = is_member(a.g, l, elevator) ? elevator : EMPTY_ID;
-        else
-            p = l == a.top ? a.entry : (a.layer_entry[l] < 0 ? EMPTY_ID : (uint32_t)a.layer_entry[l]);
-        if (p == EMPTY_ID) continue;  // search(nil) returns nothing (graph.go:101-103)
-        if (l > 0) {
-            const int c = compat_layer<C, G>(a.g, l, p, 1, a.ef, q, qn, S, st, err);
-            if (c == 0) continue;
-            elevator = S.ri[0];
-            continue;
-        }
-        nres = compat_layer<C, G>(a.g, 0, p, a.k, a.ef, q, qn, S, st, err);
-    }
-    for (int i = lane; i < a.k; i += 64) {
-        const bool ok = i < nres;
-        const uint32_t id = ok ? S.ri[i] : 0u;
-        a.out_keys[b * a.k + i] = ok ? a.g.keys[id] : (int64_t)-1;
-        a.out_dist[b * a.k + i] = ok ? S.rd[i] : __int_as_float(0x7f800000);
-        if (a.out_ids) a.out_ids[b * a.k + i] = ok ? (int32_t)id : -1;
-    }
-    if (lane == 0) {
-        a.out_n[b] = nres;
-        atomicAdd(&a.stats[0], st.E);
-        atomicAdd(&a.stats[1], st.X);
-        if (err) atomicOr(a.err, 1);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// negative-example re-ranking (graph.go:1116-1537), one wave per query: the
-// Search(near, kx) candidates are scored against the query's negatives with
-// the reference's float32 formula, then ranked by descending score (ties in
-// candidate order, NaN last).  Restated in oracle/oracle.c og_search_negatives.
-// ---------------------------------------------------------------------------
-template <class C, int G>
-__global__ __launch_bounds__(64) void k_negatives(NegArgs a) {
-#pragma clang fp contract(off)
-    __shared__ float sc[NEG_MAX_CAND];
-    __shared__ int32_t sid[NEG_MAX_CAND];
-    const int64_t b = blockIdx.x;
-    if (b >= a.B) return;
-    const int lane = lane_id();
-    const int n = min(a.cand_n[b], a.kx);
-    const int j0 = a.neg_off[b], j1 = a.neg_off[b + 1];
-    const int nn = j1 - j0;
-    for (int base = 0; base < n; base += 64) {
-        const int cnt = min(64, n - base);
-        const bool mine = lane < cnt;
-        const uint32_t cid = mine ? (uint32_t)a.cand_ids[b * a.kx + base + lane] : 0u;
-        const float qd = mine ? a.cand_d[b * a.kx + base + lane] : 0.f;
-        float total = 0.f;
-        bool close = false;
-        for (int j = j0; j < j1; ++j) {
-            QReg<C> nq;
-            load_query(nq, a.neg + (size_t)j * C::PITCH);
-            const float nqn = query_norm(nq);
-            float nd = 0.f;
-            int t = 0;
-            eval_list<C, G>(a.g, nq, nqn, cid, cnt, a.g.metric, [&](float d, uint32_t) {
-                if (lane == t) nd = d;
-                ++t;
-            });
-            total = total + (1.0f - nd);
-            close = close || nd < 0.1f;
-        }
-        const float qs = 1.0f - qd;
-        const float avg = total / (float)nn;
-        float score;
-        if (qd < 0.001f) {
-            score = 2.0f;
-        } else if (close) {
-            score = qs - a.w * 2.0f;
-        } else {
-            const int64_t key = mine ? a.g.keys[cid] : 0;
-            const float boost = ((a.flags & 1) && key >= 7 && key <= 9) ? 0.2f : 0.0f;
-            score = qs - a.w * avg + boost;
-        }
-        if (mine) {
-            sc[base + lane] = score;
-            sid[base + lane] = (int32_t)cid;
-        }
-    }
-    __syncthreads();
-    for (int e = lane; e < n; e += 64) {
-        const float se = sc[e];
-        const bool en = se != se;
-        int rank = 0;
-        for (int f = 0; f < n; ++f) {
-            const float sf = sc[f];
-            const bool fn = sf != sf;
-            const bool before = (fn != en) ? en : ((!fn && sf != se) ? sf > se : f < e);
-            rank += before ? 1 : 0;
-        }
-        if (rank < a.k) {
-            a.out_keys[b * a.k + rank] = a.g.keys[sid[e]];
-            a.out_score[b * a.k + rank] = se;
-        }
-    }
-    const int m = min(n, a.k);
-    for (int i = m + lane; i < a.k; i += 64) {
-        a.out_keys[b * a.k + i] = (int64_t)-1;
-        a.out_score[b * a.k + i] = __int_as_float(0x7fc00000);
-    }
-    if (lane == 0) a.out_n[b] = m;
-}
-
-template <class C, int R, int G>
-static int launch_beam_t(const SearchArgs& a, hipStream_t s) {
-    const size_t lds = (size_t)4 * (size_t)a.vis_n;
-    if (a.g.h16)
-        hipLaunchKernelGGL((k_search_beam<C, R, G, true>), dim3((unsigned)a.B), dim3(64), lds, s, a);
-    else
-        hipLaunchKernelGGL((k_search_beam<C, R, G, false>), dim3((unsigned)a.B), dim3(64), lds, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-template <class C, int G>
-static int launch_compat_t(const SearchArgs& a, hipStream_t s) {
-    const size_t lds = ((size_t)1 << a.vis_log2) * 4 + (size_t)(a.ef + 2) * 8 + (size_t)(a.k + 2) * 8;
-    if (lds > 160 * 1024) return -2;
-    hipLaunchKernelGGL((k_search_compat<C, G>), dim3((unsigned)a.B), dim3(64), lds, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// group width per configuration (rows in flight per wave step)
-#define MH_FOR_EACH_CFG(X)      \
-    X(16, 1, 2)                 \
-    X(32, 1, 4)                 \
-    X(64, 1, 8)                 \
-    X(64, 2, 8)                 \
-    X(64, 3, 8)                 \
-    X(64, 4, 4)                 \
-    X(64, 6, 4)                 \
-    X(64, 8, 2)            \
-    X(64, 12, 1)           \
-    X(64, 16, 1)
-
 int launch_norms(const float* X, int64_t n0, int64_t n1, int pitch, int lpr, int vpl, float* out, hipStream_t s) {
 #define X_(L, V, G) \
     if (lpr == L && vpl == V) return launch_norms_t<Cfg<L, V>>(X, n0, n1, pitch, out, s);
@@ -601,15 +383,8 @@ int launch_sweep(const float* q, const float* X, int64_t n, int pitch, int lpr, 
 
 int launch_search_beam(const SearchArgs& a, int lpr, int vpl, hipStream_t s) {
     if (a.B <= 0) return 0;
-    const int efl = a.ef > a.k ? a.ef : a.k;
-#define X_(L, V, G)                                                              \
-    if (lpr == L && vpl == V) {                                                  \
-        if (efl <= 64) return launch_beam_t<Cfg<L, V>, 1, G>(a, s);              \
-        if (efl <= 128) return launch_beam_t<Cfg<L, V>, 2, G>(a, s);             \
-        if (efl <= 256) return launch_beam_t<Cfg<L, V>, 4, G>(a, s);             \
-        if (efl <= 512) return launch_beam_t<Cfg<L, V>, 8, G>(a, s);             \
-        return -4;                                                               \
-    }
+#define X_(L, V, G) \
+    if (lpr == L && vpl == V) return launch_beam_cfg<L, V>(a, s);
     MH_FOR_EACH_CFG(X_)
 #undef X_
     return -3;
@@ -618,11 +393,8 @@ int launch_search_beam(const SearchArgs& a, int lpr, int vpl, hipStream_t s) {
 int launch_negatives(const NegArgs& a, int lpr, int vpl, hipStream_t s) {
     if (a.B <= 0) return 0;
     if (a.kx > NEG_MAX_CAND) return -4;
-#define X_(L, V, G)                                                                                        \
-    if (lpr == L && vpl == V) {                                                                            \
-        hipLaunchKernelGGL((k_negatives<Cfg<L, V>, (G < 4 ? G : 4)>), dim3((unsigned)a.B), dim3(64), 0, s, a); \
-        return hipGetLastError() == hipSuccess ? 0 : -1;                                                   \
-    }
+#define X_(L, V, G) \
+    if (lpr == L && vpl == V) return launch_negatives_cfg<L, V>(a, s);
     MH_FOR_EACH_CFG(X_)
 #undef X_
     return -3;
@@ -631,7 +403,7 @@ int launch_negatives(const NegArgs& a, int lpr, int vpl, hipStream_t s) {
 int launch_search_compat(const SearchArgs& a, int lpr, int vpl, hipStream_t s) {
     if (a.B <= 0) return 0;
 #define X_(L, V, G) \
-    if (lpr == L && vpl == V) return launch_compat_t<Cfg<L, V>, G>(a, s);
+    if (lpr == L && vpl == V) return launch_compat_cfg<L, V>(a, s);
     MH_FOR_EACH_CFG(X_)
 #undef X_
     return -3;

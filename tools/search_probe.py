@@ -45,4 +45,5 @@ for name, val in knobs:
         st = g.stats()
         r = recall_at_k(k_[:4096], n_[:4096], tk, tn, 10)
         print(f"{vl} ef={ef} qps={B / dt / 1e6:.3f}M recall={r:.4f} E={st['search_dist_evals'] / 5 / B:.1f} "
+              f"S={st['search_screened'] / 5 / B:.1f} F={st['search_f32_evals'] / 5 / B:.1f} "
               f"resets/q={st['visited_resets'] / 5 / B:.3f} kernel_ms={g.last_kernel_ms():.3f}", flush=True)
