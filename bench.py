@@ -43,7 +43,7 @@ import hnsw_amd as H  # noqa: E402
 
 # revision of the search/build kernels the recorded PMC passes (profiles/*_pmc_*.json)
 # were taken on; a pass recorded on another revision is not attached as `traffic`
-KERNEL_REV = "r02-screened-selection"
+KERNEL_REV = "r02-rowmajor-selection"
 from hnsw_amd.shard import engine_local_search, shard_range, sharded_search  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)

@@ -561,6 +561,69 @@ static int launch_build_compat_t(const CompatBuildArgs& a, int waves, hipStream_
 // ---------------------------------------------------------------------------
 // batched build
 // ---------------------------------------------------------------------------
+// One kept row r (f32 row qr, norm rn) applied to every candidate still
+// standing after list position pos (entry e = k * 64 + lane of the NR
+// registers: live / dropped flags, id eid, d(u, c) ed): a candidate is dropped
+// when alpha d(c, r) < d(u, c) -- decided by a two-sided screen of the
+// candidates' fp16 rows against per-row thresholds, the undecided pairs in
+// f32 (the neighbour selection of k_batch_search and k_batch_commit).
+template <class C, int G, int NR>
+__device__ __forceinline__ void drop_pass(const GraphDev& g, const QReg<C>& qr, float rn, int pos,
+                                          const bool (&live)[NR], bool (&dropped)[NR], const uint32_t (&eid)[NR],
+                                          const float (&ed)[NR], float alpha, float margin, WaveStats& st) {
+    const int lane = lane_id();
+    const bool scr = h16_query_ok(rn);
+    st.F += 1;  // the kept row
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const bool cand = live[r] && !dropped[r] && r * 64 + lane >= pos;
+        const unsigned long long m = __ballot(cand);
+        if (!m) continue;
+        const int cnt = __popcll(m);
+        const int before =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        const int dst = cand ? before : cnt + (lane - before);
+        const uint32_t cc = push_to(eid[r], dst);
+        const float cd = __uint_as_float(push_to(__float_as_uint(ed[r]), dst));
+        st.E += cnt;
+        // with t = d(u, c) / alpha: an estimate proving d(c, r) > t (1 + 2^-20)
+        // keeps c, one proving d(c, r) < t (1 - 2^-20) drops it; the brackets
+        // absorb the roundings of t and of the rule's product, so
+        // fl(alpha d) >= d(u, c) above and < below
+        const float t = cd / alpha;
+        int cls = 0;
+        if (scr) {
+            cls = screen_pairs<C, G>(g, qr, rn, cc, cnt, g.metric, t * (1.0f - 0x1p-20f),
+                                     t * (1.0f + 0x1p-20f), margin);
+            st.S += cnt;
+        }
+        if (!(cd > 0.f)) cls = 0;  // as the candidate-major loop: no screen for d(u, c) <= 0
+        bool dr = lane < cnt && cls < 0;
+        const bool und = lane < cnt && cls == 0;
+        const unsigned long long mu = __ballot(und);
+        if (mu) {
+            const int nu = __popcll(mu);
+            const int bu =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(mu >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mu, 0));
+            const int du = und ? bu : nu + (lane - bu);
+            const uint32_t cu = push_to(cc, du);
+            const float dcu = __uint_as_float(push_to(__float_as_uint(cd), du));
+            st.F += nu;
+            bool dk = false;
+            int k = 0;
+            eval_list<C, G>(g, qr, rn, cu, nu, g.metric, [&](float dcs, uint32_t) {
+                const bool drop = alpha * dcs < rl_f(dcu, k);
+                if (lane == k) dk = drop;
+                ++k;
+            });
+            const int dks = __shfl((int)dk, du, 64);  // all lanes: a shuffle reads inactive lanes as 0
+            dr = dr || (und && dks != 0);
+        }
+        const int drs = __shfl((int)dr, dst, 64);
+        dropped[r] = dropped[r] || (cand && drs != 0);
+    }
+}
+
 // Greedy descent (ef = 1) of every new node through the layers above its own
 // level, all layers in one launch.  Every layer l is read before its commit
 // (run_batch_layers commits layer l only after this kernel), exactly what the
@@ -640,7 +703,54 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
         float seld = 0.f;
         int nsel = 0;
         const int nl = a.ef;
-        for (int i = 0; i < nl && nsel < a.mcap; ++i) {
+        // Screened: the same rule applied kept-row-major.  A candidate is kept
+        // iff no kept row before it drops it, so each kept row r can be applied
+        // at once to every later candidate still standing (one batched
+        // two-sided screen of their fp16 rows, r's f32 row the query, and the
+        // undecided pairs in f32); the next candidate standing is kept.
+        // d(c, r) == d(r, c) bitwise (commutative products, norms multiplied
+        // both ways round), so every decision is the candidate-major loop's
+        // below (the unscreened path): the same graph (test_gpu_screen.py
+        // compares with screen 0).  A candidate meets kept rows only until the
+        // first one drops it, and the kept rows, not the candidates, are read
+        // in f32: 15.4k -> 10.0k pair evaluations and 1.38k -> 0.99k f32 rows
+        // per insert on the bench index.
+        const bool rowmajor = SCREEN && sel_screen && a.heuristic;
+        if (rowmajor) {
+            bool live[R], dropped[R];
+            uint32_t eid[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                eid[r] = L.i[r] & ID_MASK;
+                live[r] = L.i[r] != EMPTY_ID && r * 64 + lane < nl && !is_dead(a.g, eid[r]);
+                dropped[r] = false;
+            }
+            int pos = 0;
+            while (nsel < a.mcap) {
+                int idx = -1;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const unsigned long long m = __ballot(live[r] && !dropped[r] && r * 64 + lane >= pos);
+                    if (idx < 0 && m) idx = r * 64 + __ffsll((long long)m) - 1;
+                }
+                if (idx < 0) break;
+                float dc;
+                uint32_t c;
+                bl_at(L, idx, dc, c);
+                c &= ID_MASK;
+                if (lane == nsel) {
+                    sel = c;
+                    seld = dc;
+                }
+                ++nsel;
+                pos = idx + 1;
+                if (nsel >= a.mcap) break;
+                QReg<C> qr;
+                load_query(qr, a.g.vecs + (size_t)c * a.g.pitch);
+                drop_pass<C, G, R>(a.g, qr, a.g.norms[c], pos, live, dropped, eid, L.d, a.alpha, margin, st);
+            }
+        }
+        for (int i = 0; !rowmajor && i < nl && nsel < a.mcap; ++i) {
             float dc;
             uint32_t c;
             bl_at(L, i, dc, c);
@@ -656,29 +766,8 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
                 auto rule = [&](float dcs, uint32_t) {
                     if (a.alpha * dcs < dc) good = false;
                 };
-                // Screened (fp16 copy): a kept row r whose distance to c is
-                // certainly above hi cannot drop c, one certainly below lo does;
-                // only the undecided rows are evaluated in f32.  hi / lo bracket
-                // dc / alpha so that fl(alpha * d) >= dc for every d > hi and
-                // < dc for every d < lo, hence the same decision.
-                if (SCREEN && sel_screen && dc > 0.f && h16_query_ok(cn)) {
-                    const float t = dc / a.alpha;
-                    const float hi = t * (1.0f + 0x1p-20f), lo = t * (1.0f - 0x1p-20f);
-                    const int cls = screen_pairs<C, G>(a.g, qc, cn, sel, nsel, a.g.metric, lo, hi, margin);
-                    st.S += nsel;
-                    st.F += 1;  // the candidate's row
-                    if (__ballot(lane < nsel && cls < 0)) {
-                        good = false;
-                    } else {
-                        int nu;
-                        const uint32_t und = compact(sel, lane < nsel && cls == 0, nu);
-                        st.F += nu;
-                        if (nu > 0) eval_list<C, G>(a.g, qc, cn, und, nu, a.g.metric, rule);
-                    }
-                } else {
-                    st.F += nsel + 1;  // the candidate's row and the kept rows, in f32
-                    eval_list<C, G>(a.g, qc, cn, sel, nsel, a.g.metric, rule);
-                }
+                st.F += nsel + 1;  // the candidate's row and the kept rows, in f32
+                eval_list<C, G>(a.g, qc, cn, sel, nsel, a.g.metric, rule);
             }
             if (good) {
                 if (lane == nsel) {
@@ -793,7 +882,47 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
         uint32_t kept = 0;   // lane j holds the j-th kept id
         float keptd = 0.f;
         WaveStats st;
-        for (int i = 0; i < tot && nkeep < keep_cap; ++i) {
+        // with the fp16 copy: kept-row-major, as k_batch_search's selection
+        // (drop_pass; the same decisions as the candidate-major loop below)
+        const bool rowmajor = a.g.h16 != nullptr && a.alpha > 0.f;
+        if (rowmajor) {
+            const float e = a.g.h16err ? *a.g.h16err : 0.00048828125f;
+            const float margin = a.g.metric == EUCLIDEAN ? h16_margin_l2(e) : h16_margin_cos(e);
+            bool live[2], dropped[2];
+            uint32_t eid[2];
+            float ed[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int e2 = lane + 64 * h;
+                live[h] = e2 < tot;
+                eid[h] = live[h] ? guard_id(a.g, ri[e2]) : 0u;
+                ed[h] = rd[e2];
+                dropped[h] = false;
+            }
+            int pos = 0;
+            while (nkeep < keep_cap) {
+                int idx = -1;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const unsigned long long m = __ballot(live[h] && !dropped[h] && h * 64 + lane >= pos);
+                    if (idx < 0 && m) idx = h * 64 + __ffsll((long long)m) - 1;
+                }
+                if (idx < 0) break;
+                const uint32_t c = ri[idx];
+                if (lane == nkeep) {
+                    kept = c;
+                    keptd = rd[idx];
+                }
+                ++nkeep;
+                pos = idx + 1;
+                if (nkeep >= keep_cap) break;
+                QReg<C> qr;
+                const uint32_t cg = guard_id(a.g, c);
+                load_query(qr, a.g.vecs + (size_t)cg * a.g.pitch);
+                drop_pass<C, G, 2>(a.g, qr, a.g.norms[cg], pos, live, dropped, eid, ed, a.alpha, margin, st);
+            }
+        }
+        for (int i = 0; !rowmajor && i < tot && nkeep < keep_cap; ++i) {
             const uint32_t c = ri[i];
             const float dcv = rd[i];
             bool good = true;

@@ -149,12 +149,13 @@ __device__ __forceinline__ int eval_screened(const GraphDev& g, const QReg<C>& q
 
 // Two-sided screen of the rows cid[0, cnt) against a stored row held as the
 // "query" q (norm qn), for the selection rule "r drops c when alpha d(c, r) <
-// d(u, c)": lane t gets +1 when row t's f32 distance is certainly > hi, -1
-// when it is certainly < lo, 0 when the fp16 estimate cannot tell (those go
-// to the canonical f32 path).  Rows outside the copy's range are always 0.
+// d(u, c)": lane t gets +1 when row t's f32 distance is certainly > hi_t, -1
+// when it is certainly < lo_t, 0 when the fp16 estimate cannot tell (those go
+// to the canonical f32 path).  lo_t / hi_t: row t's bounds, in lane t (or the
+// same in every lane).  Rows outside the copy's range are always 0.
 template <class C, int G>
 __device__ __forceinline__ int screen_pairs(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int cnt,
-                                            int metric, float lo, float hi, float margin) {
+                                            int metric, float lo_t, float hi_t, float margin) {
     constexpr int GH = (2 * G <= C::LPR) ? 2 * G : G;
     using RM = RowMap<C, GH>;
     const int lane = lane_id();
@@ -174,6 +175,7 @@ __device__ __forceinline__ int screen_pairs(const GraphDev& g, const QReg<C>& q,
             ids[gg] = valid[gg] ? guard_id(g, ids[gg]) : 0u;
         }
         const int town = base + RM::owned_row(lane);
+        const float lo = __shfl(lo_t, town & 63, 64), hi = __shfl(hi_t, town & 63, 64);
         int c = 0;
         if (metric == EUCLIDEAN) {
             float xn[GH];

@@ -25,8 +25,9 @@ else:
 # BUILD_OPTS="a=1,b=2;a=3": one build per ';'-separated option set
 sets = [dict(kv.split("=") for kv in s_.split(",") if kv) for s_ in os.environ.get("BUILD_OPTS", "").split(";")]
 for efc, opts in [(e, o) for e in ([int(a) for a in sys.argv[1:]] or [64]) for o in sets]:
-    g = H.Graph(M=16, Ml=0.25, EfSearch=64, build_mode=H.BUILD_BATCH, ef_construction=efc, heuristic=2,
-                **base, **{k: int(v) for k, v in opts.items()})
+    kw = dict(base, heuristic=2)
+    kw.update({k: int(v) for k, v in opts.items()})
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, build_mode=H.BUILD_BATCH, ef_construction=efc, **kw)
     g.reserve(n, 768)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
