@@ -68,6 +68,8 @@ def parse():
     p.add_argument("--efc", type=int, default=400)
     p.add_argument("--keep-pruned", type=int, default=1)
     p.add_argument("--alpha", type=int, default=115, help="heuristic slack x100 (prune_alpha_pct; 100 = HNSW Alg. 4)")
+    p.add_argument("--build-expand", type=int, default=2, choices=[1, 2],
+                   help="entries expanded per step of the batched insert's layer searches")
     p.add_argument("--screen", type=int, default=1,
                    help="1: fp16 screening copy, 0: plain f32 evaluation of every candidate; same results")
     p.add_argument("--ef-sweep", default="32,48,64,72,80,96,128,256",
@@ -183,6 +185,7 @@ def main():
         X = gen_vectors(a.nbase, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=off)
         g = H.Graph(M=a.M, Ml=0.25, EfSearch=a.ef, Distance=metric, Rng=rng_seed, build_mode=H.BUILD_BATCH,
                     m0=a.M0, ef_construction=a.efc, heuristic=2, keep_pruned=a.keep_pruned, prune_alpha_pct=a.alpha,
+                    build_expand=a.build_expand,
                     screen=a.screen, time_build=1)
         g.reserve(a.nbase, a.dim)
         keys = np.arange(off, off + a.nbase, dtype=np.int64)

@@ -63,6 +63,7 @@ struct mhnsw_index {
     int efc = 0; // 0 => EfSearch
     int heuristic = 1;
     int keep_pruned = 0;
+    int build_expand = 2;     // batched insert: entries expanded per step of its layer searches (1 or 2)
     int alpha_pct = 100;
     int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
     int vis_log2 = 12;
@@ -522,6 +523,7 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         a.mcap = mcap;
         a.heuristic = h->heuristic;
         a.keep_pruned = h->keep_pruned;
+        a.expand = h->build_expand;
         a.alpha = (float)h->alpha_pct / 100.0f;
         a.inc_cnt = h->inc_cnt;
         a.inc_src = h->inc_src;
@@ -1265,6 +1267,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
         h->heuristic = (int)v;
     } else if (n == "keep_pruned") {
         h->keep_pruned = (int)(v != 0);
+    } else if (n == "build_expand") {
+        if (v != 1 && v != 2) return fail(h, MHNSW_EINVAL, "build_expand must be 1 or 2");
+        h->build_expand = (int)v;
     } else if (n == "prune_alpha_pct") {
         if (v < 50 || v > 400) return fail(h, MHNSW_EINVAL, "prune_alpha_pct must be in [50, 400]");
         h->alpha_pct = (int)v;
@@ -1335,6 +1340,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "ef_construction") *v = h->efc > 0 ? h->efc : h->ef;
     else if (n == "heuristic") *v = h->heuristic;
     else if (n == "keep_pruned") *v = h->keep_pruned;
+    else if (n == "build_expand") *v = h->build_expand;
     else if (n == "prune_alpha_pct") *v = h->alpha_pct;
     else if (n == "batch_min") *v = h->batch_min;
     else if (n == "batch_max") *v = h->batch_max;

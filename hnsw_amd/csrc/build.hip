@@ -686,7 +686,10 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
         if (lane == 0 && id != EMPTY_ID) a.cur_entry[u] = id & ID_MASK;
     } else {
         BList<R> L;
-        beam_layer<C, R, G, false, SCREEN>(a.g, l, ep, a.ef, q, qn, L, smem, 1 << a.vis_log2, st);
+        if (a.expand == 2)
+            beam_layer<C, R, G, false, SCREEN, 2>(a.g, l, ep, a.ef, q, qn, L, smem, 1 << a.vis_log2, st);
+        else
+            beam_layer<C, R, G, false, SCREEN, 1>(a.g, l, ep, a.ef, q, qn, L, smem, 1 << a.vis_log2, st);
         float d0;
         uint32_t i0;
         bl_at(L, 0, d0, i0);

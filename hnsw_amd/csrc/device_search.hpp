@@ -238,7 +238,13 @@ struct WaveEval {
 // ---------------------------------------------------------------------------
 // beam: sorted list of <= ef entries; stop when every entry is expanded
 // ---------------------------------------------------------------------------
-template <class C, int R, int G, bool COH = false, bool SCREEN = false>
+// XW: entries expanded per step.  1 is the standard best-first search (the
+// oracle's beam_layer_search; every search kernel).  2 (the batched insert's
+// layer search, option "build_expand"): the two best unexpanded entries are
+// expanded together -- their adjacency rows fetched in one round trip and
+// their new neighbours evaluated as one batch -- which halves the dependent
+// round trips of a search whose expansions yield few new candidates.
+template <class C, int R, int G, bool COH = false, bool SCREEN = false, int XW = 1>
 __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_t entry, int ef, const QReg<C>& q, float qn,
                            BList<R>& L, uint32_t* vis, int vsize, WaveStats& st) {
     const int lane = lane_id();
@@ -261,39 +267,68 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
     const int32_t* adjp = g.layers[layer].adj;
     const int capl = g.layers[layer].cap;
     for (;;) {
-        const uint32_t cur = bl_next(L);
-        if (cur == EMPTY_ID) break;
-        st.X += 1;
-        // the adjacency row is loaded together with its degree (rows are cap
-        // wide, so lanes past the degree read allocated, ignored slots): one
-        // dependent round trip per expansion instead of two
-        const uint32_t cg = guard_id(g, cur);
-        const int32_t rowv = lane < capl ? ld_i32<COH>(adjp + (size_t)cg * capl + lane) : -1;
-        const int deg = min(ld_i32<COH>(degp + cg), capl);
-        if (deg <= 0) continue;
-        const bool have = lane < deg;
-        uint32_t nb = have ? (uint32_t)rowv : 0u;
-        int pr = 0;
-        if (have && nb != 0xFFFFFFFFu) {
-            nb = guard_id(g, nb);
-            pr = vis_probe_n(vis, (uint32_t)vsize, nb);
+        uint32_t cur[XW];
+        cur[0] = bl_next(L);
+        if (cur[0] == EMPTY_ID) break;
+#pragma unroll
+        for (int w = 1; w < XW; ++w) cur[w] = bl_next(L);
+        // the adjacency rows are loaded together with their degrees (rows are
+        // cap wide, so lanes past the degree read allocated, ignored slots):
+        // one dependent round trip per step
+        int32_t rowv[XW];
+        int deg[XW];
+#pragma unroll
+        for (int w = 0; w < XW; ++w) {
+            rowv[w] = -1;
+            deg[w] = 0;
+            if (cur[w] != EMPTY_ID) {
+                st.X += 1;
+                const uint32_t cg = guard_id(g, cur[w]);
+                rowv[w] = lane < capl ? ld_i32<COH>(adjp + (size_t)cg * capl + lane) : -1;
+                deg[w] = min(ld_i32<COH>(degp + cg), capl);
+            }
         }
-        vcount += __popcll(__ballot(pr == 1));
-        int cnt;
-        const uint32_t cid = compact(nb, pr != 0, cnt);
-        if (cnt == 0) continue;
-        st.E += cnt;
-        auto sink = [&](float d, uint32_t u) { bl_insert(L, ef, d, u); };
+        uint32_t cids[XW];
+        int cnts[XW];
+#pragma unroll
+        for (int w = 0; w < XW; ++w) {
+            const bool have = lane < deg[w];
+            uint32_t nb = have ? (uint32_t)rowv[w] : 0u;
+            int pr = 0;
+            if (have && nb != 0xFFFFFFFFu) {
+                nb = guard_id(g, nb);
+                pr = vis_probe_n(vis, (uint32_t)vsize, nb);
+            }
+            vcount += __popcll(__ballot(pr == 1));
+            cids[w] = compact(nb, pr != 0, cnts[w]);
+        }
+        // one batch when the new neighbours fit the wave
+        if constexpr (XW == 2) {
+            if (cnts[0] + cnts[1] <= 64) {
+                const uint32_t c1 = shfl_u(cids[1], (lane - cnts[0]) & 63);
+                if (lane >= cnts[0]) cids[0] = c1;
+                cnts[0] += cnts[1];
+                cnts[1] = 0;
+            }
+        }
         float wd = __int_as_float(0x7f800000);
         if constexpr (SCREEN) {
             uint32_t wi;
-            bl_at(L, ef - 1, wd, wi);
+            bl_at(L, ef - 1, wd, wi);  // the worst before the step: it only decreases during it
         }
-        if (SCREEN && screen && wd < __int_as_float(0x7f800000)) {
-            st.F += eval_screened<C, G>(g, q, qn, cid, cnt, g.metric, wd, sink, st.S, margin);
-        } else {
-            st.F += cnt;
-            eval_list<C, G>(g, q, qn, cid, cnt, g.metric, sink);
+#pragma unroll
+        for (int w = 0; w < XW; ++w) {
+            const int cnt = cnts[w];
+            if (cnt == 0) continue;
+            const uint32_t cid = cids[w];
+            st.E += cnt;
+            auto sink = [&](float d, uint32_t u) { bl_insert(L, ef, d, u); };
+            if (SCREEN && screen && wd < __int_as_float(0x7f800000)) {
+                st.F += eval_screened<C, G>(g, q, qn, cid, cnt, g.metric, wd, sink, st.S, margin);
+            } else {
+                st.F += cnt;
+                eval_list<C, G>(g, q, qn, cid, cnt, g.metric, sink);
+            }
         }
         if (vcount > (vsize >> 1) + (vsize >> 2)) {  // forget: results unchanged
             __syncthreads();

@@ -120,6 +120,7 @@ struct BatchBuildArgs {
     int mcap;                     // neighbors to select on this layer
     int heuristic;                // 0 closest-M, 1 HNSW heuristic on the new row, 2 also on overflowing rows
     int keep_pruned;              // fill the new row with pruned candidates up to mcap
+    int expand;                   // entries expanded per step of the layer search (1 or 2; beam_layer XW)
     float alpha;                  // diversity slack: drop c when alpha * d(c, kept) < d(u, c) (1 = HNSW Alg. 4)
     int32_t* inc_cnt;             // [cap_nodes] incoming request counters (zero between batches)
     uint32_t* inc_src;            // [cap_nodes * inc_cap]

@@ -74,7 +74,9 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * (heuristic slack x100: c is dropped when alpha*d(c,kept) < d(u,c); 100 = HNSW
  * Alg. 4), "batch_min", "batch_max", "batch_ratio_pct", "vis_log2" (compat / build visited sets:
  * 2^n entries), "vis_entries" (beam search's visited set, 0 = 1.25 * 2^vis_log2),
- * "exact_kk",
+ * "build_expand" (batched insert: entries expanded per step of its layer
+ * searches, 2 (default) or 1 -- two fetch their adjacency rows in one round
+ * trip and evaluate their new neighbours as one batch), "exact_kk",
  * "exact_precision" (exact-mode scoring: 0 f32-input MFMA, 1 bf16x3 split MFMA,
  * 2 fp16 2-product split MFMA, 3 (default) fp16 1-product MFMA with the top-kk
  * preselection fused into the GEMM epilogue; all preselect, re-rank canonically

@@ -318,13 +318,14 @@ def _clustered(rng, n, d, nc=64, intrinsic=12, noise=0.05):
 
 
 @pytest.mark.parametrize("metric", [0, 1])
-def test_batch_build_recall_and_exact_parity(H, O, metric):
+@pytest.mark.parametrize("expand", [1, 2])
+def test_batch_build_recall_and_exact_parity(H, O, metric, expand):
     rng = np.random.default_rng(11 + metric)
     n, d = 20000, 64
     X = _clustered(rng, n, d)
     Q = _clustered(rng, 200, d)
     g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=_metric_fn(H, metric), Rng=9, build_mode=H.BUILD_BATCH,
-                ef_construction=100, heuristic=2)
+                ef_construction=100, heuristic=2, build_expand=expand)
     g.add_arrays(np.arange(n), X)
     st = g.stats()
     assert st["dropped_proposals"] == 0
