@@ -563,28 +563,38 @@ static int launch_build_compat_t(const CompatBuildArgs& a, int waves, hipStream_
 // ---------------------------------------------------------------------------
 // One kept row r (f32 row qr, norm rn) applied to every candidate still
 // standing after list position pos (entry e = k * 64 + lane of the NR
-// registers: live / dropped flags, id eid, d(u, c) ed): a candidate is dropped
+// registers: bit k of live / dropped, id ids[k] & ID_MASK, d(u, c) ed[k] --
+// the list's own registers, nothing copied): a candidate is dropped
 // when alpha d(c, r) < d(u, c) -- decided by a two-sided screen of the
 // candidates' fp16 rows against per-row thresholds, the undecided pairs in
 // f32 (the neighbour selection of k_batch_search and k_batch_commit).
 template <class C, int G, int NR>
 __device__ __forceinline__ void drop_pass(const GraphDev& g, const QReg<C>& qr, float rn, int pos,
-                                          const bool (&live)[NR], bool (&dropped)[NR], const uint32_t (&eid)[NR],
+                                          uint32_t live, uint32_t& dropped, const uint32_t (&ids)[NR],
                                           const float (&ed)[NR], float alpha, float margin, WaveStats& st) {
     const int lane = lane_id();
     const bool scr = h16_query_ok(rn);
     st.F += 1;  // the kept row
-#pragma unroll
+    // (the body is too large to unroll: register r's id / distance are picked by
+    // a small unrolled select, which keeps the list's registers out of scratch)
     for (int r = 0; r < NR; ++r) {
-        const bool cand = live[r] && !dropped[r] && r * 64 + lane >= pos;
+        uint32_t idr = ids[0];
+        float edr = ed[0];
+#pragma unroll
+        for (int k = 1; k < NR; ++k) {  // bitwise selects: a `?:` chain is folded back into an indexed load
+            const uint32_t mk = k == r ? 0xFFFFFFFFu : 0u;
+            idr = (ids[k] & mk) | (idr & ~mk);
+            edr = bsel(mk, ed[k], edr);
+        }
+        const bool cand = ((live & ~dropped) >> r & 1u) && r * 64 + lane >= pos;
         const unsigned long long m = __ballot(cand);
         if (!m) continue;
         const int cnt = __popcll(m);
         const int before =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
         const int dst = cand ? before : cnt + (lane - before);
-        const uint32_t cc = push_to(eid[r], dst);
-        const float cd = __uint_as_float(push_to(__float_as_uint(ed[r]), dst));
+        const uint32_t cc = push_to(idr & ID_MASK, dst);
+        const float cd = __uint_as_float(push_to(__float_as_uint(edr), dst));
         st.E += cnt;
         // with t = d(u, c) / alpha: an estimate proving d(c, r) > t (1 + 2^-20)
         // keeps c, one proving d(c, r) < t (1 - 2^-20) drops it; the brackets
@@ -620,7 +630,7 @@ __device__ __forceinline__ void drop_pass(const GraphDev& g, const QReg<C>& qr, 
             dr = dr || (und && dks != 0);
         }
         const int drs = __shfl((int)dr, dst, 64);
-        dropped[r] = dropped[r] || (cand && drs != 0);
+        if (cand && drs != 0) dropped |= 1u << r;
     }
 }
 
@@ -658,7 +668,7 @@ __global__ __launch_bounds__(64) void k_batch_descend(BatchBuildArgs a) {
     }
 }
 
-template <class C, int R, int G, bool SCREEN>
+template <class C, int R, int G, bool SCREEN, int XW>
 __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t u;
@@ -686,10 +696,7 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
         if (lane == 0 && id != EMPTY_ID) a.cur_entry[u] = id & ID_MASK;
     } else {
         BList<R> L;
-        if (a.expand == 2)
-            beam_layer<C, R, G, false, SCREEN, 2>(a.g, l, ep, a.ef, q, qn, L, smem, 1 << a.vis_log2, st);
-        else
-            beam_layer<C, R, G, false, SCREEN, 1>(a.g, l, ep, a.ef, q, qn, L, smem, 1 << a.vis_log2, st);
+        beam_layer<C, R, G, false, SCREEN, XW>(a.g, l, ep, a.ef, q, qn, L, smem, 1 << a.vis_log2, st);
         float d0;
         uint32_t i0;
         bl_at(L, 0, d0, i0);
@@ -720,20 +727,16 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
         // per insert on the bench index.
         const bool rowmajor = SCREEN && sel_screen && a.heuristic;
         if (rowmajor) {
-            bool live[R], dropped[R];
-            uint32_t eid[R];
+            uint32_t live = 0u, dropped = 0u;  // bit r: entry r * 64 + lane
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                eid[r] = L.i[r] & ID_MASK;
-                live[r] = L.i[r] != EMPTY_ID && r * 64 + lane < nl && !is_dead(a.g, eid[r]);
-                dropped[r] = false;
-            }
+            for (int r = 0; r < R; ++r)
+                if (L.i[r] != EMPTY_ID && r * 64 + lane < nl && !is_dead(a.g, L.i[r] & ID_MASK)) live |= 1u << r;
             int pos = 0;
             while (nsel < a.mcap) {
                 int idx = -1;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const unsigned long long m = __ballot(live[r] && !dropped[r] && r * 64 + lane >= pos);
+                    const unsigned long long m = __ballot(((live & ~dropped) >> r & 1u) && r * 64 + lane >= pos);
                     if (idx < 0 && m) idx = r * 64 + __ffsll((long long)m) - 1;
                 }
                 if (idx < 0) break;
@@ -750,7 +753,7 @@ __global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
                 if (nsel >= a.mcap) break;
                 QReg<C> qr;
                 load_query(qr, a.g.vecs + (size_t)c * a.g.pitch);
-                drop_pass<C, G, R>(a.g, qr, a.g.norms[c], pos, live, dropped, eid, L.d, a.alpha, margin, st);
+                drop_pass<C, G, R>(a.g, qr, a.g.norms[c], pos, live, dropped, L.i, L.d, a.alpha, margin, st);
             }
         }
         for (int i = 0; !rowmajor && i < nl && nsel < a.mcap; ++i) {
@@ -891,23 +894,22 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
         if (rowmajor) {
             const float e = a.g.h16err ? *a.g.h16err : 0.00048828125f;
             const float margin = a.g.metric == EUCLIDEAN ? h16_margin_l2(e) : h16_margin_cos(e);
-            bool live[2], dropped[2];
+            uint32_t live = 0u, dropped = 0u;
             uint32_t eid[2];
             float ed[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int e2 = lane + 64 * h;
-                live[h] = e2 < tot;
-                eid[h] = live[h] ? guard_id(a.g, ri[e2]) : 0u;
+                if (e2 < tot) live |= 1u << h;
+                eid[h] = e2 < tot ? guard_id(a.g, ri[e2]) : 0u;
                 ed[h] = rd[e2];
-                dropped[h] = false;
             }
             int pos = 0;
             while (nkeep < keep_cap) {
                 int idx = -1;
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const unsigned long long m = __ballot(live[h] && !dropped[h] && h * 64 + lane >= pos);
+                    const unsigned long long m = __ballot(((live & ~dropped) >> h & 1u) && h * 64 + lane >= pos);
                     if (idx < 0 && m) idx = h * 64 + __ffsll((long long)m) - 1;
                 }
                 if (idx < 0) break;
@@ -1157,10 +1159,16 @@ static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 << a.vis_log2;
     const int64_t n = a.order ? a.count : a.n1 - a.n0;
     if (n <= 0) return 0;
-    if (a.g.h16)  // fp16 screening: same graph, fewer bytes per candidate
-        hipLaunchKernelGGL((k_batch_search<C, R, G, true>), dim3((unsigned)n), dim3(64), lds, s, a);
+    // fp16 screening: same graph, fewer bytes per candidate; XW = a.expand as a
+    // template argument (one search variant per kernel keeps it spill-free)
+    if (a.g.h16 && a.expand == 2)
+        hipLaunchKernelGGL((k_batch_search<C, R, G, true, 2>), dim3((unsigned)n), dim3(64), lds, s, a);
+    else if (a.g.h16)
+        hipLaunchKernelGGL((k_batch_search<C, R, G, true, 1>), dim3((unsigned)n), dim3(64), lds, s, a);
+    else if (a.expand == 2)
+        hipLaunchKernelGGL((k_batch_search<C, R, G, false, 2>), dim3((unsigned)n), dim3(64), lds, s, a);
     else
-        hipLaunchKernelGGL((k_batch_search<C, R, G, false>), dim3((unsigned)n), dim3(64), lds, s, a);
+        hipLaunchKernelGGL((k_batch_search<C, R, G, false, 1>), dim3((unsigned)n), dim3(64), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
