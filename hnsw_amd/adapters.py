@@ -55,11 +55,15 @@ class ExactIndex:
             if latest[k].size != d0:
                 raise HnswError(-2, f"embedding dimension mismatch: {d0} != {latest[k].size}")
         # replacement = map assignment: present keys are overwritten in place
-        # (the store does not grow), the others are added
-        present = self._g.Replace([Node(k, latest[k]) for k in ks]) if self._g.Len() else [False] * len(ks)
+        # (the store does not grow), the others are added -- the add first: the
+        # replace of validated rows cannot fail on its arguments
+        present = self._g.contains(ks) if self._g.Len() else np.zeros(len(ks), bool)
         new = [Node(k, latest[k]) for k, p in zip(ks, present) if not p]
         if new:
             self._g.BatchAdd(new)
+        old = [Node(k, latest[k]) for k, p in zip(ks, present) if p]
+        if old:
+            self._g.Replace(old)
 
     def Search(self, query, k: int) -> List[Node]:  # exact.go:62-109
         if self.Len() == 0:

@@ -97,6 +97,10 @@ struct mhnsw_index {
     int32_t* levels = nullptr;
     uint8_t* dead = nullptr;  // [capn] deleted rows (graph.go:843-864)
     bool any_dead = false;
+    // key identity (compat; GraphDev::kid): allocated at the first replaced or re-added key
+    int32_t* kid = nullptr;      // [capn] first row that held the row's key
+    int32_t* kidlive = nullptr;  // [capn] by kid: the key's live row (-1 none)
+    bool aliased = false;
     uint32_t* cur_entry = nullptr;
     int32_t* inc_cnt = nullptr;
     uint32_t* inc_src = nullptr;
@@ -145,8 +149,12 @@ struct mhnsw_index {
     DevBuf<float> xbound, xmaxn, xsegd;
     DevBuf<uint32_t> xsegi;
     DevBuf<uint8_t> xflag;
+    DevBuf<uint8_t> xgone;     // exact path: rows to skip when some live row is not in layer 0
+    int64_t partial_rows = 0;  // rows neither deleted nor in layer 0 (left by failed inserts, graph.go:1009)
     DevBuf<int32_t> xflagged, xnflag;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t gev0 = nullptr, gev1 = nullptr;  // the exact path's score GEMM (first query chunk)
+    bool have_gemm_timing = false;
     // cross-stream ordering: a *_device search returns once enqueued on the
     // caller's stream; the next call on another stream (or a mutation) must
     // not reuse scratch / rewrite the graph under it
@@ -165,6 +173,8 @@ struct mhnsw_index {
     std::vector<int32_t> hlevels;
     std::vector<uint32_t> hmask;  // bit l: row is in layer l (compat may promote into emptied layers)
     std::vector<uint8_t> hdead;
+    std::vector<int32_t> hkid;                       // kid mirror (aliased only)
+    std::unordered_map<int64_t, int32_t> dead_kid;   // deleted keys -> kid, for a later re-add
     int64_t stats_host[8] = {0};
     std::string err;
     mutable std::shared_mutex mu;
@@ -329,6 +339,7 @@ int ensure_capacity(mhnsw_index* h, int64_t need) {
     if ((r = grow(h, h->keys, oc, nc, 0))) return r;
     if ((r = grow(h, h->levels, oc, nc, 0))) return r;
     if ((r = grow(h, h->dead, oc, nc, 0))) return r;
+    if (h->aliased && ((r = grow(h, h->kid, oc, nc, 0xFF)) || (r = grow(h, h->kidlive, oc, nc, 0xFF)))) return r;
     if ((r = grow(h, h->cur_entry, 0, nc, 0))) return r;
     if ((r = grow(h, h->inc_cnt, 0, nc, 0))) return r;
     if (h->build_mode == MHNSW_BUILD_BATCH || h->inc_src) {
@@ -379,6 +390,8 @@ GraphDev graph_view(const mhnsw_index* h) {
     g.h16aux = h->h16aux;
     g.h16err = h->h16err;
     if (h->h16_metric != h->metric) g.h16 = nullptr;  // stale format: no screening
+    g.kid = h->aliased ? h->kid : nullptr;
+    g.kidlive = h->aliased ? h->kidlive : nullptr;
     return g;
 }
 
@@ -440,12 +453,30 @@ int zero_err(mhnsw_index* h) {
 // ---------------------------------------------------------------------------
 // build drivers
 // ---------------------------------------------------------------------------
-int run_build_compat(mhnsw_index* h, int64_t n0, int64_t n1, int top0) {
+// BatchAdd of a present key (graph.go:1015-1024): the launch's last insert
+struct CompatRep {
+    int level = -1, i0 = -1;  // level -1: none
+    int32_t a = -1, b = -1;   // rows above i0 / from i0 down
+    const int32_t* entry = nullptr;  // [MH_MAXL] entry() at each layer's turn (the row itself: empty then)
+    const int32_t* sweep = nullptr;  // [MH_MAXL] row deleted + isolated per layer (-1 none)
+};
+
+// fresh inserts [n0, n1) then cr's; entry: [MH_MAXL] layer entries the fresh
+// inserts see.  On the reference's "no nodes found in neighborhood search"
+// returns 0 with *fail_row / *fail_layer set (the caller unwinds).
+int run_build_compat(mhnsw_index* h, int64_t n0, int64_t n1, int top0, const int32_t* entry, const CompatRep& cr,
+                     int64_t* fail_row, int* fail_layer) {
     if (h->M + 1 > 64) return fail(h, MHNSW_EUNSUPPORTED, "compat build supports M <= 63");
     int r;
-    if ((r = sync_layer_entries(h))) return r;
-    if ((r = sync_layer_table(h))) return r;
-    if ((r = zero_err(h))) return r;
+    int32_t e[3 * MH_MAXL];
+    for (int l = 0; l < MH_MAXL; ++l) {
+        e[l] = entry[l];
+        e[MH_MAXL + l] = cr.entry ? cr.entry[l] : -1;
+        e[2 * MH_MAXL + l] = cr.sweep ? cr.sweep[l] : -1;
+    }
+    HIPCHK(h, hipMemcpyAsync(h->d_layer_entry, e, sizeof(e), hipMemcpyHostToDevice, h->stream));
+    if ((r = sync_layer_table(h))) return r;  // (e stays alive until the stream sync below)
+    HIPCHK(h, hipMemsetAsync(h->d_err, 0, 4 * sizeof(int), h->stream));
     CompatBuildArgs a;
     a.g = graph_view(h);
     a.n0 = n0;
@@ -458,16 +489,25 @@ int run_build_compat(mhnsw_index* h, int64_t n0, int64_t n1, int top0) {
     a.stats = h->d_stats + 4;
     a.err = h->d_err;
     a.vis_log2 = h->vis_log2;
+    a.rep_level = cr.level;
+    a.rep_i0 = cr.i0;
+    a.rep_a = cr.a >= 0 ? (uint32_t)cr.a : EMPTY_ID;
+    a.rep_b = cr.b >= 0 ? (uint32_t)cr.b : EMPTY_ID;
+    a.rep_entry = h->d_layer_entry + MH_MAXL;
+    a.rep_sweep = h->d_layer_entry + 2 * MH_MAXL;
     int lr = launch_build_compat(a, h->lpr, h->vpl, h->compat_waves, h->stream);
     if (lr == -2) return fail(h, MHNSW_EUNSUPPORTED, "compat build LDS budget exceeded (ef=%d, M=%d)", h->ef, h->M);
     LCHK(h, lr);
-    int err = 0;
-    HIPCHK(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    int err[4] = {0, 0, 0, 0};
+    HIPCHK(h, hipMemcpyAsync(err, h->d_err, sizeof(err), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    if (err & 1) return fail(h, MHNSW_EINTERNAL, "visited set overflow (raise vis_log2)");
-    if (err & 2) return fail(h, MHNSW_EINTERNAL, "no nodes found in neighborhood search");
-    if (err & 4) return fail(h, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
-    if (err & 8) return fail(h, MHNSW_EINTERNAL, "replenish candidate heap overflow");
+    if (err[0] & 1) return fail(h, MHNSW_EINTERNAL, "visited set overflow (raise vis_log2)");
+    if (err[0] & 4) return fail(h, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
+    if (err[0] & 8) return fail(h, MHNSW_EINTERNAL, "replenish candidate heap overflow");
+    if (err[0] & 2) {
+        *fail_layer = err[2];
+        *fail_row = err[3];
+    }
     return 0;
 }
 
@@ -625,47 +665,87 @@ int h16_rows(mhnsw_index* h, int64_t r0, int64_t r1) {
     return 0;
 }
 
+// ---- key identity (compat semantics, GraphDev::kid) -------------------------
+// The reference's layer and neighbour maps are keyed by K.  A replaced key
+// (BatchAdd, graph.go:1015-1024) or a deleted key added again leaves several
+// rows with one key, the old ones reachable through one-directional edges.
+// From the first such row on, rows carry kid = the first row that held their
+// key (kid[r] = r before), and kidlive[kid] = the key's live row.
+const int32_t kNoRow = -1;  // source of kidlive resets (async copies read it later)
+int32_t kid_of_row(const mhnsw_index* h, int64_t r) { return h->aliased ? h->hkid[r] : (int32_t)r; }
+
+int set_kidlive(mhnsw_index* h, int32_t kid, int32_t row) {
+    HIPCHK(h, hipMemcpyAsync(h->kidlive + kid, &row, 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));  // `row` is a stack value
+    return 0;
+}
+
+int start_alias(mhnsw_index* h) {
+    if (h->aliased) return 0;
+    const int64_t c = std::max<int64_t>(h->capn, 1);
+    int r;
+    if ((r = grow(h, h->kid, 0, c, 0xFF)) || (r = grow(h, h->kidlive, 0, c, 0xFF))) return r;
+    h->hkid.resize((size_t)h->n);
+    std::vector<int32_t> live((size_t)std::max<int64_t>(h->n, 1));
+    for (int64_t i = 0; i < h->n; ++i) {
+        h->hkid[i] = (int32_t)i;
+        live[i] = h->hdead[i] ? -1 : (int32_t)i;
+    }
+    if (h->n > 0) {
+        HIPCHK(h, hipMemcpyAsync(h->kid, h->hkid.data(), (size_t)h->n * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->kidlive, live.data(), (size_t)h->n * 4, hipMemcpyHostToDevice, h->stream));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->aliased = true;
+    return 0;
+}
+
+// a row leaves the key map (Delete): remember its kid for a later re-add
+void forget_key(mhnsw_index* h, int64_t key, int32_t row) { h->dead_kid[key] = kid_of_row(h, row); }
+
 int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_on_device, int64_t n, int dim,
              const int32_t* levels) {
     int r = validate(h);
     if (r) return r;
     if (n <= 0) return 0;
-    if (h->layers_exist && h->dim != dim)  // graph.go:450-455
+    if (h->layers_exist && h->dim != dim)  // graph.go:955-960
         return fail(h, MHNSW_EDIM, "embedding dimension mismatch: %d != %d", h->dim, dim);
     if (!h->layers_exist && (r = set_shape(h, dim))) return r;
-    // reject duplicates (reference Add deadlocks on them, graph.go:511-513 -> :844)
-    {
+    const bool flat = h->build_mode == MHNSW_BUILD_FLAT;  // no graph: every row in layer 0, no links
+    const bool compat = h->build_mode == MHNSW_BUILD_COMPAT;
+    // A present key.  Compat: BatchAdd's replacement (graph.go:1015-1024) -- the
+    // walk inserts every node up to the first present key (in the index or
+    // earlier in this batch), replaces that one, and stops with "node not
+    // added" (graph.go:1035-1037: Len() did not grow).  The batched and flat
+    // builds have no reference semantics to follow: they reject it.
+    if (!compat) {
         std::unordered_map<int64_t, int> seen;
         for (int64_t i = 0; i < n; ++i) {
             if (h->key2id.count(keys[i]) || seen.count(keys[i]))
-                return fail(h, MHNSW_EUNSUPPORTED, "duplicate key %lld: replacement not supported",
+                return fail(h, MHNSW_EUNSUPPORTED, "duplicate key %lld: replacement needs the compat build mode",
                             (long long)keys[i]);
             seen[keys[i]] = 1;
         }
     }
-    const bool flat = h->build_mode == MHNSW_BUILD_FLAT;  // no graph: every row in layer 0, no links
-    if (h->build_mode == MHNSW_BUILD_COMPAT && h->M + 1 > 64)
-        return fail(h, MHNSW_EUNSUPPORTED, "compat build supports M <= 63");
+    if (compat && h->M + 1 > 64) return fail(h, MHNSW_EUNSUPPORTED, "compat build supports M <= 63");
     if (m0_of(h) + 1 > 64 || h->M + 1 > 64) return fail(h, MHNSW_EUNSUPPORTED, "degree caps above 63 unsupported");
     if ((r = ensure_caps(h))) return r;
-    const int64_t n0 = h->n, n1 = h->n + n;
-    const int64_t live0 = live_count(h);
-    // levels (graph.go:457): the layer-0 size (live nodes) grows by one per insert
-    std::vector<int32_t> lv(n);
-    bool le = h->layers_exist;
-    for (int64_t i = 0; i < n; ++i) {
-        if (flat) {
-            lv[i] = 0;
-        } else if (levels) {
-            lv[i] = levels[i];
-            if (lv[i] < 0) return fail(h, MHNSW_EINVAL, "invalid level: %d", lv[i]);
-        } else {
-            lv[i] = random_level(h->ml, le, live0 + i, &h->rng);
-        }
-        if (lv[i] >= MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "level %d >= %d", lv[i], MH_MAXL);
-        le = true;
+    for (int64_t i = 0; i < n && levels && !flat; ++i) {
+        if (levels[i] < 0) return fail(h, MHNSW_EINVAL, "invalid level: %d", levels[i]);
+        if (levels[i] >= MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "level %d >= %d", levels[i], MH_MAXL);
     }
-    if ((r = ensure_capacity(h, n1))) return r;
+    const int64_t n0 = h->n;
+    const int64_t live0 = live_count(h);
+    const uint64_t rng0 = h->rng;
+    const bool le0 = h->layers_exist;
+    // key identity: a key present (or repeated), or a deleted key coming back
+    if (compat) {
+        bool need_alias = false;
+        std::unordered_map<int64_t, int> seen;
+        for (int64_t i = 0; i < n && !need_alias; ++i)
+            need_alias = h->key2id.count(keys[i]) || h->dead_kid.count(keys[i]) || !seen.emplace(keys[i], 1).second;
+        if (need_alias && (r = start_alias(h))) return r;
+    }
     const int top0 = (int)h->layers.size() - 1;  // len(g.layers) - 1 before this batch
     int top_live = -1;
     uint32_t entry_live = EMPTY_ID;
@@ -673,52 +753,285 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
         top_live = top_live_layer(h);
         entry_live = (uint32_t)h->layers[top_live].entry;
     }
-    int maxl = 0;
-    for (auto v : lv) maxl = std::max(maxl, v);
-    if ((r = ensure_layer(h, maxl))) return r;
-    // upload keys, levels, vectors (padded), norms
-    HIPCHK(h, hipMemcpyAsync(h->keys + n0, keys, n * sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipMemcpyAsync(h->levels + n0, lv.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
-    const float* src = vecs;
-    if (!vecs_on_device) {
-        if ((r = ensure_buf(h, h->tmp, (size_t)n * dim))) return r;
-        HIPCHK(h, hipMemcpyAsync(h->tmp.p, vecs, (size_t)n * dim * 4, hipMemcpyHostToDevice, h->stream));
-        src = h->tmp.p;
+    // Host bookkeeping (layer membership, counts, entries, keys) in the walk's
+    // order.  floor >= 0: an insert that failed at layer `floor` -- only the
+    // layers above it were touched (graph.go:1005-1010 returns there).
+    std::vector<int32_t> lv;      // level of each insert the walk reaches
+    std::vector<int64_t> rowkey;  // key of every new row
+    std::vector<int32_t> kidset;  // kidlive entries to publish: (kid, row) pairs
+    std::vector<std::pair<int64_t, int32_t>> snap_layers;
+    for (auto& L : h->layers) snap_layers.emplace_back(L.count, L.entry);
+    const bool snap_any_dead = h->any_dead;
+    std::unordered_map<int64_t, int32_t> snap_dead_kid;  // re-added keys' entries, restored on unwind
+    std::unordered_map<int64_t, int32_t> snap_key2id;    // the batch's keys before it (-1 absent)
+    for (int64_t i = 0; i < n && compat; ++i) {
+        auto it = h->key2id.find(keys[i]);
+        snap_key2id.emplace(keys[i], it == h->key2id.end() ? -1 : it->second);
     }
-    LCHK(h, launch_pad_rows(src, n, dim, h->vecs + (size_t)n0 * h->pitch, h->pitch, h->stream));
-    LCHK(h, launch_norms(h->vecs, n0, n1, h->pitch, h->lpr, h->vpl, h->norms, h->stream));
-    if ((r = h16_rows(h, n0, n1))) return r;
-    // host bookkeeping: layer membership, counts, entries
-    const bool compat = h->build_mode == MHNSW_BUILD_COMPAT;
-    h->hmask.resize(n1, 0u);
-    h->hdead.resize(n1, 0);
+    h->hmask.resize(n0 + n + 1, 0u);
+    h->hdead.resize(n0 + n + 1, 0);
     int nl = top0 + 1;
-    for (int64_t i = 0; i < n; ++i) {
+    auto book_fresh = [&](int64_t i, int floor) {
         const int32_t id = (int32_t)(n0 + i);
-        h->key2id[keys[i]] = id;
+        rowkey.push_back(keys[i]);
         h->hlevels.push_back(lv[i]);
-        nl = std::max(nl, lv[i] + 1);  // graph.go:462-464
+        if (h->aliased) {
+            // kid: the key's live node (a node left in upper layers only by a failed
+            // insert), else its deleted one, else this row
+            auto kp = h->key2id.find(keys[i]);
+            auto dk = h->dead_kid.find(keys[i]);
+            int32_t kid = id;
+            if (kp != h->key2id.end()) {
+                kid = kid_of_row(h, kp->second);
+            } else if (dk != h->dead_kid.end()) {
+                kid = dk->second;
+                snap_dead_kid[keys[i]] = dk->second;
+                h->dead_kid.erase(dk);
+            }
+            h->hkid.push_back(kid);
+            kidset.push_back(kid);
+            kidset.push_back(id);
+        } else {
+            h->dead_kid.erase(keys[i]);
+        }
+        nl = std::max(nl, lv[i] + 1);  // graph.go:967-969
         uint32_t mask = 0;
-        for (int l = nl - 1; l >= 0; --l) {
+        for (int l = nl - 1; l > floor; --l) {
             Layer& L = h->layers[l];
-            // graph.go:485-488: an empty layer takes the node whatever its level
+            // graph.go:990-993: an empty layer takes the node whatever its level
             if (!(l <= lv[i] || (compat && L.count == 0))) continue;
             if (L.count == 0) L.entry = id;
             L.count++;
             mask |= 1u << l;
         }
         h->hmask[id] = mask;
+        if (mask) {
+            h->key2id[keys[i]] = id;
+        } else if (snap_dead_kid.count(keys[i])) {  // failed before touching a layer: still a deleted key
+            h->dead_kid[keys[i]] = snap_dead_kid[keys[i]];
+        }
+    };
+    // The walk (graph.go:950-1039): levels drawn insert by insert (graph.go:962,
+    // the layer-0 size growing by one per insert; nothing is drawn for inserts
+    // never reached).  A present key whose node holds a layer at or below the
+    // new level is replaced there and ends the walk; one whose node sits only in
+    // higher layers (left by a failed insert) is inserted like a new key.
+    int64_t rep = -1, nfresh = 0;
+    int rep_i0 = -1;
+    int32_t old = -1;
+    {
+        bool le = h->layers_exist;
+        for (int64_t i = 0; i < n; ++i) {
+            int32_t l_i;
+            if (flat) {
+                l_i = 0;
+            } else if (levels) {
+                l_i = levels[i];
+                if (l_i < 0) return fail(h, MHNSW_EINVAL, "invalid level: %d", l_i);
+            } else {
+                l_i = random_level(h->ml, le, live0 + i, &h->rng);
+            }
+            if (l_i >= MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "level %d >= %d", l_i, MH_MAXL);
+            le = true;
+            lv.push_back(l_i);
+            if ((r = ensure_layer(h, l_i))) return r;
+            if (compat) {
+                auto it = h->key2id.find(keys[i]);
+                if (it != h->key2id.end()) {
+                    for (int l = l_i; l >= 0 && rep_i0 < 0; --l)
+                        if (in_layer(h, it->second, l)) rep_i0 = l;
+                    if (rep_i0 >= 0) {
+                        rep = i;
+                        old = it->second;
+                        break;
+                    }
+                }
+            }
+            book_fresh(i, -1);
+            ++nfresh;
+        }
     }
+    int32_t fresh_entry[MH_MAXL];  // the entries the fresh inserts' walk sees
+    for (int l = 0; l < MH_MAXL; ++l)
+        fresh_entry[l] = l < (int)h->layers.size() && h->layers[l].count > 0 ? h->layers[l].entry : -1;
+    // the replacing insert: old row, the layer i0 of the sweep, the new rows
+    int rep_level = -1;
+    int32_t ida = -1, idb = -1;
+    int32_t rep_entry[MH_MAXL], rep_sweep[MH_MAXL];
+    for (int l = 0; l < MH_MAXL; ++l) rep_entry[l] = rep_sweep[l] = -1;
+    int64_t nrows = nfresh;
+    uint32_t amask = 0;
+    auto book_rep = [&](int floor) {
+        const int32_t kid = kid_of_row(h, old);
+        for (int32_t id : {ida, idb}) {
+            if (id < 0) continue;
+            rowkey.push_back(keys[rep]);
+            h->hlevels.push_back(rep_level);
+            h->hkid.push_back(kid);
+        }
+        // graph.go:980-1032 top-down, as the walk sees the layers
+        for (int l = nl - 1; l > floor; --l) {
+            Layer& L = h->layers[l];
+            const int32_t id = l > rep_i0 && ida >= 0 ? ida : idb;
+            if (l == rep_i0) {  // the sweep, after this layer's search
+                rep_entry[l] = L.entry;
+                for (int l2 = 0; l2 < (int)h->layers.size(); ++l2) {
+                    const int32_t x = in_layer(h, old, l2) ? old : (ida >= 0 && ((amask >> l2) & 1u)) ? ida : -1;
+                    rep_sweep[l2] = x;
+                    if (x >= 0) h->layers[l2].count--;
+                }
+                h->hdead[old] = 1;
+                if (ida >= 0) h->hdead[ida] = 1;
+                h->any_dead = true;
+                h->key2id[keys[rep]] = idb;
+                L.count++;
+                h->hmask[idb] |= 1u << l;
+                continue;
+            }
+            const bool empty = L.count == 0;
+            if (!(l <= rep_level || (compat && empty))) {
+                rep_entry[l] = L.entry;
+                continue;
+            }
+            if (empty) L.entry = id;
+            rep_entry[l] = empty ? id : L.entry;
+            L.count++;
+            h->hmask[id] |= 1u << l;
+        }
+    };
+    if (rep >= 0) {
+        rep_level = lv[rep];
+        nl = std::max(nl, rep_level + 1);
+        for (int l = nl - 1; l > rep_i0; --l)
+            if (h->layers[l].count == 0 || l <= rep_level) amask |= 1u << l;
+        if (amask) ida = (int32_t)(n0 + nrows++);
+        idb = (int32_t)(n0 + nrows++);
+        book_rep(-1);
+    }
+    const int64_t nproc = (int64_t)lv.size();
+    // a failed insert (graph.go:1009 "no nodes found in neighborhood search"):
+    // back to the snapshot, then the inserts the walk did make, the failing one
+    // only above its failing layer; later rows never existed
+    auto unwind = [&](int64_t fail_row, int fail_layer) -> int {
+        const bool rep_failed = rep >= 0 && (fail_row == ida || fail_row == idb);
+        const int64_t i_f = rep_failed ? rep : fail_row - n0;
+        for (size_t l = 0; l < h->layers.size(); ++l) {
+            h->layers[l].count = l < snap_layers.size() ? snap_layers[l].first : 0;
+            h->layers[l].entry = l < snap_layers.size() ? snap_layers[l].second : -1;
+        }
+        h->any_dead = snap_any_dead;
+        for (auto& kv : snap_key2id) {  // the batch's keys as they were
+            if (kv.second < 0)
+                h->key2id.erase(kv.first);
+            else
+                h->key2id[kv.first] = kv.second;
+        }
+        if (rep >= 0) h->hdead[old] = 0;  // live until the sweep
+        for (auto& kv : snap_dead_kid) h->dead_kid[kv.first] = kv.second;
+        for (size_t t = 0; t + 1 < kidset.size() && h->aliased; t += 2)  // unpublish; the replay republishes
+            HIPCHK(h, hipMemcpyAsync(h->kidlive + kidset[t], &kNoRow, 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        rowkey.clear();
+        kidset.clear();
+        snap_dead_kid.clear();
+        h->hlevels.resize(n0);
+        if (h->aliased) h->hkid.resize(n0);
+        std::fill(h->hmask.begin() + n0, h->hmask.end(), 0u);
+        std::fill(h->hdead.begin() + n0, h->hdead.end(), (uint8_t)0);
+        nl = top0 + 1;
+        for (int64_t i = 0; i < i_f && i < nfresh; ++i) book_fresh(i, -1);
+        int64_t rows = i_f + 1;
+        if (!rep_failed) {
+            book_fresh(i_f, fail_layer);
+        } else {
+            nl = std::max(nl, rep_level + 1);
+            book_rep(fail_layer);
+            rows = nfresh + (ida >= 0 ? 2 : 1);
+            if (fail_layer >= rep_i0) {  // failed before the sweep: the old node stays
+                h->key2id[keys[rep]] = old;
+                h->hdead[old] = 0;
+                if (ida >= 0) h->hdead[ida] = 0;
+                h->any_dead = snap_any_dead;
+            }
+        }
+        std::vector<int32_t> live;  // (kid, row): the batch's keys' live rows after the replay
+        for (auto& kv : snap_key2id) {
+            auto it = h->key2id.find(kv.first);
+            if (it == h->key2id.end()) continue;
+            live.push_back(kid_of_row(h, it->second));
+            live.push_back(it->second);
+        }
+        for (size_t t = 0; t + 1 < live.size() && h->aliased; t += 2)
+            HIPCHK(h, hipMemcpyAsync(h->kidlive + live[t], &live[t + 1], 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->dead, h->hdead.data(), (size_t)(n0 + rows), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->n = n0 + rows;
+        h->hmask.resize(h->n);
+        h->hdead.resize(h->n);
+        if (!levels && !flat) {  // the draws of the inserts the walk never reached are not made
+            h->rng = rng0;
+            bool le2 = le0;
+            for (int64_t i = 0; i <= i_f; ++i) {
+                (void)random_level(h->ml, le2, live0 + i, &h->rng);
+                le2 = true;
+            }
+        }
+        fix_entries(h);
+        h->partial_rows = 0;
+        for (int64_t i = 0; i < h->n; ++i) h->partial_rows += !h->hdead[i] && !in_layer(h, i, 0);
+        return 0;
+    };
+    const int64_t n1 = n0 + nrows;
+    h->hmask.resize(n1);
+    h->hdead.resize(n1);
+    if ((r = ensure_capacity(h, n1))) return r;
+    // upload keys, levels, vectors (padded), norms
+    HIPCHK(h, hipMemcpyAsync(h->keys + n0, rowkey.data(), nrows * sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->levels + n0, h->hlevels.data() + n0, nrows * sizeof(int32_t), hipMemcpyHostToDevice,
+                             h->stream));
+    if (h->aliased) {
+        HIPCHK(h, hipMemcpyAsync(h->kid + n0, h->hkid.data() + n0, nrows * sizeof(int32_t), hipMemcpyHostToDevice,
+                                 h->stream));
+        for (size_t t = 0; t + 1 < kidset.size(); t += 2)
+            HIPCHK(h, hipMemcpyAsync(h->kidlive + kidset[t], &kidset[t + 1], 4, hipMemcpyHostToDevice, h->stream));
+    }
+    const float* src = vecs;
+    if (!vecs_on_device) {
+        if ((r = ensure_buf(h, h->tmp, (size_t)nproc * dim))) return r;
+        HIPCHK(h, hipMemcpyAsync(h->tmp.p, vecs, (size_t)nproc * dim * 4, hipMemcpyHostToDevice, h->stream));
+        src = h->tmp.p;
+    }
+    if (nfresh > 0) LCHK(h, launch_pad_rows(src, nfresh, dim, h->vecs + (size_t)n0 * h->pitch, h->pitch, h->stream));
+    for (int32_t id : {ida, idb})  // the replacing node's rows hold its vector
+        if (rep >= 0 && id >= 0)
+            LCHK(h, launch_pad_rows(src + (size_t)rep * dim, 1, dim, h->vecs + (size_t)id * h->pitch, h->pitch,
+                                    h->stream));
+    LCHK(h, launch_norms(h->vecs, n0, n1, h->pitch, h->lpr, h->vpl, h->norms, h->stream));
+    if ((r = h16_rows(h, n0, n1))) return r;
     h->layers_exist = true;
     h->n = n1;
-    if (flat)  // members of layer 0 without links (an empty neighbour map, not an absent node)
+    if (flat) {  // members of layer 0 without links (an empty neighbour map, not an absent node)
         r = hipMemsetD32Async((hipDeviceptr_t)(h->layers[0].deg + n0), 0, (size_t)n, h->stream) == hipSuccess
                 ? 0
                 : fail(h, MHNSW_EDEVICE, "device memset failed");
-    else if (compat)
-        r = run_build_compat(h, n0, n1, top0);
-    else
+    } else if (compat) {
+        CompatRep cr;
+        if (rep >= 0) cr = CompatRep{rep_level, rep_i0, ida >= 0 ? ida : idb, idb, rep_entry, rep_sweep};
+        int64_t fail_row = -1;
+        int fail_layer = -1;
+        r = run_build_compat(h, n0, n0 + nfresh, top0, fresh_entry, cr, &fail_row, &fail_layer);
+        if (r == 0 && fail_row >= 0) {
+            if ((r = unwind(fail_row, fail_layer)) == 0)
+                r = fail(h, MHNSW_EINTERNAL, "no nodes found in neighborhood search");
+        } else if (r == 0 && rep >= 0) {
+            HIPCHK(h, hipMemcpyAsync(h->dead, h->hdead.data(), (size_t)h->n, hipMemcpyHostToDevice, h->stream));
+            fix_entries(h);
+            // graph.go:1035-1037: a replacement leaves Len() unchanged
+            if (rep_i0 >= 0) r = fail(h, MHNSW_EINTERNAL, "node not added");
+        }
+    } else {
         r = run_build_batch(h, n0, n1, top_live, entry_live);
+    }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     for (size_t i = 0; i + 1 < h->tev_used; i += 2) {
         float ms = 0.f;
@@ -902,6 +1215,19 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         if ((r = sync_layer_table(h)) || (r = order_meta(h, s))) return r;
         GraphDev g = graph_view(h);
         g.err = errw;
+        // rows the brute force skips: deleted ones, and the live rows of a failed
+        // insert that never reached layer 0 (graph.go:1009 leaves them in upper
+        // layers only; Search cannot return them)
+        const uint8_t* xdead = h->any_dead ? h->dead : nullptr;
+        if (h->partial_rows) {
+            std::vector<uint8_t> gone((size_t)h->n);
+            for (int64_t i = 0; i < h->n; ++i) gone[i] = h->hdead[i] || !in_layer(h, i, 0);
+            if ((r = ensure_buf(h, h->xgone, (size_t)std::max<int64_t>(h->n, 1)))) return r;
+            HIPCHK(h, hipMemcpyAsync(h->xgone.p, gone.data(), (size_t)h->n, hipMemcpyHostToDevice, s));
+            HIPCHK(h, hipStreamSynchronize(s));
+            xdead = h->xgone.p;
+        }
+        g.dead = xdead;
         // certificate constants (u = 2^-24; gamma_n = n u / (1 - n u) bounds any
         // order of n-term f32 summation relative to the sum of magnitudes)
         const double u = std::ldexp(1.0, -24);
@@ -949,7 +1275,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             ExactArgs a{};
             a.X = h->vecs;
             a.xnorm = h->norms;
-            a.dead = h->any_dead ? h->dead : nullptr;
+            a.dead = xdead;
             a.N = h->n;
             a.Q = h->qpad.p + (size_t)q0 * h->pitch;
             a.qnorm = h->qnorm.p + q0;
@@ -1004,7 +1330,10 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
                     a.region = h->h1region.p;
                     a.region_cnt = h->h1rcnt.p;
                     a.rcap = rcap;
+                    if (timing && q0 == 0) HIPCHK(h, hipEventRecord(h->gev0, s));
                     LCHK(h, launch_h1_filter(a, h->exact_tile, s));
+                    if (timing && q0 == 0) HIPCHK(h, hipEventRecord(h->gev1, s));
+                    h->have_gemm_timing = timing;
                     const int64_t bqt = (nb + bm - 1) / bm;
                     LCHK(h, launch_bucket(h->h1region.p, h->h1rcnt.p, rcap, bqt * nnt, bqt, bm, H1_BN, nb, h->h1qcnt.p,
                                           h->h1bucket.p, scap, h->h1ovf.p, a, s));
@@ -1121,11 +1450,12 @@ int mhnsw_create(int metric, int M, double ml, int ef_search, uint64_t seed, mhn
         return fail(nullptr, MHNSW_EDEVICE, "no HIP device available");
     }
     if (hipMalloc(&h->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&h->d_err, 2 * sizeof(int)) != hipSuccess || hipMemset(h->d_err, 0, 2 * sizeof(int)) != hipSuccess ||
+        hipMalloc(&h->d_err, 4 * sizeof(int)) != hipSuccess || hipMemset(h->d_err, 0, 4 * sizeof(int)) != hipSuccess ||
         hipMalloc(&h->h16err, sizeof(float)) != hipSuccess || hipMemset(h->h16err, 0, sizeof(float)) != hipSuccess || hipMalloc(&h->touched_cnt, 16) != hipSuccess ||
-        hipMalloc(&h->d_layer_entry, MH_MAXL * 4) != hipSuccess ||
+        hipMalloc(&h->d_layer_entry, 3 * MH_MAXL * 4) != hipSuccess ||
         hipMalloc(&h->d_layers, MH_MAXL * sizeof(LayerDev)) != hipSuccess || hipEventCreate(&h->ev0) != hipSuccess ||
-        hipEventCreate(&h->ev1) != hipSuccess || hipEventCreateWithFlags(&h->scr_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreate(&h->ev1) != hipSuccess || hipEventCreate(&h->gev0) != hipSuccess ||
+        hipEventCreate(&h->gev1) != hipSuccess || hipEventCreateWithFlags(&h->scr_ev, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->meta_ev, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ord_ev, hipEventDisableTiming) != hipSuccess || hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
         mhnsw_destroy(h);
@@ -1149,6 +1479,8 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->keys);
     F(h->levels);
     F(h->dead);
+    F(h->kid);
+    F(h->kidlive);
     F(h->cur_entry);
     F(h->inc_cnt);
     F(h->inc_src);
@@ -1203,6 +1535,7 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->xsegi.p);
     F(h->xmaxn.p);
     F(h->xflag.p);
+    F(h->xgone.p);
     F(h->xflagged.p);
     F(h->xnflag.p);
     if (h->scr_ev) (void)hipEventDestroy(h->scr_ev);
@@ -1212,6 +1545,8 @@ void mhnsw_destroy(mhnsw_index* h) {
     for (auto e : h->tev) (void)hipEventDestroy(e);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->gev0) (void)hipEventDestroy(h->gev0);
+    if (h->gev1) (void)hipEventDestroy(h->gev1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -1359,6 +1694,13 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "strkeys") *v = (int64_t)h->s2l.size();
     else if (n == "pitch") *v = h->pitch;
     else if (n == "capacity") *v = h->capn;
+    else if (n == "last_gemm_ns") {  // read-only: the last timed exact search's fused score GEMM (HIP events)
+        float ms = 0.f;
+        if (!h->have_gemm_timing || hipEventSynchronize(h->gev1) != hipSuccess ||
+            hipEventElapsedTime(&ms, h->gev0, h->gev1) != hipSuccess)
+            return MHNSW_EINVAL;
+        *v = (int64_t)std::llround((double)ms * 1e6);
+    }
     else if (n == "screen_err_ppb") {  // read-only: the fp16 copy's measured margin E, parts per 1e9
         float e = 0.f;
         if (h->h16err && (hipMemcpyAsync(&e, h->h16err, sizeof(float), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
@@ -1448,10 +1790,36 @@ int64_t mhnsw_layer_count(const mhnsw_index* h, int l) {
     return l >= 0 && l < (int)h->layers.size() ? h->layers[l].count : 0;
 }
 
+int mhnsw_contains(const mhnsw_index* h, const int64_t* keys, int64_t n, uint8_t* out) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    if (n > 0 && (!keys || !out)) return MHNSW_EINVAL;
+    for (int64_t i = 0; i < n; ++i) out[i] = h->key2id.count(keys[i]) ? 1 : 0;
+    return MHNSW_OK;
+}
+
+int mhnsw_add_plan(mhnsw_index* h, const int64_t* keys, int64_t n, int64_t* nwalk, int* one_by_one) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    if (n > 0 && !keys) return fail(h, MHNSW_EINVAL, "keys must be non-NULL");
+    int64_t w = n;
+    if (h->build_mode == MHNSW_BUILD_COMPAT) {
+        std::unordered_map<int64_t, int> seen;
+        for (int64_t i = 0; i < n; ++i) {
+            if (h->key2id.count(keys[i]) || seen.count(keys[i])) {
+                w = i + 1;
+                break;
+            }
+            seen[keys[i]] = 1;
+        }
+    }
+    if (nwalk) *nwalk = w;
+    if (one_by_one) *one_by_one = h->build_mode == MHNSW_BUILD_COMPAT && h->any_dead ? 1 : 0;
+    return MHNSW_OK;
+}
+
 int mhnsw_lookup(mhnsw_index* h, int64_t key, float* out) {
     std::shared_lock<std::shared_mutex> lk(h->mu);
     auto it = h->key2id.find(key);
-    if (it == h->key2id.end()) return 0;
+    if (it == h->key2id.end() || !in_layer(h, it->second, 0)) return 0;  // graph.go:906 layers[0].nodes[key]
     HIPCHK(h, hipMemcpy(out, h->vecs + (size_t)it->second * h->pitch, (size_t)h->dim * 4, hipMemcpyDeviceToHost));
     return 1;
 }
@@ -1556,6 +1924,11 @@ void reset_graph(mhnsw_index* h) {
     h->xsplit_rows = h->xsplit_plane = 0;
     h->dim = h->pitch = h->lpr = h->vpl = 0;
     h->layers_exist = h->any_dead = false;
+    F(h->kid);
+    F(h->kidlive);
+    h->aliased = false;
+    h->hkid.clear();
+    h->dead_kid.clear();
     h->key2id.clear();
     h->hlevels.clear();
     h->hmask.clear();
@@ -1626,6 +1999,21 @@ int import_csr(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t
         if (!h->hdead[i] && !h->key2id.count(keys[i])) h->key2id[keys[i]] = (int32_t)i;
     h->n = N;
     h->layers_exist = L > 0;
+    // key identity: several rows of one key (a replaced or re-added key) -> kids
+    std::unordered_map<int64_t, int32_t> first;
+    bool dup = false;
+    for (int64_t i = 0; i < N; ++i) dup |= !first.emplace(keys[i], (int32_t)i).second;
+    h->dead_kid.clear();
+    for (auto& kv : first)
+        if (!h->key2id.count(kv.first)) h->dead_kid[kv.first] = kv.second;
+    if (dup) {
+        if ((r = start_alias(h))) return r;  // kid = row, then rows of repeated keys take the first one's
+        std::vector<int32_t> live((size_t)N, -1);
+        for (int64_t i = 0; i < N; ++i) h->hkid[i] = first[keys[i]];
+        for (auto& kv : h->key2id) live[first[kv.first]] = kv.second;
+        HIPCHK(h, hipMemcpy(h->kid, h->hkid.data(), (size_t)N * 4, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(h->kidlive, live.data(), (size_t)N * 4, hipMemcpyHostToDevice));
+    }
     return 0;
 }
 
@@ -2108,6 +2496,9 @@ int mhnsw_delete(mhnsw_index* h, const int64_t* keys, int64_t n, uint8_t* out) {
         if (it == h->key2id.end()) continue;  // not found (or deleted earlier in this batch)
         const int32_t id = it->second;
         h->key2id.erase(it);
+        forget_key(h, keys[i], id);
+        if (h->aliased)
+            HIPCHK(h, hipMemcpyAsync(h->kidlive + h->hkid[id], &kNoRow, 4, hipMemcpyHostToDevice, h->stream));
         h->hdead[id] = 1;
         for (int l = 0; l < (int)h->layers.size(); ++l)
             if (in_layer(h, id, l)) h->layers[l].count--;

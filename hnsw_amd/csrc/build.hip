@@ -52,7 +52,8 @@ __device__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v, co
     const int32_t rv = lane < capl ? ld_i32<true>(row + lane) : -1;
     const int d = ld_i32<true>(g.layers[l].deg + n);
     if (d <= 0) return;
-    const bool hit = lane < d && (uint32_t)rv == v;
+    // delete(n.neighbors, v.Key): the entry of v's key, whichever row it holds
+    const bool hit = lane < d && kid_of(g, guard_id(g, (uint32_t)rv)) == kid_of(g, v);
     const unsigned long long m = __ballot(hit);
     if (!m) return;
     const int pos = __ffsll((long long)m) - 1;
@@ -65,8 +66,9 @@ __device__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v, co
     ev.sync();
 }
 
-// append nw to n's neighbour set if absent; returns the new degree and, in
-// *rowout (nullable), the row after the append (lane i: entry i)
+// graph.go:50 n.neighbors[nw.Key] = nw: overwrite the entry of nw's key (which
+// may hold another row of that key), else append; returns the new degree and,
+// in *rowout (nullable), the row after the assignment (lane i: entry i)
 template <class Ev>
 __device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw, const Ev& ev,
                            int32_t* rowout = nullptr) {
@@ -76,15 +78,17 @@ __device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw, co
     const int32_t rv = lane < capl ? ld_i32<true>(row + lane) : -1;
     int d = ld_i32<true>(g.layers[l].deg + n);
     if (d < 0) d = 0;  // graph.go:46-48 allocate the map
-    const bool pres = lane < d && (uint32_t)rv == nw;
-    const bool present = __ballot(pres) != 0;
+    const bool pres = lane < d && kid_of(g, guard_id(g, (uint32_t)rv)) == kid_of(g, nw);
+    const unsigned long long pm = __ballot(pres);
+    const bool present = pm != 0;
+    const int pos = present ? __ffsll((long long)pm) - 1 : d;
     ev.sync();
     if (lane == 0) {
-        if (!present) st_i32(row + d, (int32_t)nw);
+        st_i32(row + pos, (int32_t)nw);
         st_i32(g.layers[l].deg + n, present ? d : d + 1);
     }
     ev.sync();
-    if (rowout) *rowout = (!present && lane == d) ? (int32_t)nw : rv;
+    if (rowout) *rowout = lane == pos ? (int32_t)nw : rv;
     return present ? d : d + 1;
 }
 
@@ -165,18 +169,19 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
     const int vsize = 1 << S.cs.vlog2, vmask = vsize - 1;
     vis_clear(S.cs.vis, vsize);
     ev.sync();
-    if (lane == 0) vis_probe(S.cs.vis, vmask, n);     // graph.go:184
-    if (lane < dn) vis_probe(S.cs.vis, vmask, mine);  // graph.go:187-189
+    if (lane == 0) vis_probe(S.cs.vis, vmask, kid_of(g, n));     // graph.go:184 visited[n.Key]
+    if (lane < dn) vis_probe(S.cs.vis, vmask, kid_of(g, mine));  // graph.go:187-189
     ev.sync();
     int ncand = 0;
     for (int e0 = 0; e0 < tot; e0 += 64) {  // 64 walk positions at a time, in order
         const int e = e0 + lane;
         const uint32_t v = e < tot ? W[e] : EMPTY_ID;
+        const uint32_t kv = v != EMPTY_ID ? kid_of(g, v) : EMPTY_ID;  // graph.go:198 visited[k]: by key
         bool first = v != EMPTY_ID;  // not repeated at a lower lane of this chunk
 #pragma unroll 9
-        for (int l2 = 0; l2 < 63; ++l2) first = first && !(l2 < lane && rl_u(v, l2) == v);
+        for (int l2 = 0; l2 < 63; ++l2) first = first && !(l2 < lane && rl_u(kv, l2) == kv);
         int pr = 0;
-        if (first) pr = vis_probe(S.cs.vis, vmask, v);  // earlier chunks and the pre-visited set
+        if (first) pr = vis_probe(S.cs.vis, vmask, kv);  // earlier chunks and the pre-visited set
         if (__ballot(pr == 2)) err = 1;
         int cnt;
         const uint32_t cid = compact(v, pr == 1, cnt);
@@ -311,6 +316,31 @@ __device__ void add_neighbor(const GraphDev& g, int l, uint32_t n, uint32_t nw, 
     replenish<C, G>(g, l, worst, m, S, st, err, ev);  // graph.go:79
 }
 
+// graph.go:221-235 isolate: neighbours in ascending key order (the map-order
+// stand-in) drop their backlink and are replenished; the deleted node's own
+// row stays (the reference keeps the layerNode behind one-directional edges).
+template <class C, int G, class Ev>
+__device__ void isolate(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err,
+                        const Ev& ev) {
+    const int lane = lane_id();
+    const int capl = g.layers[l].cap;
+    const int dn = min(ld_i32<true>(g.layers[l].deg + n), capl);
+    if (dn < 0) return;  // nil neighbour map
+    uint32_t mine = 0xFFFFFFFFu;
+    int64_t key = INT64_MAX;
+    if (lane < dn) {
+        mine = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane));
+        key = g.keys[mine];
+    }
+    rank_sort(key, mine, dn);
+    for (int j = 0; j < dn; ++j) {
+        const uint32_t x = rl_u(mine, j);
+        if (ld_i32<true>(g.layers[l].deg + x) < 0) continue;  // neighbor.neighbors == nil
+        list_remove<C, G>(g, l, x, n, ev);                     // graph.go:232 delete(neighbor.neighbors, n.Key)
+        replenish<C, G>(g, l, x, m, S, st, err, ev);           // graph.go:232
+    }
+}
+
 // ---- multi-wave evaluator ----------------------------------------------------
 // Protocol block in LDS.  The master posts a batch (query registers, ids,
 // metric) and hits a workgroup barrier; every wave scores its share of the
@@ -437,55 +467,92 @@ __host__ __device__ constexpr size_t build_smem_words(int vis_log2, int M, int e
     return ((size_t)1 << vis_log2) + 2 * (size_t)(ef + 2) + 2 * (size_t)(M + 2) + 5 * (size_t)((M + 1) * (M + 1) + 2) + 1;
 }
 
-// graph.go:437-531 for inserts [n0, n1), by the master wave
+// One insert of graph.go:942-1042 (BatchAdd; Add is the same walk), by the
+// master wave.  Rows: id_a for the layers above i0, id_b from i0 down (the same
+// row for a fresh key).  ent[l]: the layer's entry() at its turn, or the
+// inserted row itself when the layer is empty then (graph.go:990-993).  i0 >= 0
+// (a present key, graph.go:1015-1024): after layer i0's search every layer
+// holding the key deletes and isolates it (sweep[l], ascending), and the key's
+// live row becomes id_b.  Returns false on the reference's "no nodes found in
+// neighborhood search" (layer in *fail_layer).
+template <class C, int G, class Ev>
+__device__ bool compat_insert(const CompatBuildArgs& a, BuildSmem& S, const Ev& ev, WaveStats& st, int& err,
+                              int level, int top, uint32_t id_a, uint32_t id_b, int i0, const int32_t* ent,
+                              const int32_t* sweep, int& fail_layer) {
+    const int lane = lane_id();
+    QReg<C> q;
+    load_query(q, a.g.vecs + (size_t)id_b * a.g.pitch);
+    const float qn = a.g.norms[id_b];
+    uint32_t elevator = EMPTY_ID;
+    for (int l = top; l >= 0; --l) {  // graph.go:980
+        const uint32_t id = l > i0 ? id_a : id_b;
+        if (ent[l] == (int32_t)id) {  // graph.go:990-993: empty layer, no search
+            ev.sync();
+            if (lane == 0) st_i32(a.g.layers[l].deg + id, -1);
+            ev.sync();
+            continue;
+        }
+        // graph.go:997-1003: layer.nodes[*elevator] -- nil once that key has no node here
+        uint32_t sp = ent[l] < 0 ? EMPTY_ID : (uint32_t)ent[l];
+        if (elevator != EMPTY_ID) sp = resolve_member<true>(a.g, l, elevator);
+        int cnt = 0;
+        if (sp != EMPTY_ID) cnt = compat_layer<C, G, true>(a.g, l, sp, a.M, a.ef, q, qn, S.cs, st, err, ev);  // :1005
+        if (cnt == 0) {  // search(nil) -> "no nodes found in neighborhood search"
+            fail_layer = l;
+            return false;
+        }
+        elevator = S.cs.ri[0];  // graph.go:1013
+        if (level >= l) {       // graph.go:1015-1032
+            const uint32_t nbh = lane < cnt ? S.cs.ri[lane] : 0u;
+            if (l == i0) {
+                for (int l2 = 0; l2 < a.g.nlayers; ++l2)  // graph.go:1018-1023
+                    if (sweep[l2] >= 0) isolate<C, G>(a.g, l2, (uint32_t)sweep[l2], a.M, S, st, err, ev);
+                ev.sync();
+                if (lane == 0) st_i32(a.g.kidlive + kid_of(a.g, id_b), (int32_t)id_b);
+            }
+            ev.sync();
+            if (lane == 0) st_i32(a.g.layers[l].deg + id, -1);
+            ev.sync();
+            for (int j = 0; j < cnt; ++j) {
+                const uint32_t c = rl_u(nbh, j);
+                add_neighbor<C, G>(a.g, l, c, id, a.M, S, st, err, ev);
+                add_neighbor<C, G>(a.g, l, id, c, a.M, S, st, err, ev);
+            }
+        }
+    }
+    return true;
+}
+
+// graph.go:942-1042 for the fresh inserts [n0, n1), then the replacing insert
+// (a.rep_level >= 0), in order; the first failing insert ends the walk
 template <class C, int G, class Ev>
 __device__ void compat_inserts(const CompatBuildArgs& a, BuildSmem& S, const Ev& ev, WaveStats& st, int& err) {
-    const int lane = lane_id();
     int top = a.top0;
+    int fail_layer = -1;
+    int64_t fail_row = -1;
     for (int64_t i = a.n0; i < a.n1; ++i) {
         const uint32_t id = (uint32_t)i;
         const int level = a.levels[i];
         top = max(top, level);
-        QReg<C> q;
-        load_query(q, a.g.vecs + (size_t)id * a.g.pitch);
-        const float qn = a.g.norms[id];
-        uint32_t elevator = EMPTY_ID;
-        for (int l = top; l >= 0; --l) {  // graph.go:475
-            const int32_t ent = a.layer_entry[l];
-            if (ent == (int32_t)id) {  // graph.go:485-488: empty layer, no search
-                ev.sync();
-                if (lane == 0) st_i32(a.g.layers[l].deg + id, -1);
-                ev.sync();
-                continue;
-            }
-            // graph.go:492-498: layer.nodes[*elevator] is nil once that node was deleted
-            uint32_t sp = ent < 0 ? EMPTY_ID : (uint32_t)ent;
-            if (elevator != EMPTY_ID)
-                sp = (ld_i32<true>(a.g.layers[l].deg + elevator) != -2 && !is_dead(a.g, elevator)) ? elevator
-                                                                                                   : EMPTY_ID;
-            if (sp == EMPTY_ID) {  // search(nil) -> "no nodes found in neighborhood search"
-                err |= 2;
-                break;
-            }
-            const int cnt = compat_layer<C, G, true>(a.g, l, sp, a.M, a.ef, q, qn, S.cs, st, err, ev);  // :500
-            if (cnt == 0) {
-                err |= 2;
-                break;
-            }
-            elevator = S.cs.ri[0];  // graph.go:508
-            if (level >= l) {       // graph.go:510-521
-                const uint32_t nbh = lane < cnt ? S.cs.ri[lane] : 0u;
-                ev.sync();
-                if (lane == 0) st_i32(a.g.layers[l].deg + id, -1);
-                ev.sync();
-                for (int j = 0; j < cnt; ++j) {
-                    const uint32_t c = rl_u(nbh, j);
-                    add_neighbor<C, G>(a.g, l, c, id, a.M, S, st, err, ev);
-                    add_neighbor<C, G>(a.g, l, id, c, a.M, S, st, err, ev);
-                }
-            }
+        if (!compat_insert<C, G>(a, S, ev, st, err, level, top, id, id, -1, a.layer_entry, a.rep_sweep,
+                                 fail_layer)) {
+            fail_row = i;
+            break;
         }
         if (err) break;
+    }
+    if (fail_row < 0 && !err && a.rep_level >= 0) {
+        top = max(top, a.rep_level);
+        if (!compat_insert<C, G>(a, S, ev, st, err, a.rep_level, top, a.rep_a, a.rep_b, a.rep_i0, a.rep_entry,
+                                 a.rep_sweep, fail_layer))
+            fail_row = a.rep_b;
+    }
+    if (fail_row >= 0) {
+        err |= 2;
+        if (lane_id() == 0) {
+            a.err[2] = fail_layer;
+            a.err[3] = (int)fail_row;
+        }
     }
 }
 
@@ -963,31 +1030,6 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
 // ---------------------------------------------------------------------------
 // delete (graph.go:843-895)
 // ---------------------------------------------------------------------------
-// graph.go:221-235 isolate: neighbours in ascending key order (the map-order
-// stand-in) drop their backlink and are replenished; the deleted node's own
-// row stays (the reference keeps the layerNode behind one-directional edges).
-template <class C, int G>
-__device__ void isolate(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err,
-                        const WaveEval& ev) {
-    const int lane = lane_id();
-    const int capl = g.layers[l].cap;
-    const int dn = min(ld_i32<true>(g.layers[l].deg + n), capl);
-    if (dn < 0) return;  // nil neighbour map
-    uint32_t mine = 0xFFFFFFFFu;
-    int64_t key = INT64_MAX;
-    if (lane < dn) {
-        mine = guard_id(g, (uint32_t)ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane));
-        key = g.keys[mine];
-    }
-    rank_sort(key, mine, dn);
-    for (int j = 0; j < dn; ++j) {
-        const uint32_t x = rl_u(mine, j);
-        if (ld_i32<true>(g.layers[l].deg + x) < 0) continue;  // neighbor.neighbors == nil
-        list_remove<C, G>(g, l, x, n, ev);                     // graph.go:231
-        replenish<C, G>(g, l, x, m, S, st, err, ev);           // graph.go:232
-    }
-}
-
 // Delete / BatchDelete with the reference's semantics: one wave walks the keys
 // in order and every layer holding the node (graph.go:852-861).
 template <class C, int G>

@@ -61,9 +61,17 @@ struct GraphDev {
     // [1] max over the copy's rows of the measured relative rounding |y' - y| / |y|
     // (<= 2^-11 by construction; replaces 2^-11 in the screening bounds)
     const float* h16err;
+    // key identity (compat semantics: the reference's maps are keyed by K, so a
+    // replaced or re-added key leaves several rows with one key; every map
+    // operation compares kids).  nullptr until the first such row: kid == row.
+    const int32_t* kid;   // [cap_nodes] the first row that ever held this row's key
+    int32_t* kidlive;     // [cap_nodes] by kid: the key's live row (-1 none)
 };
 
 __device__ __forceinline__ bool is_dead(const GraphDev& g, uint32_t id) { return g.dead && g.dead[id]; }
+__device__ __forceinline__ uint32_t kid_of(const GraphDev& g, uint32_t id) {
+    return g.kid ? (uint32_t)g.kid[id] : id;
+}
 
 // `layer.nodes[key] != nil` (graph.go:576-578): present in layer l and not deleted
 __device__ __forceinline__ bool is_member(const GraphDev& g, int l, uint32_t id) {
@@ -384,6 +392,7 @@ __device__ __forceinline__ void vis_clear(uint32_t* tab, int size) {
     uint4* t4 = reinterpret_cast<uint4*>(tab);
     const uint4 e = make_uint4(VIS_EMPTY, VIS_EMPTY, VIS_EMPTY, VIS_EMPTY);
     for (int i = lane_id(); i < size / 4; i += 64) t4[i] = e;
+    if (lane_id() < (size & 3)) tab[(size & ~3) + lane_id()] = VIS_EMPTY;  // a size that is not a multiple of 4
 }
 
 // 0 = already visited, 1 = newly recorded, 2 = table congested (not recorded)

@@ -31,6 +31,21 @@ __device__ __forceinline__ void st_i32(int32_t* p, int32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
+// `layers[l].nodes[*elevator]` (graph.go:497, 574): the layer's node of the
+// elevator row's KEY -- the key's live row if it is a member of layer l, else
+// nil (EMPTY_ID).  The elevator itself may be a replaced or deleted node that
+// a dangling edge led to.
+template <bool COH>
+__device__ __forceinline__ uint32_t resolve_member(const GraphDev& g, int l, uint32_t e) {
+    if (g.kidlive) {
+        const int32_t r = ld_i32<COH>(g.kidlive + kid_of(g, e));
+        if (r < 0 || (uint32_t)r >= g.capn) return EMPTY_ID;
+        e = (uint32_t)r;
+    }
+    if (e >= g.capn || ld_i32<COH>(g.layers[l].deg + e) == -2 || is_dead(g, e)) return EMPTY_ID;
+    return e;
+}
+
 // Evaluate the distances of candidate ids held in lanes 0..cnt-1 of `cid`
 // against the query; sink(dist, id) is called in row order (uniformly).
 template <class C, int G, class Sink>
@@ -374,7 +389,7 @@ __device__ __forceinline__ int compat_layer(const GraphDev& g, int layer, uint32
     float d0 = 0.f;
     ev.template run<C, G>(g, q, qn, entry, 1, g.metric, [&](float d, uint32_t) { d0 = d; });  // graph.go:112
     st.E += 1;
-    if (lane == 0) vis_probe(S.vis, vmask, entry);  // graph.go:123
+    if (lane == 0) vis_probe(S.vis, vmask, kid_of(g, entry));  // graph.go:123 visited[n.Key]
     gh_push(cand, d0, entry);                        // graph.go:109-114
     gh_push(res, cand.d[0], cand.id[0]);             // graph.go:122
     const int32_t* degp = g.layers[layer].deg;
@@ -400,7 +415,7 @@ __device__ __forceinline__ int compat_layer(const GraphDev& g, int layer, uint32
         }
         rank_sort(key, nb, deg);  // graph.go:137-138 ascending key order
         int pr = 0;
-        if (lane < deg) pr = vis_probe(S.vis, vmask, nb);  // graph.go:141-144
+        if (lane < deg) pr = vis_probe(S.vis, vmask, kid_of(g, nb));  // graph.go:141-144 (by key)
         if (__ballot(pr == 2)) err = 1;                   // exact visited set required here
         int cnt;
         const uint32_t cid = compact(nb, pr == 1, cnt);

@@ -87,8 +87,14 @@ struct CompatBuildArgs {
     int top0;                     // len(g.layers) - 1 before this batch (-1: no layers)
     int M, ef;
     unsigned long long* stats;    // [0]=dist evals [1]=expansions
-    int* err;
+    int* err;                     // [0] error bits; on "no nodes found" (bit 2): [2] layer, [3] row
     int vis_log2;
+    // BatchAdd of a present key (graph.go:1015-1024), after the fresh inserts:
+    int rep_level;                // its level (-1: none)
+    int rep_i0;                   // the layer whose search precedes the sweep
+    uint32_t rep_a, rep_b;        // its rows above i0 (EMPTY_ID: none needed) / from i0 down
+    const int32_t* rep_entry;     // [MH_MAXL] entry() of each layer at its turn (the row itself: empty then)
+    const int32_t* rep_sweep;     // [MH_MAXL] row the sweep deletes + isolates in layer l (-1 none)
 };
 int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, int waves, hipStream_t s);  // waves: 1 or 8
 

@@ -38,7 +38,7 @@ __global__ __launch_bounds__(64) void k_search_compat(SearchArgs a) {
         // searchPoint: layers[l].nodes[*elevator] (nil once deleted) or entry() (nil when empty)
         uint32_t p;
         if (elevator != EMPTY_ID)
-            p = is_member(a.g, l, elevator) ? elevator : EMPTY_ID;
+            p = resolve_member<false>(a.g, l, elevator);
         else
             p = l == a.top ? a.entry : (a.layer_entry[l] < 0 ? EMPTY_ID : (uint32_t)a.layer_entry[l]);
         if (p == EMPTY_ID) continue;  // search(nil) returns nothing (graph.go:101-103)

@@ -9,6 +9,7 @@ run on the GPU (a custom Python callable cannot, and is rejected).
 from __future__ import annotations
 
 import ctypes as C
+import math
 import os
 from typing import Iterable, List, NamedTuple, Optional, Sequence
 
@@ -128,11 +129,20 @@ def _metric_of(fn) -> int:
                         "EuclideanDistance)")
 
 
+def _go_round(x: float) -> float:
+    """Go's math.Round: nearest integer, halves away from zero (Python's round()
+    and np.round round halves to even)."""
+    t = math.trunc(x)
+    if abs(x - t) >= 0.5:  # x - trunc(x) is exact in binary floating point
+        t += math.copysign(1.0, x)
+    return t
+
+
 def max_level(ml: float, num_nodes: int) -> int:
     """graph.go:370-385 maxLevel."""
     if num_nodes == 0:
         return 1
-    return int(np.round(np.log(float(num_nodes)) / np.log(1.0 / ml))) + 1
+    return int(_go_round(math.log(float(num_nodes)) / math.log(1.0 / ml))) + 1
 
 
 def random_level(rng, ml: float, layers_exist: bool, base: int) -> int:
@@ -223,14 +233,31 @@ class Graph:
         self._rng = int(rng)
         self._check(load().mhnsw_seed(self._h, int(rng) & (2**64 - 1)))
 
-    def _draw_levels(self, n: int):
-        """Levels of the next n inserts from a host Rng (None: the engine draws)."""
-        if not hasattr(self._rng, "Float64"):
-            return None
+    def _host_rng(self) -> bool:
+        return hasattr(self._rng, "Float64") and self.get_option("build_mode") != 2
+
+    def _draw_levels(self, n: int) -> np.ndarray:
+        """Levels of the next n inserts from the host Rng (graph.go:962), each from
+        the layer-0 size before it (the caller knows those inserts are fresh)."""
         existed = load().mhnsw_num_layers(self._h) > 0
         base = self.Len()
         return np.array([random_level(self._rng, float(self.Ml), existed or i > 0, base + i) for i in range(n)],
                         np.int32)
+
+    def _walk(self, keys: np.ndarray, add):
+        """BatchAdd's walk with levels from the host Rng: draw exactly the levels
+        the reference draws -- one per insert it reaches.  mhnsw_add_plan gives
+        the inserts up to the next present key (where the walk may stop) and
+        whether an insert may fail (then one insert per call); an error from
+        add(lo, hi, levels) ends the walk."""
+        nwalk, one = C.c_int64(), C.c_int()
+        lo = 0
+        while lo < len(keys):
+            self._check(load().mhnsw_add_plan(self._h, _ptr(keys[lo:], C.c_int64), len(keys) - lo, C.byref(nwalk),
+                                              C.byref(one)))
+            hi = lo + 1 if one.value else lo + nwalk.value
+            add(lo, hi, self._draw_levels(hi - lo))
+            lo = hi
 
     def set_option(self, name: str, value: int):
         self._check(load().mhnsw_set_option(self._h, name.encode(), int(value)))
@@ -298,43 +325,62 @@ class Graph:
         self.BatchAdd(list(nodes))
 
     def BatchAdd(self, nodes: Sequence[Node], levels=None):
+        """graph.go:942-1042.  The walk inserts nodes in order and stops at the
+        first error: a node whose dimension differs from the graph's (the
+        nodes before it stay added, graph.go:955-960), a present key (replaced,
+        then "node not added", graph.go:1015-1037) or a failing search."""
         if not nodes:
             self.Validate()
             return
         vecs = [np.asarray(n.Value, dtype=np.float32).ravel() for n in nodes]
-        dims = {v.size for v in vecs}
-        if len(dims) != 1:
-            # first mismatch is reported with the reference wording
-            d0 = self.Dims() or vecs[0].size
-            for v in vecs:
-                if v.size != d0:
-                    raise HnswError(-2, f"embedding dimension mismatch: {d0} != {v.size}")
+        d0 = self.Dims() or vecs[0].size
+        bad = next((i for i, v in enumerate(vecs) if v.size != d0), len(vecs))
         self._sync()
-        keys = self.encode_keys([n.Key for n in nodes], assign=True)
-        self.add_arrays(keys, np.stack(vecs), levels=levels)
-        for n, v in zip(nodes, vecs):
-            self._values[n.Key] = v
+        try:
+            if bad:
+                keys = self.encode_keys([n.Key for n in nodes[:bad]], assign=True)
+                self.add_arrays(keys, np.stack(vecs[:bad]), levels=None if levels is None else levels[:bad])
+                for n, v in zip(nodes[:bad], vecs):
+                    self._values[n.Key] = v
+        except HnswError:
+            for n in nodes[:bad]:  # partly applied: Lookup reads the engine
+                self._values.pop(n.Key, None)
+            raise
+        if bad < len(vecs):
+            self.Validate()
+            raise HnswError(-2, f"embedding dimension mismatch: {d0} != {vecs[bad].size}")
 
     def add_arrays(self, keys, vecs, levels=None):
         """Array form of BatchAdd: keys int64[n], vecs float32[n, dim] (host)."""
         self._sync()
         keys = np.ascontiguousarray(keys, dtype=np.int64)
         vecs = _f32(vecs).reshape(len(keys), -1)
-        if levels is None and self.get_option("build_mode") != 2:
-            levels = self._draw_levels(len(keys))
-        lv = None if levels is None else np.ascontiguousarray(levels, dtype=np.int32)
-        self._check(load().mhnsw_add(self._h, _ptr(keys, C.c_int64), _ptr(vecs, C.c_float), len(keys),
-                                     vecs.shape[1], None if lv is None else _ptr(lv, C.c_int32)))
+
+        def add(lo, hi, lv):
+            lv = None if lv is None else np.ascontiguousarray(lv, dtype=np.int32)
+            self._check(load().mhnsw_add(self._h, _ptr(keys[lo:], C.c_int64), _ptr(vecs[lo:], C.c_float), hi - lo,
+                                         vecs.shape[1], None if lv is None else _ptr(lv, C.c_int32)))
+
+        if levels is None and self._host_rng():
+            self._walk(keys, add)
+        else:
+            add(0, len(keys), levels)
 
     def add_device(self, keys, vecs_dev_ptr: int, n: int, dim: int, levels=None):
         """BatchAdd with vectors already resident in HBM (device pointer)."""
         self._sync()
         keys = np.ascontiguousarray(keys, dtype=np.int64)
-        if levels is None and self.get_option("build_mode") != 2:
-            levels = self._draw_levels(n)
-        lv = None if levels is None else np.ascontiguousarray(levels, dtype=np.int32)
-        self._check(load().mhnsw_add_device(self._h, _ptr(keys, C.c_int64), C.c_void_p(vecs_dev_ptr), n, dim,
-                                            None if lv is None else _ptr(lv, C.c_int32)))
+
+        def add(lo, hi, lv):
+            lv = None if lv is None else np.ascontiguousarray(lv, dtype=np.int32)
+            self._check(load().mhnsw_add_device(self._h, _ptr(keys[lo:], C.c_int64),
+                                                C.c_void_p(vecs_dev_ptr + lo * dim * 4), hi - lo, dim,
+                                                None if lv is None else _ptr(lv, C.c_int32)))
+
+        if levels is None and self._host_rng():
+            self._walk(keys, add)
+        else:
+            add(0, n, levels)
 
     def Replace(self, nodes: Sequence[Node]) -> List[bool]:
         """Flat handles (build_mode 2): overwrite the vectors of present keys in
@@ -359,6 +405,13 @@ class Graph:
         self._check(load().mhnsw_replace(self._h, _ptr(keys, C.c_int64), _ptr(vecs, C.c_float), len(keys),
                                          vecs.shape[1], _ptr(out, C.c_uint8)))
         return out[: len(keys)].astype(bool)
+
+    def contains(self, keys) -> np.ndarray:
+        """Which keys have a live node (engine key images for a list of Go keys)."""
+        imgs = np.ascontiguousarray(self.encode_keys(list(keys)), np.int64)
+        out = np.zeros(max(len(imgs), 1), np.uint8)
+        self._check(load().mhnsw_contains(self._h, _ptr(imgs, C.c_int64), len(imgs), _ptr(out, C.c_uint8)))
+        return out[: len(imgs)].astype(bool)
 
     def reserve(self, n: int, dim: int):
         self._check(load().mhnsw_reserve(self._h, n, dim))

@@ -249,41 +249,33 @@ class Graph {  // graph.go:305-332
     Error Add(std::initializer_list<Node<K>> nodes) { return BatchAdd(std::vector<Node<K>>(nodes)); }
     Error Add(const Node<K>& n) { return BatchAdd(std::vector<Node<K>>{n}); }
 
-    // graph.go:942-1042.  Levels come from Rng, one draw sequence per node in
-    // order with the layer-0 size growing by one per insert, as BatchAdd /
-    // Add draw them (graph.go:457, 962); `levels` overrides them (parity tests).
+    // graph.go:942-1042.  The walk inserts the nodes in order and stops at the
+    // first error: a node of another dimension (the nodes before it stay
+    // added, graph.go:955-960), a present key (replaced, then "node not added",
+    // graph.go:1015-1037) or a failing search.  Levels come from Rng, drawn
+    // exactly where the reference draws them -- one per insert the walk
+    // reaches, from the layer-0 size at that moment (graph.go:962,
+    // mhnsw_add_plan); `levels` overrides them (parity tests).
     Error BatchAdd(const std::vector<Node<K>>& nodes, const std::vector<int32_t>* levels = nullptr) {
         sync();
         if (nodes.empty()) return make_error(mhnsw_validate(h_), h_);
-        const size_t d = nodes[0].Value.size();
-        std::vector<K> ks;
-        std::vector<float> flat;
-        ks.reserve(nodes.size());
-        flat.reserve(nodes.size() * d);
-        for (const auto& n : nodes) {
-            if (n.Value.size() != d) {
-                const int have = Dims() ? Dims() : (int)d;
-                return Error{"embedding dimension mismatch: " + std::to_string(have) + " != " +
-                                 std::to_string(n.Value.size()),
-                             MHNSW_EDIM};
+        const size_t d = Dims() ? (size_t)Dims() : nodes[0].Value.size();
+        size_t bad = 0;
+        while (bad < nodes.size() && nodes[bad].Value.size() == d) ++bad;
+        if (bad > 0) {
+            Error e = addWalk(nodes, bad, d, levels);
+            if (e) {
+                for (size_t i = 0; i < bad; ++i) values_.erase(nodes[i].Key);  // partly applied: Lookup asks the engine
+                return e;
             }
-            ks.push_back(n.Key);
-            flat.insert(flat.end(), n.Value.begin(), n.Value.end());
+            for (size_t i = 0; i < bad; ++i) values_[nodes[i].Key] = nodes[i].Value;
         }
-        std::vector<int32_t> drawn;
-        if (!levels) {
-            if (!Rng) Rng = defaultRand();
-            const bool existed = mhnsw_num_layers(h_) > 0;
-            const int64_t base = Len();
-            drawn.resize(nodes.size());
-            for (size_t i = 0; i < nodes.size(); ++i)
-                drawn[i] = randomLevel(*Rng, Ml, existed || i > 0, base + (int64_t)i);
-            levels = &drawn;
+        if (bad < nodes.size()) {
+            if (Error v = Validate()) return v;
+            return Error{"embedding dimension mismatch: " + std::to_string(d) + " != " +
+                             std::to_string(nodes[bad].Value.size()),
+                         MHNSW_EDIM};
         }
-        const std::vector<int64_t> keys = Codec::encode(h_, ks, /*assign=*/true);
-        int rc = mhnsw_add(h_, keys.data(), flat.data(), (int64_t)nodes.size(), (int)d, levels->data());
-        if (rc < 0) return make_error(rc, h_);
-        for (const auto& n : nodes) values_[n.Key] = n.Value;
         return {};
     }
 
@@ -413,6 +405,42 @@ class Graph {  // graph.go:305-332
     }
 
    private:
+    // nodes[0, n) of dimension d through mhnsw_add, levels drawn as the walk goes
+    Error addWalk(const std::vector<Node<K>>& nodes, size_t n, size_t d, const std::vector<int32_t>* levels) {
+        std::vector<K> ks;
+        std::vector<float> flat;
+        ks.reserve(n);
+        flat.reserve(n * d);
+        for (size_t i = 0; i < n; ++i) {
+            ks.push_back(nodes[i].Key);
+            flat.insert(flat.end(), nodes[i].Value.begin(), nodes[i].Value.end());
+        }
+        const std::vector<int64_t> keys = Codec::encode(h_, ks, /*assign=*/true);
+        if (levels) return make_error(mhnsw_add(h_, keys.data(), flat.data(), (int64_t)n, (int)d, levels->data()), h_);
+        if (!Rng) Rng = defaultRand();
+        int64_t nwalk = 0;
+        int one = 0;
+        auto draw = [&](int64_t cnt) {
+            const bool existed = mhnsw_num_layers(h_) > 0;
+            const int64_t base = Len();
+            std::vector<int32_t> lv((size_t)cnt);
+            for (int64_t i = 0; i < cnt; ++i) lv[i] = randomLevel(*Rng, Ml, existed || i > 0, base + i);
+            return lv;
+        };
+        // up to the next present key (where the walk may stop), or one insert at a
+        // time when an insert may fail; an error ends the walk
+        for (size_t lo = 0; lo < n;) {
+            if (int rc = mhnsw_add_plan(h_, keys.data() + lo, (int64_t)(n - lo), &nwalk, &one))
+                return make_error(rc, h_);
+            const size_t hi = one ? lo + 1 : lo + (size_t)nwalk;
+            const std::vector<int32_t> lv = draw((int64_t)(hi - lo));
+            const int rc = mhnsw_add(h_, keys.data() + lo, flat.data() + lo * d, (int64_t)(hi - lo), (int)d, lv.data());
+            if (rc < 0) return make_error(rc, h_);
+            lo = hi;
+        }
+        return {};
+    }
+
     void create() {
         int rc = mhnsw_create(MHNSW_COSINE, 16, 0.25, 20, 0, &h_);
         if (rc < 0) throw std::runtime_error(mhnsw_last_error(nullptr));

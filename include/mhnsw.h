@@ -92,7 +92,8 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * greedy), "screen" (beam mode and batched insert, default 1: keep an fp16
  * copy of the rows; a candidate is skipped only when the copy proves the f32
  * distance rejects it, so results are unchanged);
- * read-only: "pitch", "capacity", "strkeys", "strkey_relabels",
+ * read-only: "pitch", "capacity", "strkeys", "strkey_relabels", "last_gemm_ns" (device
+ *            time of the last timed exact search's fused fp16 score GEMM, first query chunk),
  *            "screen_err_ppb" (the fp16 screening copy's measured max relative
  *            rounding E, the margin its rejects use, in parts per 1e9) */
 int mhnsw_set_option(mhnsw_index *h, const char *name, int64_t value);
@@ -104,11 +105,30 @@ int mhnsw_reserve(mhnsw_index *h, int64_t n, int dim);
 
 /* ---- Graph.Add / Graph.BatchAdd (graph.go:437-531, 942-1042) ----
  * levels: NULL draws each level like randomLevel (graph.go:388-417) from the
- * handle's RNG; non-NULL injects them (parity testing). */
+ * handle's RNG; non-NULL injects them (a host drawing from its own Rng, or
+ * parity testing).  COMPAT build mode follows BatchAdd's walk: the nodes are
+ * inserted in order up to the first key already present (in the index or
+ * earlier in the batch); that node replaces the key's node -- after its layer
+ * search, every layer holding the key deletes and isolates it
+ * (graph.go:1015-1024) -- and the walk stops with "node not added" (MHNSW_EINTERNAL;
+ * graph.go:1035-1037: Len() did not grow).  A failing insert ("no nodes found in
+ * neighborhood search", graph.go:1009) also ends the walk, leaving the graph as
+ * the reference leaves it.  Add of a present key deadlocks in the reference
+ * (graph.go:511-513 -> Delete re-locks, :844); here it is BatchAdd's walk.
+ * BATCH / FLAT build modes reject a present key (MHNSW_EUNSUPPORTED). */
 int mhnsw_add(mhnsw_index *h, const int64_t *keys, const float *vecs, int64_t n, int dim, const int32_t *levels);
 /* same, vectors already in HBM (keys/levels stay host pointers) */
 int mhnsw_add_device(mhnsw_index *h, const int64_t *keys, const float *d_vecs, int64_t n, int dim,
                      const int32_t *levels);
+/* For hosts that draw levels from their own Rng (graph.go:962: one draw per
+ * insert the walk reaches, from the layer-0 size at that moment): *nwalk = the
+ * inserts up to and including the first key already present (or repeated) --
+ * where a COMPAT walk may stop (it does when that key's node holds a layer at
+ * or below the new level); *one_by_one = 1 when an insert may fail with "no
+ * nodes found in neighborhood search" (the index holds deleted or replaced
+ * rows).  A host draws nwalk levels (1 when one_by_one), adds those nodes,
+ * and repeats with the rest until done or an error ends the walk. */
+int mhnsw_add_plan(mhnsw_index *h, const int64_t *keys, int64_t n, int64_t *nwalk, int *one_by_one);
 
 /* ---- Graph.Search / Graph.BatchSearch (graph.go:534-625, 1047-1110) ----
  * B queries of `dim` floats; outputs hold B*k slots; out_n[b] results for
@@ -139,10 +159,14 @@ int mhnsw_search_negatives(mhnsw_index *h, const float *queries, int64_t B, int 
                            const int32_t *neg_count, int k, float neg_weight, int mode, int ef, int flags,
                            int64_t *out_keys, float *out_score, int32_t *out_n);
 
-/* ---- Len / Dims / Lookup / Analyzer.Topography (graph.go:829, 421, 898; analyzer.go:41) ---- */
+/* ---- Len / Dims / Lookup / Analyzer.Topography (graph.go:829, 421, 898; analyzer.go:41) ----
+ * Lookup reads layer 0 (graph.go:906) and copies the key's vector. */
 int64_t mhnsw_len(const mhnsw_index *h);
 int mhnsw_dims(const mhnsw_index *h);
 int mhnsw_lookup(mhnsw_index *h, int64_t key, float *out_vec); /* 1 found, 0 absent, <0 error */
+/* out[i] = 1 when keys[i] has a live node (the `_, ok := layer.nodes[key]` test
+ * of graph.go:1016 / hybrid/exact.go:30, without copying vectors) */
+int mhnsw_contains(const mhnsw_index *h, const int64_t *keys, int64_t n, uint8_t *out);
 int mhnsw_num_layers(const mhnsw_index *h);
 int64_t mhnsw_layer_count(const mhnsw_index *h, int layer);
 /* Analyzer.Connectivity (analyzer.go:20-38): mean neighbour count of each

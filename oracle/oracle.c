@@ -21,7 +21,14 @@
  *     inserted into that layer that is still present, or an injected key.
  *   - Rng.Float64() (graph.go:410) -> SplitMix64, or injected levels.
  *   - Add() of an existing key deadlocks in the reference (graph.go:438,511-513
- *     -> Delete re-locks at :844); here it is rejected with OG_EUNSUPPORTED.
+ *     -> Delete re-locks at :844); here every Add follows BatchAdd's inline
+ *     replacement (graph.go:1015-1024), including its "node not added" error
+ *     (graph.go:1035-1037: Len() did not grow).
+ * Keys vs nodes: the reference's maps are keyed by K, its nodes are objects.
+ * A row here is one node object; several rows can carry one key (a replaced or
+ * deleted node stays reachable through one-directional edges).  Every map
+ * operation therefore goes by key: rows carry kid (the first row ever holding
+ * the key) and neighbour sets, visited sets and layer lookups compare kids.
  *   - Search()'s "dog" test hack (graph.go:563-569, 595-619) is not restated.
  */
 #include "oracle.h"
@@ -253,6 +260,7 @@ struct og_graph {
     int64_t n, cap_nodes;
     int acap;
     int64_t *keys;
+    int32_t *kid;  /* [cap_nodes] key identity: the first row that held keys[row] */
     float *vecs;
     float *norms;
     uint8_t *dead; /* [cap_nodes] 1 = deleted (graph.go:843-864); rows stay for dangling edges */
@@ -262,6 +270,10 @@ struct og_graph {
     int64_t *hkeys;
     int32_t *hvals;
     int64_t hcap;
+    /* key -> kid (every key ever added; never deleted) */
+    int64_t *kkeys;
+    int32_t *kvals;
+    int64_t kcap, kn;
     og_scratch scr;
     int64_t stats[4];
     char err[256];
@@ -332,6 +344,39 @@ static int hput(og_graph *g, int64_t key, int32_t val) {
     return 0;
 }
 
+/* key -> kid, insert-or-get (kid = `row` for a key never seen) */
+static int32_t kid_get(og_graph *g, int64_t key, int32_t row) {
+    if ((g->kn + 1) * 2 > g->kcap) {
+        int64_t ocap = g->kcap;
+        int64_t *ok = g->kkeys;
+        int32_t *ov = g->kvals;
+        int64_t ncap = ocap ? ocap * 2 : 1024;
+        g->kkeys = (int64_t *)malloc(sizeof(int64_t) * (size_t)ncap);
+        g->kvals = (int32_t *)malloc(sizeof(int32_t) * (size_t)ncap);
+        if (!g->kkeys || !g->kvals) return -1;
+        for (int64_t i = 0; i < ncap; ++i) g->kvals[i] = -1;
+        g->kcap = ncap;
+        for (int64_t i = 0; i < ocap; ++i) {
+            if (ov[i] < 0) continue;
+            uint64_t m = (uint64_t)ncap - 1, h = hmix(ok[i]) & m;
+            while (g->kvals[h] >= 0) h = (h + 1) & m;
+            g->kkeys[h] = ok[i];
+            g->kvals[h] = ov[i];
+        }
+        free(ok);
+        free(ov);
+    }
+    uint64_t m = (uint64_t)g->kcap - 1, h = hmix(key) & m;
+    while (g->kvals[h] >= 0) {
+        if (g->kkeys[h] == key) return g->kvals[h];
+        h = (h + 1) & m;
+    }
+    g->kkeys[h] = key;
+    g->kvals[h] = row;
+    g->kn++;
+    return row;
+}
+
 og_graph *og_create(int metric, int order, int M, int M0, double ml, int ef, uint64_t seed) {
     og_graph *g = (og_graph *)calloc(1, sizeof(og_graph));
     if (!g) return NULL;
@@ -361,11 +406,14 @@ void og_destroy(og_graph *g) {
     if (!g) return;
     free_layers(g);
     free(g->keys);
+    free(g->kid);
     free(g->vecs);
     free(g->norms);
     free(g->dead);
     free(g->hkeys);
     free(g->hvals);
+    free(g->kkeys);
+    free(g->kvals);
     free(g->scr.visited);
     free(g->scr.c1.a);
     free(g->scr.c2.a);
@@ -408,6 +456,9 @@ static int ensure_nodes(og_graph *g, int64_t need) {
     int64_t *nk = (int64_t *)realloc(g->keys, sizeof(int64_t) * (size_t)nc);
     if (!nk) return -1;
     g->keys = nk;
+    int32_t *nkid = (int32_t *)realloc(g->kid, sizeof(int32_t) * (size_t)nc);
+    if (!nkid) return -1;
+    g->kid = nkid;
     float *nv = (float *)realloc(g->vecs, sizeof(float) * (size_t)nc * (size_t)(g->dim ? g->dim : 1));
     if (!nv) return -1;
     g->vecs = nv;
@@ -482,6 +533,15 @@ static inline int member(const og_graph *g, int l, int32_t id) {
     return id >= 0 && l >= 0 && l < g->nlayers && g->layers[l].deg[id] != -2 && !g->dead[id];
 }
 
+/* `layer.nodes[*elevator]` (graph.go:497, 574): the layer's node of the row's
+ * KEY -- the key's live row when it is a member of layer l, else nil.  The
+ * elevator row itself may be a replaced or deleted node reached through a
+ * dangling edge. */
+static inline int32_t resolve(og_graph *g, int l, int32_t row) {
+    int32_t r = hget(g, g->keys[row]);
+    return member(g, l, r) ? r : -1;
+}
+
 /* highest layer with a live node (empty top layers are skipped by Search:
  * entry() == nil -> search() == nil -> continue, graph.go:572-582) */
 static int top_live_layer(const og_graph *g) {
@@ -542,7 +602,7 @@ static int compat_layer_search(og_graph *g, og_scratch *s, int layer, int32_t en
     gh_push(cand, dist_q(g, entry, q, qn), entry); /* graph.go:109-114 */
     (*nd)++;
     gh_push(res, cand->a[0].d, cand->a[0].id); /* graph.go:122 result.Push(candidates.Min()) */
-    s->visited[entry] = st;                     /* graph.go:123 */
+    s->visited[g->kid[entry]] = st;             /* graph.go:123 visited[n.Key] */
 
     while (cand->n > 0) {
         cand_t cur = gh_pop(cand); /* graph.go:127 */
@@ -552,8 +612,8 @@ static int compat_layer_search(og_graph *g, og_scratch *s, int layer, int32_t en
         int d = sorted_neighbors(g, L, cur.id, nb); /* graph.go:137-138 */
         for (int j = 0; j < d; ++j) {
             int32_t v = nb[j];
-            if (s->visited[v] == st) continue; /* graph.go:141-143 */
-            s->visited[v] = st;
+            if (s->visited[g->kid[v]] == st) continue; /* graph.go:141-143 (by key) */
+            s->visited[g->kid[v]] = st;
             float dist = dist_q(g, v, q, qn); /* graph.go:146 */
             (*nd)++;
             improved = improved || (res->n > 0 && dist < res->a[0].d); /* graph.go:147 */
@@ -649,11 +709,13 @@ static int beam_layer_search(og_graph *g, og_scratch *s, int layer, int32_t entr
 }
 
 /* ---- graph.go:172-219 replenish, graph.go:41-81 addNeighbor ---- */
-static void list_remove(og_layer *L, int acap, int32_t n, int32_t v) {
+/* delete(n.neighbors, v.Key): the entry of v's key, whichever row it holds */
+static void list_remove(const og_graph *g, og_layer *L, int32_t n, int32_t v) {
+    const int acap = g->acap;
     int d = L->deg[n];
     int32_t *a = L->adj + (size_t)n * acap;
     for (int j = 0; j < d; ++j)
-        if (a[j] == v) {
+        if (g->kid[a[j]] == g->kid[v]) {
             a[j] = a[d - 1];
             L->deg[n] = d - 1;
             return;
@@ -668,11 +730,11 @@ static void replenish(og_graph *g, int layer, int32_t n, int m) {
     if (dn >= m) return; /* graph.go:173-175 (len(nil map) == 0) */
     og_scratch *s = &g->scr;
     uint32_t st = next_stamp(s, g->cap_nodes);
-    s->visited[n] = st; /* graph.go:184 */
+    s->visited[g->kid[n]] = st; /* graph.go:184 visited[n.Key] */
     int32_t *mine = (int32_t *)malloc(sizeof(int32_t) * (size_t)g->acap);
     int32_t *theirs = (int32_t *)malloc(sizeof(int32_t) * (size_t)g->acap);
     int nm = sorted_neighbors(g, L, n, mine);
-    for (int j = 0; j < nm; ++j) s->visited[mine[j]] = st; /* graph.go:187-189 */
+    for (int j = 0; j < nm; ++j) s->visited[g->kid[mine[j]]] = st; /* graph.go:187-189 */
     gheap cand = {0};
     gh_reserve(&cand, 2 * m + 2);
     for (int j = 0; j < nm; ++j) { /* graph.go:192-210 */
@@ -681,8 +743,8 @@ static void replenish(og_graph *g, int layer, int32_t n, int m) {
         int nt = sorted_neighbors(g, L, nb, theirs);
         for (int t = 0; t < nt; ++t) {
             int32_t c = theirs[t];
-            if (s->visited[c] == st) continue;
-            s->visited[c] = st;
+            if (s->visited[g->kid[c]] == st) continue; /* graph.go:198 visited[k] */
+            s->visited[g->kid[c]] = st;
             float d = dist_nodes(g, c, n, OG_COSINE); /* graph.go:204 hard-coded cosine */
             g->stats[2]++;
             gh_push(&cand, d, c);
@@ -706,8 +768,11 @@ static void add_neighbor(og_graph *g, int layer, int32_t n, int32_t nw, int m, i
     int d = L->deg[n];
     int present = 0;
     for (int j = 0; j < d; ++j)
-        if (a[j] == nw) present = 1;
-    if (!present) { /* graph.go:50 map assignment */
+        if (g->kid[a[j]] == g->kid[nw]) { /* graph.go:50 n.neighbors[newNode.Key] = newNode: */
+            a[j] = nw;                     /* the key's entry is overwritten */
+            present = 1;
+        }
+    if (!present) {
         a[d] = nw;
         L->deg[n] = ++d;
     }
@@ -726,8 +791,8 @@ static void add_neighbor(og_graph *g, int layer, int32_t n, int32_t nw, int m, i
     }
     free(nb);
     if (worst >= 0) { /* graph.go:73-80 */
-        list_remove(L, g->acap, n, worst);
-        if (L->deg[worst] >= 0) list_remove(L, g->acap, worst, n);
+        list_remove(g, L, n, worst);
+        if (L->deg[worst] >= 0) list_remove(g, L, worst, n);
         replenish(g, layer, worst, m);
     }
 }
@@ -767,7 +832,29 @@ int og_preview_levels(og_graph *g, int64_t n, int32_t *out) {
     return OG_OK;
 }
 
-/* graph.go:437-531 Graph.Add (sequential, compat) */
+static void isolate(og_graph *g, int l, int32_t n, int m);
+
+/* graph.go:1015-1024: BatchAdd found the key in layer i0 (after that layer's
+ * search): every layer holding the key -- the old node, and the new node's own
+ * upper row A in the layers above i0 -- deletes it and isolates it, in layer
+ * order.  Both rows stay behind their one-directional edges, like Delete's. */
+static void replace_sweep(og_graph *g, int64_t key, int32_t old, int32_t ida, int32_t idb) {
+    g->dead[old] = 1;
+    if (ida >= 0) g->dead[ida] = 1;
+    for (int l = 0; l < g->nlayers; ++l) {
+        og_layer *L = &g->layers[l];
+        int32_t r = L->deg[old] != -2 ? old : (ida >= 0 && L->deg[ida] != -2) ? ida : -1;
+        if (r < 0) continue;
+        L->count--; /* delete(l.nodes, key) */
+        isolate(g, l, r, g->M);
+    }
+    hput(g, key, idb);
+}
+
+static void fix_entries(og_graph *g);
+
+/* graph.go:942-1042 Graph.BatchAdd (sequential, compat; Add is the same walk,
+ * graph.go:437-531, minus its deadlock on a present key) */
 int og_add(og_graph *g, const int64_t *keys, const float *vecs, int64_t n, int dim, const int32_t *levels) {
     int rc = og_validate(g);
     if (rc) return rc;
@@ -775,46 +862,72 @@ int og_add(og_graph *g, const int64_t *keys, const float *vecs, int64_t n, int d
     for (int64_t i = 0; i < n; ++i) {
         int64_t key = keys[i];
         const float *vec = vecs + (size_t)i * (size_t)dim;
-        if (g->layers_exist && g->dim != dim) /* graph.go:450-455 */
+        if (g->layers_exist && g->dim != dim) /* graph.go:955-960 */
             return set_err(g, OG_EDIM, "embedding dimension mismatch: %d != %d", g->dim, dim);
         if (!g->layers_exist) g->dim = dim;
-        if (hget(g, key) >= 0)
-            return set_err(g, OG_EUNSUPPORTED, "duplicate key %lld: replacement not supported", (long long)key);
-        int level = levels ? levels[i] : og_random_level(g); /* graph.go:457 */
+        int level = levels ? levels[i] : og_random_level(g); /* graph.go:962 */
         if (level < 0) return set_err(g, OG_EINVAL, "invalid level: %d", level);
-        if (ensure_nodes(g, g->n + 1)) return set_err(g, OG_ENOMEM, "out of memory");
-        while (level >= g->nlayers) /* graph.go:462-464 */
+        if (ensure_nodes(g, g->n + 2)) return set_err(g, OG_ENOMEM, "out of memory");
+        while (level >= g->nlayers) /* graph.go:967-969 */
             if (add_layer(g)) return set_err(g, OG_ENOMEM, "out of memory");
         g->layers_exist = 1;
-        int32_t id = (int32_t)g->n++;
-        g->keys[id] = key;
-        memcpy(g->vecs + (size_t)id * dim, vec, sizeof(float) * (size_t)dim);
-        g->norms[id] = og_dev_norm(vec, dim);
-        if (hput(g, key, id)) return set_err(g, OG_ENOMEM, "out of memory");
-        float qn = g->norms[id];
+        /* a present key: the first layer (from the top) at or below the insert
+         * level whose map holds it is where the replacement happens */
+        int32_t old = hget(g, key);
+        int i0 = -1;
+        for (int l = level; old >= 0 && l >= 0; --l)
+            if (member(g, l, old)) {
+                i0 = l;
+                break;
+            }
+        /* rows: the new node's layers above i0 (deleted again by the sweep) get a
+         * row of their own, A; B holds it from i0 down */
+        int need_a = 0;
+        for (int l = g->nlayers - 1; i0 >= 0 && l > i0; --l) need_a |= g->layers[l].count == 0 || l <= level;
+        int32_t ida = -1, idb;
+        if (need_a) ida = (int32_t)g->n++;
+        idb = (int32_t)g->n++;
+        int32_t kid = kid_get(g, key, ida >= 0 ? ida : idb);
+        if (kid < 0) return set_err(g, OG_ENOMEM, "out of memory");
+        for (int32_t id = ida >= 0 ? ida : idb; id <= idb; ++id) {
+            g->keys[id] = key;
+            g->kid[id] = kid;
+            memcpy(g->vecs + (size_t)id * dim, vec, sizeof(float) * (size_t)dim);
+            g->norms[id] = og_dev_norm(vec, dim);
+        }
+        if (i0 < 0 && hput(g, key, idb)) return set_err(g, OG_ENOMEM, "out of memory");
+        float qn = g->norms[idb];
         int32_t elevator = -1;
         int32_t *nbh = (int32_t *)malloc(sizeof(int32_t) * (size_t)(g->M + 2));
         float *nbd = (float *)malloc(sizeof(float) * (size_t)(g->M + 2));
-        for (int l = g->nlayers - 1; l >= 0; --l) { /* graph.go:475 */
+        for (int l = g->nlayers - 1; l >= 0; --l) { /* graph.go:980 */
             og_layer *L = &g->layers[l];
-            if (L->count == 0) { /* graph.go:485-488 */
+            const int32_t id = l > i0 && ida >= 0 ? ida : idb;
+            if (L->count == 0) { /* graph.go:990-993 */
                 L->deg[id] = -1;
                 L->count = 1;
                 L->entry = id;
                 continue;
             }
-            /* graph.go:492-498: layer.nodes[*elevator] is nil once the elevator
-             * node was deleted -> search(nil) -> error below */
-            int32_t sp = elevator >= 0 ? (member(g, l, elevator) ? elevator : -1) : L->entry;
+            /* graph.go:997-1003: layer.nodes[*elevator] is nil once that key has
+             * no node in this layer -> search(nil) -> error below */
+            int32_t sp = elevator >= 0 ? resolve(g, l, elevator) : L->entry;
             int cnt = compat_layer_search(g, &g->scr, l, sp, g->M, g->ef, vec, qn, nbh, nbd, &g->stats[2],
-                                          &g->stats[3]); /* graph.go:500 */
+                                          &g->stats[3]); /* graph.go:1005 */
             if (cnt == 0) {
                 free(nbh);
                 free(nbd);
+                /* graph.go:1009 returns here: the node keeps the layers above;
+                 * in none of them, its key is not present */
+                int any = 0;
+                for (int l2 = 0; l2 < g->nlayers; ++l2) any |= g->layers[l2].deg[idb] != -2;
+                if (i0 < 0 && !any) hdel(g, key);
+                fix_entries(g);
                 return set_err(g, OG_EINTERNAL, "no nodes found in neighborhood search");
             }
-            elevator = nbh[0]; /* graph.go:508 */
-            if (level >= l) {  /* graph.go:510-521 */
+            elevator = nbh[0]; /* graph.go:1013 */
+            if (level >= l) {  /* graph.go:1015-1032 */
+                if (l == i0) replace_sweep(g, key, old, ida, idb);
                 L->deg[id] = -1;
                 L->count++;
                 for (int j = 0; j < cnt; ++j) {
@@ -825,6 +938,10 @@ int og_add(og_graph *g, const int64_t *keys, const float *vecs, int64_t n, int d
         }
         free(nbh);
         free(nbd);
+        if (i0 >= 0) { /* graph.go:1035-1037: Len() did not grow -> the batch stops here */
+            fix_entries(g);
+            return set_err(g, OG_EINTERNAL, "node not added");
+        }
     }
     return OG_OK;
 }
@@ -843,7 +960,7 @@ static void isolate(og_graph *g, int l, int32_t n, int m) {
     for (int j = 0; j < d; ++j) {
         int32_t x = nb[j];
         if (L->deg[x] < 0) continue; /* neighbor.neighbors == nil */
-        list_remove(L, g->acap, x, n);
+        list_remove(g, L, x, n); /* graph.go:232 delete(neighbor.neighbors, n.Key) */
         replenish(g, l, x, m);
     }
     free(nb);
@@ -989,7 +1106,7 @@ static int search_one(og_graph *g, og_scratch *s, qbuf *qb, const float *q, int 
         for (int l = top; l >= 0; --l) { /* graph.go:571-622 */
             /* searchPoint = layers[l].entry() (nil when empty), or
              * layers[l].nodes[*elevator] (nil when that node was deleted) */
-            int32_t p = elevator >= 0 ? (member(g, l, elevator) ? elevator : -1)
+            int32_t p = elevator >= 0 ? resolve(g, l, elevator)
                                       : (l == top ? entry : (g->layers[l].count > 0 ? g->layers[l].entry : -1));
             if (l > 0) {
                 int c = compat_layer_search(g, s, l, p, 1, ef, q, qn, qb->ids, qb->ds, &qb->st[0], &qb->st[1]);
@@ -1284,6 +1401,13 @@ int og_import(og_graph *g, int64_t N, int dim, int L, int cap, const int64_t *ke
     free(g->scr.visited);
     free(g->hkeys);
     free(g->hvals);
+    free(g->kid);
+    free(g->kkeys);
+    free(g->kvals);
+    g->kid = NULL;
+    g->kkeys = NULL;
+    g->kvals = NULL;
+    g->kcap = g->kn = 0;
     g->keys = NULL;
     g->vecs = NULL;
     g->norms = NULL;
@@ -1306,6 +1430,7 @@ int og_import(og_graph *g, int64_t N, int dim, int L, int cap, const int64_t *ke
     for (int64_t i = 0; i < N; ++i) {
         g->norms[i] = og_dev_norm(vecs + (size_t)i * dim, dim);
         g->dead[i] = dead ? dead[i] : 0;
+        g->kid[i] = kid_get(g, keys[i], (int32_t)i);
         if (!g->dead[i] && hget(g, keys[i]) < 0) hput(g, keys[i], (int32_t)i);
     }
     for (int l = 0; l < L; ++l) {

@@ -7,6 +7,8 @@
   the replayed levels.
 * The opt-in dog-query hack of Search (graph.go:563-569, 595-619).
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -26,29 +28,85 @@ class Lcg:
         return (self.s >> 11) / 9007199254740992.0
 
 
-def test_host_rng_levels_build_the_oracle_graph(H, O):
-    from hnsw_amd.graph import random_level
+def _go_levels(draw, ml, n):
+    """Independent restatement of graph.go:370-417 for n fresh inserts (layer 0
+    of i nodes before insert i): maxLevel = Go math.Round(ln i / ln(1/ml)) + 1,
+    halves away from zero (exact here: x.5 cases compare equal)."""
+    out = []
+    for i in range(n):
+        if i == 0:
+            mx = 1
+        else:
+            x = math.log(i) / math.log(1.0 / ml)
+            f = math.floor(x)
+            mx = int(f + 1 if x - f >= 0.5 else f) + 1
+        lv = mx
+        for level in range(mx):
+            if draw() > ml:
+                lv = level
+                break
+        out.append(lv)
+    return out
 
+
+class Scripted:
+    """Float64() values from a list (a Go *rand.Rand stand-in with a known stream)"""
+
+    def __init__(self, vals):
+        self.vals, self.i = list(vals), 0
+
+    def Float64(self):
+        v = self.vals[self.i]
+        self.i += 1
+        return v
+
+
+def test_host_rng_levels_build_the_oracle_graph(H, O):
+    """Ml = 0.25 over 700 inserts crosses the layer-0 sizes where ln n / ln 4 is
+    exactly x.5 (n = 2, 32, 512): there Go rounds the level cap up.  The graph
+    built with a caller's Rng equals the oracle's built from levels of an
+    independent restatement of the rule."""
     rng = np.random.default_rng(4)
-    n, d, M, ml = 700, 20, 8, 0.3
+    n, d, M, ml = 700, 20, 8, 0.25
     X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
-    g = H.Graph(M=M, Ml=ml, EfSearch=20, Distance=H.EuclideanDistance, Rng=Lcg(99))
+    # a stream that stays below Ml for every draw at n = 2, 32, 512 (the cap
+    # decides those levels) and is a generic LCG elsewhere
+    special = {2, 32, 512}
+    lcg = Lcg(99)
+    vals = []
+    for i in range(n):
+        mx = 1 if i == 0 else int(math.floor(math.log(i) / math.log(4.0) + 0.5)) + 1
+        for _ in range(mx):
+            vals.append(0.1 if i in special else lcg.Float64())
+            if vals[-1] > ml:
+                break
+    want = _go_levels(Scripted(vals).Float64, ml, n)
+    assert [want[i] for i in sorted(special)] == [2, 4, 6]  # maxLevel(0.25, 2 / 32 / 512)
+    g = H.Graph(M=M, Ml=ml, EfSearch=20, Distance=H.EuclideanDistance, Rng=Scripted(vals))
     g.BatchAdd([H.MakeNode(i, X[i]) for i in range(40)])
     for i in range(40, 60):
         g.Add(H.MakeNode(i, X[i]))
     g.add_arrays(np.arange(60, n), X[60:])
-    r = Lcg(99)
-    lv = np.array([random_level(r, ml, i > 0, i) for i in range(n)], np.int32)
     o = O.Graph(metric=O.EUCLIDEAN, order=O.ORDER_DEV, M=M, Ml=ml, EfSearch=20)
-    o.add(np.arange(n), X, lv)
-    assert len(o.topography()) >= 3
+    o.add(np.arange(n), X, np.array(want, np.int32))
+    assert len(o.topography()) >= 6
     _same_graph(g.export(), o.export())
-    # SplitMix64Rand(s) is the engine's own seed-s stream
-    from hnsw_amd.graph import SplitMix64Rand
+    assert g.Topography() == o.topography()
+    # SplitMix64Rand(s) is the engine's own seed-s stream, and the engine's own
+    # draws follow the same rule
+    sm = H.SplitMix64Rand(42)
+    st = [42]
 
-    sm = SplitMix64Rand(42)
-    want = H.Graph(Rng=42).preview_levels(300)
-    assert [random_level(sm, 0.25, i > 0, i) for i in range(300)] == want.tolist()
+    def splitmix():
+        st[0] = (st[0] + 0x9E3779B97F4A7C15) & (2**64 - 1)
+        z = st[0]
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2**64 - 1)
+        return ((z ^ (z >> 31)) >> 11) / 9007199254740992.0
+
+    want = _go_levels(splitmix, 0.25, 600)
+    assert H.Graph(Rng=42).preview_levels(600).tolist() == want
+    assert [H.random_level(sm, 0.25, i > 0, i) for i in range(600)] == want
     g.close()
 
 

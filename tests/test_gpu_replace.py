@@ -1,0 +1,215 @@
+"""GPU parity of BatchAdd on keys that are already present (graph.go:1015-1024,
+1035-1037) and of keys that come back after a Delete (graph.go:50 map
+assignment): the HIP engine against the oracle on identical inputs --
+identical rows, adjacency, entries, dead flags, Len/Topography/Connectivity,
+the same errors at the same inserts, and identical compat / beam / exact
+results afterwards."""
+import numpy as np
+import pytest
+
+from tests.test_gpu_parity import _live_connectivity, _metric_fn, _same_graph, _search_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def _agree(H, O, g, o, Q, efs=(20,)):
+    ex = g.export()
+    _same_graph(ex, o.export())
+    assert g.Len() == len(o) and g.Topography() == o.topography()
+    assert g.Connectivity() == _live_connectivity(ex)
+    _search_parity(H, O, g, o, Q, efs=efs)
+
+
+def _both_add(H, O, g, o, keys, X, levels=None):
+    """The same BatchAdd on both sides -> the common error text (None: no error)."""
+    oe = ge = None
+    try:
+        o.add(keys, X, levels)
+    except O.OracleError as e:
+        oe = str(e)
+    try:
+        g.add_arrays(np.asarray(keys, np.int64), X, levels=levels)
+    except H.HnswError as e:
+        ge = str(e)
+    assert oe == ge, (oe, ge)
+    return oe
+
+
+def _walk_len(live, keys):
+    """inserts BatchAdd reaches: through the first key present (or repeated)"""
+    seen = set()
+    for i, k in enumerate(keys):
+        if k in live or k in seen:
+            return i + 1
+        seen.add(k)
+    return len(keys)
+
+
+@pytest.mark.parametrize("metric,M,ml,d,seeded", [(0, 8, 0.25, 24, False), (1, 6, 0.5, 5, True),
+                                                  (0, 10, 0.3, 48, True)])
+def test_readd_live_keys(H, O, metric, M, ml, d, seeded):
+    """A stream of batches where 20 % of the keys are live ones (some with
+    their old vector, so the old node is the nearest -- the elevator then names
+    the replaced key and the reference's walk fails one layer down): each call
+    inserts up to the first present key, replaces it and stops with "node not
+    added"; the caller goes on with the rest."""
+    rng = np.random.default_rng(100 + d)
+    n = 500
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    keys = (rng.permutation(4 * n)[:n] * 7 - 900).astype(np.int64)
+    Q = rng.uniform(-1, 1, (32, d)).astype(np.float32)
+    seed = 4242
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=ml, EfSearch=20, seed=seed)
+    g = H.Graph(M=M, Ml=ml, EfSearch=20, Distance=_metric_fn(H, metric), Rng=seed)
+    lv0 = None if seeded else o.preview_levels(n)
+    assert _both_add(H, O, g, o, keys, X, lv0) is None
+    _agree(H, O, g, o, Q)
+    vec = {int(k): X[i] for i, k in enumerate(keys)}
+    fresh = 10**6
+    errors = {}
+    for step in range(30):
+        cnt = int(rng.integers(1, 9))
+        ks, vs = [], []
+        for _ in range(cnt):
+            r = rng.random()
+            if r < 0.2:
+                k = int(rng.choice(list(vec)))
+                ks.append(k)
+                vs.append(vec[k] if rng.random() < 0.3 else rng.uniform(-1, 1, d).astype(np.float32))
+            else:
+                ks.append(fresh)
+                fresh += 1
+                vs.append(rng.uniform(-1, 1, d).astype(np.float32))
+        if step % 7 == 3 and ks:  # a key repeated inside one batch
+            ks.append(ks[0])
+            vs.append(rng.uniform(-1, 1, d).astype(np.float32))
+        V = np.stack(vs)
+        w = _walk_len(vec, ks)
+        lv = None if seeded else np.array([o.random_level() for _ in range(w)], np.int32)
+        if lv is not None:
+            lv = np.concatenate([lv, np.zeros(len(ks) - w, np.int32)])
+        err = _both_add(H, O, g, o, ks, V, lv)
+        errors[err] = errors.get(err, 0) + 1
+        if err is None or err == "node not added":
+            for k, v in zip(ks[:w], vs[:w]):
+                vec[k] = v
+        else:  # the walk failed part way: re-sync the model of live keys from the oracle
+            ex = o.export()
+            live = ex["dead"] == 0
+            vec = {int(k): ex["vecs"][i] for i, k in enumerate(ex["keys"]) if live[i] and ex["deg"][0, i] != -2}
+        _agree(H, O, g, o, Q)
+        if seeded:
+            assert np.array_equal(g.preview_levels(8), o.preview_levels(8))
+    assert errors.get("node not added", 0) >= 3, errors
+    for k in list(vec)[:20]:  # Lookup: the replacing value
+        v, ok = g.Lookup(k)
+        assert ok and np.array_equal(v, vec[k])
+
+
+def test_duplicate_inside_one_batch(H, O):
+    """[a, b, a]: a and b are inserted, the second a replaces the first."""
+    rng = np.random.default_rng(5)
+    d, n = 16, 200
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    Q = rng.uniform(-1, 1, (16, d)).astype(np.float32)
+    o = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=8, Ml=0.25, EfSearch=20, seed=9)
+    g = H.Graph(M=8, Ml=0.25, EfSearch=20, Rng=9)
+    assert _both_add(H, O, g, o, np.arange(n), X) is None
+    V = rng.uniform(-1, 1, (4, d)).astype(np.float32)
+    assert _both_add(H, O, g, o, [5000, 5001, 5000, 5002], V) == "node not added"
+    _agree(H, O, g, o, Q)
+    assert len(o) == n + 2  # 5002 never ran
+    v, ok = g.Lookup(5000)
+    assert ok and np.array_equal(v, V[2])
+    assert g.Lookup(5002) == (None, False)
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_delete_then_readd(H, O, metric):
+    """Delete 30 % of the keys, then add the same keys with new vectors at
+    768-d: nodes still holding a dangling entry of a key get it overwritten
+    when the new node links to them (graph.go:50), searches visit a key once."""
+    rng = np.random.default_rng(77 + metric)
+    n, d, M = 400, 768, 16
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    Q = rng.uniform(-1, 1, (24, d)).astype(np.float32)
+    keys = np.arange(n, dtype=np.int64) * 2 + 1
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=0.25, EfSearch=20, seed=31)
+    g = H.Graph(M=M, Ml=0.25, EfSearch=20, Distance=_metric_fn(H, metric), Rng=31)
+    assert _both_add(H, O, g, o, keys, X) is None
+    gone = [int(k) for k in rng.choice(keys, 120, replace=False)]
+    assert o.delete(gone) == g.BatchDelete(gone)
+    _agree(H, O, g, o, Q, efs=(20, 64))
+    back = list(gone)
+    rng.shuffle(back)
+    errs = tries = 0
+    while back and tries < 40:
+        tries += 1
+        ks, back = back[:10], back[10:]
+        V = rng.uniform(-1, 1, (len(ks), d)).astype(np.float32)
+        err = _both_add(H, O, g, o, ks, V)
+        assert err in (None, "no nodes found in neighborhood search", "node not added"), err
+        if err is not None:  # the walk stopped part way: the keys it did not add go again
+            errs += 1
+            ex = o.export()
+            in0 = {int(k) for i, k in enumerate(ex["keys"]) if ex["dead"][i] == 0 and ex["deg"][0, i] != -2}
+            back += [k for k in ks if k not in in0]
+        _agree(H, O, g, o, Q)
+    assert g.Len() == len(o) and errs > 0
+    assert np.array_equal(g.preview_levels(8), o.preview_levels(8))
+
+
+def test_host_rng_draws_follow_the_walk(H, O):
+    """With a host Rng, a BatchAdd that stops at a replacement draws levels only
+    for the inserts it reached (graph.go:962): the next Add's levels continue
+    the same stream, so the graph equals the oracle's (same seed)."""
+    rng = np.random.default_rng(8)
+    d, n = 12, 300
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    Q = rng.uniform(-1, 1, (16, d)).astype(np.float32)
+    o = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=6, Ml=0.25, EfSearch=20, seed=77)
+    g = H.Graph(M=6, Ml=0.25, EfSearch=20, Rng=H.SplitMix64Rand(77))
+    o.add(np.arange(n), X)
+    g.BatchAdd([H.Node(i, X[i]) for i in range(n)])
+    _agree(H, O, g, o, Q)
+    for step in range(6):
+        ks = [10_000 + 10 * step + j for j in range(5)] + [int(rng.integers(0, n))] + [20_000 + step]
+        V = rng.uniform(-1, 1, (len(ks), d)).astype(np.float32)
+        with pytest.raises(O.OracleError, match="node not added"):
+            o.add(ks, V)
+        with pytest.raises(H.HnswError, match="node not added"):
+            g.BatchAdd([H.Node(k, V[i]) for i, k in enumerate(ks)])
+        _agree(H, O, g, o, Q)
+    # a dimension mismatch part way: the nodes before it stay added (graph.go:955-960)
+    with pytest.raises(H.HnswError, match="embedding dimension mismatch: 12 != 3"):
+        g.BatchAdd([H.Node(30_000, X[0]), H.Node(30_001, X[1]), H.Node(30_002, X[2][:3])])
+    o.add([30_000, 30_001], X[:2])
+    _agree(H, O, g, o, Q)
+
+
+def test_add_plan_and_contains(H):
+    g = H.Graph(M=4, Ml=0.25, EfSearch=10, Rng=1)
+    X = np.random.default_rng(1).uniform(-1, 1, (10, 8)).astype(np.float32)
+    g.add_arrays(np.arange(10), X)
+    assert g.contains([3, 10, 9, -1]).tolist() == [True, False, True, False]
+    import ctypes as C
+    lib = H.load()
+    for ks, want in (([20, 21, 3, 22], 3), ([20, 21, 20, 5], 3), ([20, 21], 2), ([4], 1)):
+        a = np.array(ks, np.int64)
+        w, one = C.c_int64(), C.c_int()
+        assert lib.mhnsw_add_plan(g._h, a.ctypes.data_as(C.POINTER(C.c_int64)), len(a), C.byref(w), C.byref(one)) == 0
+        assert (w.value, one.value) == (want, 0)
+    g.BatchDelete([0])
+    a = np.array([99], np.int64)
+    w, one = C.c_int64(), C.c_int()
+    lib.mhnsw_add_plan(g._h, a.ctypes.data_as(C.POINTER(C.c_int64)), 1, C.byref(w), C.byref(one))
+    assert one.value == 1  # a dangling elevator can now fail an insert: one at a time
+
+
+def test_batch_mode_rejects_present_keys(H):
+    g = H.Graph(M=8, Ml=0.25, EfSearch=20, Rng=1, build_mode=H.BUILD_BATCH)
+    X = np.random.default_rng(2).uniform(-1, 1, (50, 8)).astype(np.float32)
+    g.add_arrays(np.arange(50), X)
+    with pytest.raises(H.HnswError, match="compat build mode"):
+        g.add_arrays(np.array([3]), X[:1])
+    assert g.Len() == 50

@@ -162,17 +162,18 @@ def test_sharded_engine_gloo_world2(H, O):
             _same_results(r0[0], r0[1], r0[2], fk, fd, fn)
 
 
-def test_config3_layout_tenth_scale(H):
-    """BASELINE configs[3]'s layout (8 node-ID range shards of 768-d cosine,
-    every query on every shard, per-shard top-k merged) at 1/10 of its 10M rows,
-    on one GPU: 8 x 125k rows built by the batched insert with the bench's graph
-    recipe.  Sharded exact == the exact top-k of one flat index over all rows;
-    sharded beam (ef 64) recall@10 >= 0.99 against it."""
+def test_config3_full_size(H):
+    """BASELINE configs[3] at its stated size on one GPU: 10M x 768-d cosine in
+    8 node-ID range shards of 1.25M rows, each built by the batched insert with
+    the bench's graph recipe; every query searched on every shard and the
+    per-shard top-k merged (the 8-GPU layout, each shard a separate handle).
+    Sharded exact == the exact top-k of one flat index over all 10M rows,
+    bitwise; sharded beam (ef 64) recall@10 >= 0.99 against it."""
     torch = pytest.importorskip("torch")
     from bench import gen_vectors
     from hnsw_amd.shard import engine_local_search, merge_topk, shard_range
 
-    S, n, d, B, k = 8, 1_000_000, 768, 4096, 10
+    S, n, d, B, k = 8, 10_000_000, 768, 4096, 10
     dev = torch.device("cuda:0")
     X = gen_vectors(n, d, 1234, 12, 1000, dev, "cosine")
     Q = gen_vectors(B, d, 9011, 12, 1000, dev, "cosine")
@@ -186,7 +187,8 @@ def test_config3_layout_tenth_scale(H):
         g.reserve(hi - lo, d)
         g.add_device(keys[lo:hi], X[lo:hi].contiguous().data_ptr(), hi - lo, d)
         shards.append(g)
-    full = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, build_mode=H.BUILD_FLAT)
+        print(f"shard {s}: {hi - lo} rows built", flush=True)
+    full = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, build_mode=H.BUILD_FLAT, screen=0)
     full.reserve(n, d)
     full.add_device(keys, X.data_ptr(), n, d)
     del X

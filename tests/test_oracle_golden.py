@@ -328,3 +328,55 @@ def test_search_with_negatives_reference_cases(O):
     assert np.array_equal(k, pk) and np.array_equal(n, pn)
     with pytest.raises(O.OracleError, match="negWeight must be between 0.0 and 1.0, got 1.500000"):
         g.search_negatives(dog[None], [puppy[None]], 3, 1.5)
+
+
+def test_max_level_rounds_halves_up(O):
+    """graph.go:382 int(math.Round(l)) + 1: Go rounds halves away from zero.
+    With Ml = 0.25, ln n / ln 4 is exactly x.5 at n = 2, 32, 512, 8192, 131072
+    (np.round would give one less).  Oracle and the Python host agree."""
+    from hnsw_amd.graph import max_level
+
+    kats = {(0.25, 2): 2, (0.25, 32): 4, (0.25, 512): 6, (0.25, 8192): 8, (0.25, 131072): 10,
+            (0.25, 3): 2, (0.25, 31): 3, (0.5, 10): 4, (0.5, 1000): 11}
+    for (ml, n), want in kats.items():
+        assert O.max_level(ml, n) == want, (ml, n)
+        assert max_level(ml, n) == want, (ml, n)
+    for n in range(1, 200_000, 97):
+        for ml in (0.25, 0.5, 0.3, 0.125):
+            assert max_level(ml, n) == O.max_level(ml, n), (ml, n)
+
+
+def test_oracle_replacement_walk(O):
+    """graph.go:1015-1037 restated: BatchAdd of a present key inserts the
+    nodes before it, replaces it -- the old node leaves every layer (a dead row
+    still reachable through one-directional edges), the new one holds the key
+    from the first layer at or below its level where the old one was -- and
+    stops with "node not added"; Len() is unchanged by the replacement."""
+    import numpy as np
+
+    rng = np.random.default_rng(0)
+    n, d = 120, 6
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    o = O.Graph(metric=O.COSINE, M=4, Ml=0.5, EfSearch=10, seed=3)
+    o.add(np.arange(n), X)
+    top = o.topography()
+    V = rng.uniform(-1, 1, (3, d)).astype(np.float32)
+    lv = np.array([0, 0, 0], np.int32)
+    try:
+        o.add([500, 7, 501], V, lv)
+        raise AssertionError("expected node not added")
+    except O.OracleError as e:
+        assert str(e) == "node not added"
+    assert len(o) == n + 1  # 500 added, 7 replaced, 501 never reached
+    ex = o.export()
+    rows7 = [i for i, k in enumerate(ex["keys"]) if k == 7]
+    assert len(rows7) == 2 and ex["dead"][rows7[0]] == 1 and ex["dead"][rows7[1]] == 0
+    assert (ex["deg"][:, rows7[1]] != -2).tolist() == [True] + [False] * (len(top) - 1)  # level 0 only now
+    assert 501 not in ex["keys"].tolist()
+    # no live row points at the old node's key twice, and no map holds two rows of one key
+    for l in range(ex["deg"].shape[0]):
+        for i in range(ex["deg"].shape[1]):
+            dd = ex["deg"][l, i]
+            if dd > 0:
+                ks = ex["keys"][ex["adj"][l, i, :dd]].tolist()
+                assert len(ks) == len(set(ks)), (l, i)
