@@ -57,7 +57,12 @@ def parse():
     p.add_argument("--mode", choices=["replica", "shard"], default="replica",
                    help="headline layout; with replica the shard layout is measured too (--no-shard-leg skips it)")
     p.add_argument("--no-shard-leg", action="store_true")
-    p.add_argument("--nbase", type=int, default=1_000_000, help="vectors per index (per shard in shard mode)")
+    p.add_argument("--nbase", type=int, default=1_000_000, help="vectors of the replica index")
+    p.add_argument("--total-rows", type=int, default=10_000_000,
+                   help="rows of the sharded index over all ranks (BASELINE configs[3]: 10M, 1.25M per rank at 8)")
+    p.add_argument("--configs", default="0,2,4",
+                   help="secondary BASELINE configs measured at N=1 (configs[0] reference shape, [2] L2 build, "
+                        "[4] exact); '' disables")
     p.add_argument("--dim", type=int, default=768)
     p.add_argument("--batch", type=int, default=65536, help="queries per step per GPU")
     p.add_argument("--ef", type=int, default=64)
@@ -134,6 +139,173 @@ def recall_at_k(res, n, truth, tn, k):
     return tot / res.shape[0]
 
 
+def host_threads():
+    """CPUs this process can use: the affinity mask (nproc), capped by the
+    cgroup's CPU quota when one is set (a container's share of a large host)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            parts = open(path).read().split()
+            if path.endswith("cpu.max") and parts[0] != "max":
+                n = min(n, max(1, int(int(parts[0]) / int(parts[1]))))
+            elif path.endswith("quota_us") and int(parts[0]) > 0:
+                period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+                n = min(n, max(1, int(parts[0]) // period))
+        except (OSError, ValueError, IndexError):
+            continue
+    return n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def build_roofline(bs, secs, n, dim, m0, metric, traffic=None):
+    """Batched insert: the search kernels' algorithmic bytes -- f32 rows (4d + 4:
+    row + norm) for every f32 evaluation and neighbour-selection row, fp16 rows
+    (2d, + 8 for L2's {unscale, |x|}) for every screened candidate, one layer-0
+    adjacency row per expansion, the new row and its adjacency/proposal writes --
+    over their device time (HIP events around each launch)."""
+    F, Sc, Xp = bs["build_f32_rows"], bs["build_screened"], bs["build_expansions"]
+    aux = 8 if metric == "euclidean" else 0
+    byts = F * (4 * dim + 4) + Sc * (2 * dim + aux) + Xp * 4 * (m0 + 1) + n * (4 * dim + 16 * m0)
+    us = bs["build_search_us"]
+    gbs = byts / (us * 1e-6) / 1e9 if us > 0 else None
+    return {"inserts_per_s": round(n / secs, 1), "seconds": round(secs, 2),
+            "dist_evals_per_insert": round(bs["build_dist_evals"] / n, 1),
+            "f32_rows_per_insert": round(F / n, 1), "screened_per_insert": round(Sc / n, 1),
+            "expansions_per_insert": round(Xp / n, 1), "dropped_proposals": bs["dropped_proposals"],
+            "roofline": {"bound": "hbm", "kernel": "k_batch_search + k_batch_descend",
+                         "kernel_ms_total": round(us / 1e3, 2), "alg_bytes": int(byts),
+                         "achieved": round(gbs, 1) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None,
+                         "traffic": traffic, "traffic_kernel": "k_batch_search"}}
+
+
+def timed(fn, reps=1):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps, r
+
+
+def config0(device, seconds):
+    """BASELINE configs[0], the reference's own CPU benchmark shape
+    (graph_benchmark_test.go:50-89): 10k x 128 U[-1,1) cosine, M 16, Ml 0.25,
+    EfSearch 20, k 10, 1000 queries -- with the reference's semantics end to end
+    (compat Add and compat Search, graph.go:437-625) on the GPU, and the same
+    Search restated in C (oracle/) on the host's cores on the same graph."""
+    import oracle as O  # CPU baseline only
+
+    n, d, nq, k = 10_000, 128, 1000, 10
+    rng = np.random.default_rng(42)
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    Qh = rng.uniform(-1, 1, (nq, d)).astype(np.float32)
+    g = H.Graph(M=16, Ml=0.25, EfSearch=20, Distance=H.CosineDistance, Rng=42)  # compat build (reference Add)
+    bt, _ = timed(lambda: g.add_arrays(np.arange(n), X))
+    Q = torch.from_numpy(Qh).to(device)
+    S = Searcher(g, nq, k, d, device)
+    S.run(Q, H.MODE_COMPAT, 20)
+    st, (ck, _, cn) = timed(lambda: S.run(Q, H.MODE_COMPAT, 20), reps=20)
+    g.device_status()
+    ck, cn = ck.clone(), cn.clone()
+    tk, _, tn = (x.clone() for x in Searcher(g, nq, k, d, device).run(Q, H.MODE_EXACT, 0))
+    rec = recall_at_k(ck, cn, tk, tn, k)
+    o = O.Graph(metric=O.COSINE, order=O.ORDER_REF, M=16, Ml=0.25, EfSearch=20)
+    o.import_graph(**g.export())
+    cpu = {}
+    for name, nt in (("1_thread", 1), ("all_threads", host_threads())):
+        chunk = max(nq, 64 * nt)
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds / 4:
+            o.search(Qh[np.arange(done, done + chunk) % nq], k, mode=O.MODE_COMPAT, threads=nt)
+            done += chunk
+        cpu[name] = round(done / (time.perf_counter() - t0), 1)
+    ob = O.Graph(metric=O.COSINE, order=O.ORDER_REF, M=16, Ml=0.25, EfSearch=20, seed=42)
+    nb = 2000  # bounded sample of the reference Add walk
+    cbt, _ = timed(lambda: ob.add(np.arange(nb), X[:nb]))
+    g.close()
+    return {"workload": "10k x 128-d U[-1,1) cosine, M=16 Ml=0.25 EfSearch=20, k=10, 1000 queries (reference "
+                        "semantics: compat Add + compat Search)",
+            "gpu_compat_add_inserts_per_s": round(n / bt, 1), "gpu_compat_search_qps": round(nq / st, 1),
+            "recall_at_10_compat": round(rec, 4),
+            "cpu_compat_search_qps": cpu["1_thread"], "cpu_compat_search_qps_all_threads": cpu["all_threads"],
+            "cpu_threads": host_threads(), "cpu_model": cpu_model(),
+            "cpu_compat_add_inserts_per_s": round(nb / cbt, 1), "cpu_compat_add_sample": nb,
+            "cpu_kind": "port (oracle/: C restatement of graph.go, ORDER_REF sequential fp32; the Go toolchain is absent)"}
+
+
+def config2(device):
+    """BASELINE configs[2]: 1M x 768 Euclidean, the batched insert at SURVEY
+    8(d) C3's efConstruction = EfSearch = 64 (graph.go:500), M 16; recall@10 of
+    the built graph at ef 64 against the exact path."""
+    n, d = 1_000_000, 768
+    X = gen_vectors(n, d, 77, 12, 1000, device, "euclidean")
+    Q = gen_vectors(4096, d, 78, 12, 1000, device, "euclidean")
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.EuclideanDistance, Rng=5, build_mode=H.BUILD_BATCH,
+                m0=48, ef_construction=64, heuristic=2, time_build=1)
+    g.reserve(n, d)
+    bt, _ = timed(lambda: g.add_device(np.arange(n), X.data_ptr(), n, d))
+    bs = g.stats()
+    del X
+    tk, _, tn = (x.clone() for x in Searcher(g, 4096, 10, d, device).run(Q, H.MODE_EXACT, 0))
+    k_, _, n_ = Searcher(g, 4096, 10, d, device).run(Q, H.MODE_BEAM, 64)
+    rec = recall_at_k(k_, n_, tk, tn, 10)
+    g.close()
+    out = {"workload": "1M x 768-d Euclidean batched insert, M=16 M0=48 efConstruction=64 (SURVEY 8(d) C3)"}
+    out.update(build_roofline(bs, bt, n, d, 48, "euclidean"))
+    out["recall_at_10_ef64"] = round(rec, 4)
+    return out
+
+
+def config4(device, steps=10):
+    """BASELINE configs[4]: 1M x 1536 cosine, batch 1024, the exact path (fp16
+    MFMA scores with the fused preselection, canonical re-rank, certificate)."""
+    n, d, B = 1_000_000, 1536, 1024
+    X = gen_vectors(n, d, 55, 12, 1000, device, "cosine")
+    Q = gen_vectors(B, d, 56, 12, 1000, device, "cosine")
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_FLAT, screen=0)
+    g.reserve(n, d)
+    g.add_device(np.arange(n), X.data_ptr(), n, d)
+    del X
+    S = Searcher(g, B, 10, d, device)
+    for _ in range(2):
+        S.run(Q, H.MODE_EXACT, 0)
+    g.reset_stats()
+    gemm, path = [], []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        S.run(Q, H.MODE_EXACT, 0)
+        path.append(g.last_kernel_ms())
+        gemm.append(g.get_option("last_gemm_ns") * 1e-6)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    g.device_status()
+    unc = g.stats()["exact_uncertified"] / steps
+    g.close()
+    flops = 2.0 * B * n * d
+    gm = float(np.mean(gemm))
+    return {"workload": "1M x 1536-d cosine exact search, batch 1024, k=10 (recall 1.0: certified canonical top-k)",
+            "queries_per_s": round(B / dt, 1), "ms_per_batch": round(dt * 1e3, 3),
+            "exact_path_ms": round(float(np.mean(path)), 3), "uncertified_per_batch": unc,
+            "roofline": {"bound": "mfma", "kernel": "k_scores_ring (fp16 1-product, fused filter epilogue)",
+                         "kernel_ms": round(gm, 4), "flops_per_launch": flops,
+                         "achieved": round(flops / (gm * 1e-3) / 1e12, 1), "peak": 2500.0, "unit": "TFLOP/s",
+                         "frac": round(flops / (gm * 1e-3) / 1e12 / 2500.0, 4), "traffic": None}}
+
+
 def cpu_baseline(g, queries_np, k, ef, metric, seconds):
     """The CPU restatement (oracle/, test infrastructure) timed on this host on a
     bounded sample: same graph, same beam algorithm; plus the reference's
@@ -147,14 +319,15 @@ def cpu_baseline(g, queries_np, k, ef, metric, seconds):
     o.import_graph(**ex)
     del ex
     out = {}
-    threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
+    threads = host_threads()
+    nq = len(queries_np)
     for name, mode, nt, frac in (("beam", O.MODE_BEAM, 1, 0.4), ("compat", O.MODE_COMPAT, 1, 0.3),
                                  ("beam_mt", O.MODE_BEAM, threads, 0.3)):
-        chunk = 32 * nt
+        chunk = 32 * nt  # 32 queries per thread per call (thread start-up amortised)
         done, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < seconds * frac and done < len(queries_np):
-            o.search(queries_np[done:done + chunk], k, mode=mode, ef=ef, threads=nt)
-            done += min(chunk, len(queries_np) - done)
+        while time.perf_counter() - t0 < seconds * frac:  # cycles through the sample
+            o.search(queries_np[np.arange(done, done + chunk) % nq], k, mode=mode, ef=ef, threads=nt)
+            done += chunk
         out[name] = (done / (time.perf_counter() - t0), done, nt)
     return out
 
@@ -180,21 +353,22 @@ def main():
 
     sweep = None
 
-    def build(off, rng_seed):
+    def build(off, rng_seed, nrows=None):
         nonlocal sweep
-        X = gen_vectors(a.nbase, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=off)
+        nrows = a.nbase if nrows is None else nrows
+        X = gen_vectors(nrows, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=off)
         g = H.Graph(M=a.M, Ml=0.25, EfSearch=a.ef, Distance=metric, Rng=rng_seed, build_mode=H.BUILD_BATCH,
                     m0=a.M0, ef_construction=a.efc, heuristic=2, keep_pruned=a.keep_pruned, prune_alpha_pct=a.alpha,
                     build_expand=a.build_expand,
                     screen=a.screen, time_build=1)
-        g.reserve(a.nbase, a.dim)
-        keys = np.arange(off, off + a.nbase, dtype=np.int64)
+        g.reserve(nrows, a.dim)
+        keys = np.arange(off, off + nrows, dtype=np.int64)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        g.add_device(keys, X.data_ptr(), a.nbase, a.dim)
+        g.add_device(keys, X.data_ptr(), nrows, a.dim)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        if sweep is None and rank == 0:
+        if sweep is None and rank == 0 and nrows == a.nbase:
             sweep = sweep_bench(X)
         del X
         return g, dt, g.stats()
@@ -271,12 +445,14 @@ def main():
 
     # ---- shard layout: rank r owns rows [r*nbase, (r+1)*nbase) of one dataset --------
     shard_out = None
+    shard_g = None
     if shard_only or not a.no_shard_leg:
-        lo, _ = shard_range(a.nbase * world, world, rank)
-        if g is not None and lo == 0:
+        lo, hi = shard_range(a.total_rows, world, rank)
+        if g is not None and lo == 0 and hi == a.nbase:
             gs, sbuild_s, sbstats = g, build_s, bstats  # rank 0's shard is the replica index
         else:
-            gs, sbuild_s, sbstats = build(lo, a.seed + rank)
+            gs, sbuild_s, sbstats = build(lo, a.seed + rank, hi - lo)
+        shard_g = gs
         Qs = gen_vectors(a.batch, a.dim, qseed, a.intrinsic, a.clusters, device, a.metric)  # same on every rank
 
         def sstep():
@@ -291,51 +467,38 @@ def main():
         shard_out = {
             "value": round(a.batch * a.steps / s_el, 1), "unit": "queries/s",
             "ms_per_step": round(s_el / a.steps * 1e3, 3), "recall_at_10": round(srecall, 4),
-            "n_base_total": a.nbase * world, "shards": world, "rows_per_shard": a.nbase,
+            "n_base_total": a.total_rows, "shards": world, "rows_per_shard": hi - lo,
             "queries_per_step": a.batch, "search_kernel_ms": round(skms, 4),
             "exchange": ("none (one shard)" if world == 1 else
                          f"one all-gather of {a.batch * (12 * a.k + 4)} B per rank ({a.backend}), k_merge on the GPU"),
             "recall_reference": "sharded exact search (per-shard MFMA exact + the same gather + merge)",
-            "build_inserts_per_s_per_rank": round(a.nbase / sbuild_s, 1),
+            "build_inserts_per_s_per_rank": round((hi - lo) / sbuild_s, 1),
+            "scaling": "strong (fixed total rows; BASELINE configs[3] at 8 ranks)",
+            "layout_ceiling": ("node-ID range shards: every query runs on every shard and a shard's search cost "
+                               "falls only ~log(rows per shard), so N ranks serve about the queries/s of one GPU "
+                               "searching a total/N-row index -- at most ~1.2x one 10M index at 8 ranks "
+                               "(DESIGN.md section 8); throughput scales with replicas (`value`)"),
         }
         if shard_only:
             g, build_s, bstats, recall, elapsed, kernel_ms, st = gs, sbuild_s, sbstats, srecall, s_el, s_kms, s_st
             Q, S = Qs, Searcher(gs, a.batch, a.k, a.dim, device)
             tk, tn = ek, en
 
-    def build_roofline(bs, secs):
-        """Batched insert (configs[2] kernel family, here on the bench index): the
-        search kernels' algorithmic bytes -- f32 rows (4d + 4: row + norm) for every
-        f32 evaluation and neighbour-selection row, fp16 rows (2d) for every screened
-        candidate, one layer-0 adjacency row per expansion, the new row and its
-        adjacency/proposal writes -- over their device time (HIP events)."""
-        F, Sc, Xp = bs["build_f32_rows"], bs["build_screened"], bs["build_expansions"]
-        aux = 8 if a.metric == "euclidean" else 0
-        byts = F * (4 * a.dim + 4) + Sc * (2 * a.dim + aux) + Xp * 4 * (a.M0 + 1) + a.nbase * (4 * a.dim + 16 * a.M0)
-        us = bs["build_search_us"]
-        gbs = byts / (us * 1e-6) / 1e9 if us > 0 else None
-        # HBM bytes of k_batch_search from a separate rocprofv3 --pmc pass of this
-        # same configuration (tools/profile_round.sh), when one is recorded
-        traffic = None
+    def build_traffic(n):
+        """HBM bytes of k_batch_search from a separate rocprofv3 --pmc pass of this
+        same configuration (tools/profile_round.sh), when one is recorded"""
         try:
             pm = json.load(open(a.pmc_build_json))
-            want = dict(n=a.nbase, dim=a.dim, efc=a.efc, m0=a.M0, keep_pruned=a.keep_pruned, alpha=a.alpha,
+            want = dict(n=n, dim=a.dim, efc=a.efc, m0=a.M0, keep_pruned=a.keep_pruned, alpha=a.alpha,
                         screen=a.screen, rev=KERNEL_REV)
             if all(pm.get(k) == v for k, v in want.items()):
-                traffic = pm.get("hbm_bytes_total")
+                return pm.get("hbm_bytes_total")
         except (OSError, ValueError):
-            traffic = None
-        return {"inserts_per_s": round(a.nbase / secs, 1), "seconds": round(secs, 2),
-                "dist_evals_per_insert": round(bs["build_dist_evals"] / a.nbase, 1),
-                "f32_rows_per_insert": round(F / a.nbase, 1), "screened_per_insert": round(Sc / a.nbase, 1),
-                "expansions_per_insert": round(Xp / a.nbase, 1), "dropped_proposals": bs["dropped_proposals"],
-                "roofline": {"bound": "hbm", "kernel": "k_batch_search + k_batch_descend",
-                             "kernel_ms_total": round(us / 1e3, 2), "alg_bytes": int(byts),
-                             "achieved": round(gbs, 1) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None,
-                             "traffic": traffic, "traffic_kernel": "k_batch_search"}}
+            pass
+        return None
 
     shard = shard_only
+    g_rows = (shard_out["rows_per_shard"] if shard_only else a.nbase)
     queries_done = a.batch * a.steps * (1 if shard else world)
     qps = queries_done / elapsed
 
@@ -430,7 +593,7 @@ def main():
             "screened_per_query": round(Sc / a.batch, 1), "f32_evals_per_query": round(F / a.batch, 1),
             "screen_margin": (g.get_option("screen_err_ppb") * 1e-9) if (g is not None and a.screen) else None,
         },
-        "build": build_roofline(bstats, build_s),
+        "build": build_roofline(bstats, build_s, g_rows, a.dim, a.M0, a.metric, build_traffic(g_rows)),
         "sweep": sweep,
         "cpu_baseline": None,
         "operating_points": points,
@@ -447,8 +610,24 @@ def main():
                       f"sequential fp32), single thread, ~{a.cpu_seconds * 0.4:.0f}s time box",
             "compat_search_qps": round(cb["compat"][0], 2), "compat_sample": cb["compat"][1],
             "beam_mt_qps": round(cb["beam_mt"][0], 2), "beam_mt_threads": cb["beam_mt"][2],
-            "beam_mt_sample": cb["beam_mt"][1], "host_cpus": os.cpu_count(),
+            "beam_mt_sample": cb["beam_mt"][1], "host_cpus": os.cpu_count(), "affinity_cpus": host_threads(),
+            "cpu_model": cpu_model(),
+            "note": ("compat = the reference's Search() semantics on the same 1M graph; beam_mt = concurrent "
+                     "Search on every CPU this process may use (graph_benchmark_test.go:70-89)"),
         }
+    if rank == 0 and world == 1 and a.configs:
+        for h_ in {id(x): x for x in (g, shard_g) if x is not None}.values():
+            h_.close()
+        torch.cuda.empty_cache()
+        which = set(a.configs.split(","))
+        cfg = {}
+        if "0" in which:
+            cfg["configs[0]"] = config0(device, a.cpu_seconds)
+        if "2" in which:
+            cfg["configs[2]"] = config2(device)
+        if "4" in which:
+            cfg["configs[4]"] = config4(device)
+        out["configs"] = cfg
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
