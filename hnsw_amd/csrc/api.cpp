@@ -143,6 +143,7 @@ struct mhnsw_index {
     // exact_precision 3 (fp16 1-product, fused preselection): sample thresholds,
     // filter constants, tile regions + counts, per-query buckets, the queries' rounding
     DevBuf<float> h1thr, h1c, h1s, qerr;
+    DevBuf<float> h1xw;  // [4 capn] per-row filter constants of k_h1_pp (k_h1_rowconst)
     DevBuf<uint2> h1region, h1bucket;
     DevBuf<int32_t> h1rcnt, h1qcnt;
     DevBuf<uint8_t> h1ovf;
@@ -1171,7 +1172,10 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         // fused preselection (h1): the sample = every stride-th full row tile (about 32
         // tiles), its J-th best score per query is the threshold (J = kk when the
         // sample is every tile); a row passes at a rate of ~J / sample rows
-        const int bm = h1_tile_bm(h->exact_tile);
+        // the GEMM variant this search runs (exact_tile 0: the default; a variant the
+        // shape does not admit falls back to k_h1_gemm)
+        const int ev = h1_effective_variant(h->exact_tile, h->pitch, std::max<int64_t>(qc, h->capn));
+        const int bm = h1_tile_bm(ev);
         const int64_t nnt = (h->n + H1_BN - 1) / H1_BN, nqt = (qc + bm - 1) / bm;
         const int stride = (int)std::max<int64_t>(1, std::min<int64_t>(128, nnt / 32));
         const int64_t nsamp = h1 ? ((h->n / H1_BN) - 1) / stride + 1 : 0;  // sampled full tiles
@@ -1185,13 +1189,16 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         // pairs per tile region / per query sub-bucket: 4x what the threshold lets
         // through on average (~J N / ns per query, ~bm J BN / ns per tile), with floors
         const int64_t ns = std::max<int64_t>(1, nsamp * H1_BN);
-        const int rcap = (int)std::min<int64_t>((int64_t)bm * H1_BN, std::max<int64_t>(2048, 4 * bm * J * H1_BN / ns));
+        // (a multiple of 8: k_h1_pp splits each tile's region among its 8 waves)
+        const int rcap = (int)std::min<int64_t>((int64_t)bm * H1_BN, std::max<int64_t>(2048, 4 * bm * J * H1_BN / ns) + 7) / 8 * 8;
+        const int rsub = h1_region_split(ev);
         const int scap = (int)std::min<int64_t>(std::max<int64_t>(h->n, 1),
                                                 std::max<int64_t>(512, 8 * J * h->n / ns / H1_BSUB));
         if (h1 && ((r = ensure_buf(h, h->h1thr, (size_t)qc)) || (r = ensure_buf(h, h->h1c, (size_t)nqt * bm + 256)) ||
                    (r = ensure_buf(h, h->h1s, (size_t)nqt * bm + 256)) ||
                    (r = ensure_buf(h, h->h1region, (size_t)nqt * nnt * rcap)) ||
-                   (r = ensure_buf(h, h->h1rcnt, (size_t)nqt * nnt)) ||
+                   (r = ensure_buf(h, h->h1rcnt, (size_t)nqt * nnt * rsub)) ||
+                   (r = ensure_buf(h, h->h1xw, (size_t)std::max<int64_t>(h->n, 1) * 4)) ||
                    (r = ensure_buf(h, h->h1qcnt, (size_t)qc * H1_BSUB * H1_CSTRIDE)) || (r = ensure_buf(h, h->h1ovf, (size_t)qc)) ||
                    (r = ensure_buf(h, h->h1bucket, (size_t)qc * H1_BSUB * scap)) || (r = ensure_buf(h, h->qerr, 1)) ||
                    (r = ensure_buf(h, h->xsegd, (size_t)qc * sseg * J)) ||
@@ -1313,7 +1320,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
                     as.tile_stride = stride;
                     as.nsample_tiles = nsamp;
                     as.ldS = nsamp * H1_BN;
-                    LCHK(h, launch_h1_sample(as, h->exact_tile, s));
+                    LCHK(h, launch_h1_sample(as, ev, s));
                     as.N = nsamp * H1_BN;
                     as.kk = J;
                     as.nseg = sseg;
@@ -1330,13 +1337,17 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
                     a.region = h->h1region.p;
                     a.region_cnt = h->h1rcnt.p;
                     a.rcap = rcap;
+                    a.xw = reinterpret_cast<const float4*>(h->h1xw.p);
+                    if (q0 == 0)
+                        LCHK(h, launch_h1_rowconst(h->xinv.p, h->norms, xdead, h->n, h->metric,
+                                                   reinterpret_cast<float4*>(h->h1xw.p), s));
                     if (timing && q0 == 0) HIPCHK(h, hipEventRecord(h->gev0, s));
-                    LCHK(h, launch_h1_filter(a, h->exact_tile, s));
+                    LCHK(h, launch_h1_filter(a, ev, s));
                     if (timing && q0 == 0) HIPCHK(h, hipEventRecord(h->gev1, s));
                     h->have_gemm_timing = timing;
                     const int64_t bqt = (nb + bm - 1) / bm;
                     LCHK(h, launch_bucket(h->h1region.p, h->h1rcnt.p, rcap, bqt * nnt, bqt, bm, H1_BN, nb, h->h1qcnt.p,
-                                          h->h1bucket.p, scap, h->h1ovf.p, a, s));
+                                          h->h1bucket.p, scap, h->h1ovf.p, rsub, a, s));
                     LCHK(h, launch_select_bucket(a, h->h1qcnt.p, h->h1bucket.p, scap, h->h1ovf.p, h->h1thr.p, s));
                 } else if (h2) {
                     a.xinv = h->xinv.p;
@@ -1353,7 +1364,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
                 LCHK(h, launch_exact_scores(a, s));
             }
             if (!h1) LCHK(h, launch_exact_select(a, s));
-            if (h1 && h->exact_tile >= 7) continue;  // timing diagnostic: no re-rank, no results
+            if (h1 && h1_timing_diag(ev)) continue;  // timing diagnostic: no re-rank, no results
             HIPCHK(h, hipMemsetAsync(h->xnflag.p, 0, sizeof(int32_t), s));
             CertArgs c1 = cert;
             c1.bound = h->xbound.p;
@@ -1370,7 +1381,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             LCHK(h, launch_rerank(a.Q, g, h->cand.p, kk, nb, h->lpr, h->vpl, k, ok_, od_, on_, oi_, c2, s));
         }
         if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));
-        if (h->exact_precision == 3 && h->n >= H1_BN && h->exact_tile >= 7)
+        if (h->exact_precision == 3 && h->n >= H1_BN && h1_timing_diag(ev))
             return fail(h, MHNSW_EUNSUPPORTED, "exact_tile %d is a timing diagnostic: no results", h->exact_tile);
     } else {
         if ((r = sync_layer_entries(h))) return r;
@@ -1523,6 +1534,7 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->h1thr.p);
     F(h->h1c.p);
     F(h->h1s.p);
+    F(h->h1xw.p);
     F(h->qerr.p);
     F(h->h1region.p);
     F(h->h1bucket.p);
@@ -1623,7 +1635,7 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "exact_kk") {
         h->exact_kk = (int)v;
     } else if (n == "exact_tile") {
-        if (v < 0 || v > 9) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 9]");
+        if (v < 0 || v > 26) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 26]");
         h->exact_tile = (int)v;
     } else if (n == "upper_ef") {
         if (v < 1 || v > 64) return fail(h, MHNSW_EINVAL, "upper_ef must be in [1, 64]");

@@ -25,6 +25,7 @@
 //  k_merge  : per query, merge S shard top-k lists by (distance, key).
 #include <algorithm>
 #include <type_traits>
+#include <utility>
 
 #include "device_search.hpp"
 #include "engine.hpp"
@@ -680,6 +681,1053 @@ int launch_exact_scores_x3(const ExactArgs& a, int tile, hipStream_t s) { return
 int launch_exact_scores_x2h(const ExactArgs& a, int tile, hipStream_t s) { return launch_split_scores<RING_H2>(a, tile, s); }
 
 // ---------------------------------------------------------------------------
+// k_h1_gemm: the fp16 1-product scores (exact_precision 3) on a 256 x 256 block
+// tile (queries x rows) with 64-deep K-tiles, 8 waves of 128 x 64 on
+// v_mfma_f32_32x32x16_f16 (8 accumulators of 16 per lane).  Each block reads
+// 256 query rows and 256 base rows per K-tile: 2 x fewer L2 -> LDS bytes per
+// flop than the 128 x 256 ring.  Two 64-KiB LDS buffers, each a whole K-tile
+// (A then B, 128-B rows, 16-B chunk kc of row r at slot kc ^ ((r >> 1) & 7):
+// every 16-lane group of a fragment ds_read_b128 hits 16 distinct slots),
+// filled by LDS-DMA (global_load_lds_dwordx4, 8 per thread per K-tile: a
+// piece = 8 rows x 128 B, source pre-swizzled so the linear DMA image is the
+// swizzled one).  K-tile t + 1 streams into one buffer while the waves multiply
+// K-tile t out of the other; one wait + barrier per K-tile.  Per lane the
+// DMA source offsets are fixed; a K-tile only advances two scalar bases.
+// Epilogues as k_scores_ring's (EPI 0 sample scores, EPI 1 fused filter).
+// DIAG as k_scores_ring's (exact_tile 11-13: 1 no epilogue, 2 also no waits /
+// barriers, 3 also no DMA).
+// ---------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int G_BM = 256, G_BN = 256, G_BK = 64;
+constexpr int G_BUF = (G_BM + G_BN) * G_BK * 2;  // 64 KiB per K-tile buffer
+
+template <int EPI, int DIAG = 0>
+__global__ __launch_bounds__(512) void k_h1_gemm(ExactArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t L0[G_BUF + 16];  // tail: the tile's region counter
+    __shared__ __attribute__((aligned(16))) uint8_t L1[G_BUF];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 2, wn = wave & 3;  // wave tile: queries wm*128.., rows wn*64..
+    // XCD-aware tile order (as k_scores_ring): each XCD walks a contiguous run of
+    // logical tiles, query tiles fastest, so a base tile enters its L2 once
+    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
+    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
+    const int64_t nblk = nqt * nnt;
+    const int64_t per = nblk / 8, rem = nblk % 8;
+    const int64_t xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
+    const int64_t logical = xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+    const int64_t qt = logical % nqt, nt = logical / nqt;
+    const int64_t q0 = qt * G_BM;
+    const int64_t n0 = (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
+    int* const tile_ctr = reinterpret_cast<int*>(L0 + G_BUF);
+    if (EPI == 1 && tid == 0) *tile_ctr = 0;  // ordered before the epilogue by the main loop's barriers
+
+    // DMA pieces of this wave: A pieces wv*4 + i and B pieces wv*4 + i (i < 4), a
+    // piece = image rows 8P .. 8P+7 (1 KiB).  Lane l: image row rr = 8P + l/8,
+    // slot l%8 holds chunk kc = (l%8) ^ ((rr >> 1) & 7) = halves 8kc .. 8kc+7 of
+    // the K-tile, which sit in K-block 2 kc'/.. of the 16-blocked plane: byte
+    // ((kc/2) ld + row) 32 + (kc%2) 16 from the tile's base.  Rows past B / N
+    // are clamped to the last row (valid loads; those outputs are never kept).
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    uint32_t poff[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const bool isA = i < 4;
+        const int P = wv * 4 + (i & 3);
+        const int rr = P * 8 + (lane >> 3);
+        const int kc = (lane & 7) ^ ((rr >> 1) & 7);
+        const int64_t row0 = isA ? q0 : n0, rmax = isA ? a.B - 1 : a.N - 1, ld = isA ? a.ldQs : a.ldXs;
+        const int64_t rc = min(row0 + rr, rmax) - row0;
+        poff[i] = (uint32_t)((((int64_t)(kc >> 1)) * ld + rc) * 32 + (kc & 1) * 16);
+    }
+    const char* const abase = reinterpret_cast<const char*>(a.Qh + q0 * X3K);
+    const char* const bbase = reinterpret_cast<const char*>(a.Xh + n0 * X3K);
+    const int64_t astep = a.ldQs * X3K * 4 * 2, bstep = a.ldXs * X3K * 4 * 2;  // bytes per K-tile (4 K-blocks)
+    const int nkt = a.pitch / G_BK;
+    auto sbase = [](const char* p) {  // a wave-uniform pointer in scalar registers
+        const uint64_t u = reinterpret_cast<uint64_t>(p);
+        return reinterpret_cast<const char*>((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u) |
+                                             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32))
+                                              << 32));
+    };
+    // global_load_lds with the K-tile's base in scalar registers and the lane's
+    // 32-bit offset in a VGPR (saddr + voffset addressing)
+    // piece i of K-tile t into buf (i < 4: A, else B)
+    auto piece = [&](int t, uint8_t* buf, int i) {
+        const char* src = sbase((i < 4 ? abase + (int64_t)t * astep : bbase + (int64_t)t * bstep)) + poff[i];
+        uint8_t* dst = buf + (i < 4 ? 0 : G_BM * 128) + (wv * 4 + (i & 3)) * 1024;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src), (__attribute__((address_space(3))) void*)dst,
+                                         16, 0, 0);
+    };
+    auto issue = [&](int t, uint8_t* buf) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) piece(t, buf, i);
+    };
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // fragment of a 32-row block at k-step ks (16 deep): row lane & 31, chunk
+    // 2 ks + lane / 32; the block's first row is a multiple of 32, so the
+    // swizzle is ((lane & 31) >> 1) & 7
+    const int sw = ((lane & 31) >> 1) & 7;
+    int foff[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) foff[ks] = (lane & 31) * 128 + (((2 * ks + (lane >> 5)) ^ sw) << 4);
+    const int arow = wm * 128 * 128, brow = G_BM * 128 + wn * 64 * 128;
+    // One K-tile per wave: 4 k-steps of 8 MFMAs (4 query blocks x 2 row blocks of
+    // 32); the next k-step's 6 fragments are read before this k-step's MFMAs
+    // (48 fragment registers live at most); sched_barrier keeps the steps apart
+    // so the scheduler cannot hoist every read of the tile.
+    // compute(buf, t, nbuf): multiply the K-tile in buf; with t >= 0 the 8 DMA
+    // pieces of K-tile t into nbuf go out two per k-step, between its MFMAs, so
+    // the vector-memory path drains while the wave keeps issuing MFMAs
+    auto compute = [&](const uint8_t* buf, int tn, uint8_t* nbuf) {
+        f16x8 fa[2][4], fb[2][2];
+        auto ld = [&](int ks, int slot) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                fa[slot][m] = *reinterpret_cast<const f16x8*>(buf + arow + m * 32 * 128 + foff[ks]);
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+                fb[slot][n] = *reinterpret_cast<const f16x8*>(buf + brow + n * 32 * 128 + foff[ks]);
+        };
+        auto mma = [&](int slot, int m0) {
+#pragma unroll
+            for (int m = m0; m < m0 + 2; ++m)
+#pragma unroll
+                for (int n = 0; n < 2; ++n)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[slot][m], fb[slot][n], acc[m][n], 0, 0, 0);
+        };
+        ld(0, 0);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (ks + 1 < 4) ld(ks + 1, (ks + 1) & 1);
+            mma(ks & 1, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (DIAG < 3 && tn >= 0) {
+                piece(tn, nbuf, 2 * ks);
+                piece(tn, nbuf, 2 * ks + 1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            mma(ks & 1, 2);
+        }
+    };
+    constexpr int VMCNT0 = 0x0F70;  // s_waitcnt vmcnt(0) (lgkm / exp counters untouched)
+    auto sync = [&]() {
+        if (DIAG < 2) {
+            __builtin_amdgcn_s_waitcnt(VMCNT0);
+            __builtin_amdgcn_s_barrier();
+        }
+    };
+    if (DIAG < 3) issue(0, L0);
+    __builtin_amdgcn_s_waitcnt(VMCNT0);
+    __builtin_amdgcn_s_barrier();
+    // pairs of K-tiles (L0 then L1); an odd last K-tile runs after the loop (one
+    // loop exit keeps the accumulators in one register assignment)
+    int t = 0;
+    for (; t + 1 < nkt; t += 2) {  // (the DMA issued up front: spreading it over the k-steps measured slower)
+        if (DIAG < 3) issue(t + 1, L1);
+        compute(L0, -1, L1);
+        sync();
+        if (DIAG < 3 && t + 2 < nkt) issue(t + 2, L0);
+        compute(L1, -1, L0);
+        sync();
+    }
+    if (t < nkt) compute(L0, -1, L1);
+    if constexpr (DIAG > 0) {
+        __builtin_amdgcn_s_waitcnt(VMCNT0);  // no DMA may land after the workgroup ends
+        float keep = 0.f;                    // keeps the MFMAs live
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) keep += acc[i][j][r];
+        __syncthreads();
+        if (tid == 0) a.region_cnt[logical] = keep == -1.0e38f ? 1 : 0;
+        return;
+    }
+    // accumulator acc[mb][nb] (32 x 32): column = lane & 31 (base row), row =
+    // (r & 3) + 8 (r >> 2) + 4 (lane >> 5) (query)
+    const int li = lane & 31, lh = lane >> 5;
+    if constexpr (EPI == 0) {
+        const int64_t col0 = a.nsample_tiles > 0 ? nt * G_BN : n0;  // sample: compact columns
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const int ro = wn * 64 + nb * 32 + li;
+            const int64_t xr = n0 + ro;
+            if (xr >= a.N) continue;
+            const bool xok = !(a.dead && a.dead[xr]);
+            const float xn = a.xnorm[xr], xi = a.xinv[xr];
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t qr = q0 + wm * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (qr >= a.B) continue;
+                    float sc = split_score(RING_H1, a.metric, acc[mb][nb][r], xi, a.qinv[qr], a.qnorm[qr], xn);
+                    if (!xok) sc = __int_as_float(0x7f800000);
+                    a.scores[(size_t)qr * a.ldS + col0 + ro] = sc;
+                }
+        }
+    } else {
+        // the fused filter of k_scores_ring (same constants, same test, same entries)
+        bool rok[2];
+        float w0[2], w1[2];
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const int64_t xr = n0 + wn * 64 + nb * 32 + li;
+            rok[nb] = xr < a.N && !(a.dead && a.dead[xr]);
+            const int64_t xc = xr < a.N ? xr : a.N - 1;
+            const float xi = a.xinv[xc], xn = a.xnorm[xc];
+            if (a.metric == COSINE) {
+                w0[nb] = xn / xi;
+                w1[nb] = 0.f;
+            } else {
+                w0[nb] = 1.f / xi;
+                w1[nb] = xn * xn * 0.5f * (1.0f - 0x1p-20f) / xi;
+            }
+        }
+        uint2* reg = a.region + logical * (int64_t)a.rcap;
+        unsigned long long rokm[2];
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) rokm[nb] = __builtin_amdgcn_ballot_w64(rok[nb]);
+        auto epi = [&](auto cos_tag) {
+            constexpr bool COS = decltype(cos_tag)::value;
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+                for (int r4 = 0; r4 < 4; ++r4) {
+                    const int64_t qb = q0 + wm * 128 + mb * 32 + 8 * r4 + 4 * lh;  // 4 consecutive queries
+                    const float4 c4 = *reinterpret_cast<const float4*>(a.ring_c + qb);
+                    const float cq[4] = {c4.x, c4.y, c4.z, c4.w};
+                    float sq[4] = {0.f, 0.f, 0.f, 0.f};
+                    if constexpr (!COS) {
+                        const float4 s4 = *reinterpret_cast<const float4*>(a.ring_s + qb);
+                        sq[0] = s4.x, sq[1] = s4.y, sq[2] = s4.z, sq[3] = s4.w;
+                    }
+#pragma unroll
+                    for (int r1 = 0; r1 < 4; ++r1) {
+#pragma unroll
+                        for (int nb = 0; nb < 2; ++nb) {
+                            const int r = r4 * 4 + r1;
+                            const float v = acc[mb][nb][r];
+                            float t;
+                            if constexpr (COS)
+                                t = fmaf(-cq[r1], w0[nb], v);
+                            else
+                                t = v - fmaf(cq[r1], w0[nb], w1[nb] * sq[r1]);
+                            const unsigned long long m = __builtin_amdgcn_ballot_w64(!(t < 0.f)) & rokm[nb];
+                            if (m) {
+                                const bool pass = (m >> lane) & 1ull;
+                                const int first = __ffsll((long long)m) - 1;
+                                int base = 0;
+                                if (lane == first) base = atomicAdd(tile_ctr, __popcll(m));
+                                base = __shfl(base, first, 64);
+                                if (pass) {
+                                    const int e = base + __builtin_amdgcn_mbcnt_hi(
+                                                             (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                                    const int qo = wm * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                                    const int ro = wn * 64 + nb * 32 + li;
+                                    if (e < a.rcap)
+                                        reg[e] = make_uint2((uint32_t)ro | ((uint32_t)qo << 16), __float_as_uint(v));
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        };
+        if (a.metric == COSINE)
+            epi(std::true_type{});
+        else
+            epi(std::false_type{});
+        __syncthreads();
+        if (tid == 0) a.region_cnt[logical] = *tile_ctr;
+    }
+}
+
+template <int EPI, int DIAG = 0>
+static int launch_h1_gemm_t(const ExactArgs& a, hipStream_t s) {
+    if (a.pitch % G_BK) return -5;
+    if ((3 * std::max(a.ldQs, a.ldXs) + G_BM) * 32 >= ((int64_t)1 << 32)) return -5;  // per-lane 32-bit DMA offsets
+    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
+    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
+    hipLaunchKernelGGL((k_h1_gemm<EPI, DIAG>), dim3((unsigned)(nqt * nnt)), dim3(512), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------
+// k_h1_stream: k_h1_gemm's 256 x 256 block tile (8 waves of 128 x 64 on
+// v_mfma_f32_32x32x16_f16) as a persistent stream.  One workgroup per CU walks
+// its tiles back to back, and the LDS-DMA runs as one ring of 32-deep stages
+// over all of them: stage s + 3 (possibly of the next tile) streams in while
+// stage s is multiplied, and a tile's epilogue runs while the first stages of
+// the next tile are already in flight -- no per-tile prologue, no per-tile
+// launch, no exposed epilogue latency beyond its own instructions.
+//   ring: 4 stages x 32 KiB (A 256 rows then B 256 rows, 64-B rows = 32 halves
+//         of K); 16-B chunk kc of image row r sits at slot kc ^ ((r >> 2) & 3),
+//         so each 16-lane group of a fragment ds_read_b128 (rows {0-3, 12-15,
+//         20-27} / {4-11, 16-19, 28-31} of a 32-row block) hits 16 distinct slots.
+//   DMA:  a piece = 16 image rows x 64 B (1 KiB, one global_load_lds_dwordx4);
+//         per stage and wave 2 A + 2 B pieces, issued 2 per k-step between the
+//         MFMAs; lane l loads row 16 P + l / 4, slot l % 4, i.e. chunk
+//         kc = (l % 4) ^ ((l / 16) % 4) -- two 512-B runs of the 16-blocked planes.
+//   sync: per stage one counted vmcnt (the 2 younger stages stay in flight) and
+//         one s_barrier.  The fragment reads are inline ds_read_b128 with a
+//         tied s_waitcnt lgkmcnt(0) before their MFMAs: the compiler sees no LDS
+//         read of the ring, so it adds no vmcnt(0) for the DMA it cannot track
+//         through the ring's dynamic stage index.
+// Tile order: XCD x owns the contiguous logical range of k_h1_gemm (query tiles
+// fastest); its wx workgroups take every wx-th tile of it, so at any time the
+// XCD's CUs work on wx consecutive tiles (wx / nqt row tiles, each read from
+// HBM once into that XCD's L2).  DIAG as k_h1_gemm's (exact_tile 15-17).
+// ---------------------------------------------------------------------------
+constexpr int S_NB = 4, S_SK = 32;
+constexpr int S_BUF = (G_BM + G_BN) * S_SK * 2;  // 32 KiB per stage
+
+#define MH_DSR(dst, addr, off) asm volatile("ds_read_b128 %0, %1 offset:" #off : "=v"(dst) : "v"(addr))
+#define MH_LGKM0(f0, f1, f2, f3, f4, f5) \
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3), "+v"(f4), "+v"(f5))
+
+template <int EPI, int DIAG = 0>
+__global__ __launch_bounds__(512) void k_h1_stream(ExactArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[S_NB * S_BUF];
+    __shared__ int tile_ctr;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
+    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
+    const int64_t nblk = nqt * nnt;
+    const int W = gridDim.x, xcd = blockIdx.x % 8, jx = blockIdx.x / 8;
+    const int wx = W / 8 + (xcd < W % 8 ? 1 : 0);
+    const int64_t per = nblk / 8, rem = nblk % 8;
+    const int64_t lo = xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per;
+    const int64_t hi = lo + per + (xcd < rem ? 1 : 0);
+    const int64_t first = lo + jx;
+    const int64_t ntile = first < hi ? (hi - first + wx - 1) / wx : 0;
+    const int nkt = a.pitch / S_SK;
+    const int64_t S = ntile * nkt;
+    if (EPI == 1 && tid == 0) tile_ctr = 0;
+
+    // per-lane DMA constants: piece i (0, 1) of this wave = image rows
+    // 16 (2 wv + i) + lane / 4; chunk kc of the stage's 32 halves = K-block kc / 2
+    // (16-deep planes, 32 B per row), half kc % 2
+    const int kc = (lane & 3) ^ ((lane >> 4) & 3);
+    const uint32_t pkA = (uint32_t)((kc >> 1) * a.ldQs * 32 + (kc & 1) * 16);
+    const uint32_t pkB = (uint32_t)((kc >> 1) * a.ldXs * 32 + (kc & 1) * 16);
+    const int rr0 = wv * 32 + (lane >> 2);  // piece 1: + 16
+    const int64_t astep = a.ldQs * 64, bstep = a.ldXs * 64;  // bytes per stage (2 K-blocks)
+    auto sbase = [](const char* p) {
+        const uint64_t u = reinterpret_cast<uint64_t>(p);
+        return reinterpret_cast<const char*>((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u) |
+                                             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32))
+                                              << 32));
+    };
+    // producer: the stage being streamed in (tile p_tile of this workgroup, K-stage p_kt)
+    int64_t p_tile = 0;
+    int p_kt = 0;
+    const char *p_a = nullptr, *p_b = nullptr;
+    int p_la = 0, p_lb = 0;  // last valid image row of the tile (rows past B / N clamp to it)
+    auto p_set = [&]() {
+        const int64_t L = first + p_tile * wx;
+        const int64_t qt = L % nqt, nt = L / nqt;
+        const int64_t q0 = qt * G_BM;
+        const int64_t n0 = (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
+        p_a = reinterpret_cast<const char*>(a.Qh + q0 * X3K);
+        p_b = reinterpret_cast<const char*>(a.Xh + n0 * X3K);
+        p_la = (int)min<int64_t>(G_BM - 1, a.B - 1 - q0);
+        p_lb = (int)min<int64_t>(G_BN - 1, a.N - 1 - n0);
+    };
+    // piece i of the producer stage into ring stage slot `st`: 0, 1 A; 2, 3 B
+    auto piece = [&](int st, int i) {
+        const bool isA = i < 2;
+        const int rr = rr0 + (i & 1) * 16;
+        const char* base = sbase((isA ? p_a + (int64_t)p_kt * astep : p_b + (int64_t)p_kt * bstep));
+        const uint32_t off = (isA ? pkA : pkB) + (uint32_t)min(rr, isA ? p_la : p_lb) * 32;
+        uint8_t* dst = ring + st * S_BUF + (isA ? 0 : G_BM * 64) + (wv * 2 + (i & 1)) * 1024;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + off),
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    };
+    auto p_next = [&]() {
+        if (++p_kt == nkt) {
+            p_kt = 0;
+            if (++p_tile < ntile) p_set();
+        }
+    };
+
+    f32x16 acc[4][2];
+    auto zero = [&]() {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    };
+    zero();
+    // fragment addresses: row lane & 31 of a 32-row block, chunk 2 ks + lane / 32
+    // at slot chunk ^ (((lane & 31) >> 2) & 3); blocks at +2048 B
+    const uint32_t ring_lds = (uint32_t)reinterpret_cast<uintptr_t>(ring);
+    const int sw = ((lane & 31) >> 2) & 3;
+    const uint32_t lo0 = (lane & 31) * 64 + (((lane >> 5) ^ sw) << 4);
+    const uint32_t lo1 = (lane & 31) * 64 + (((2 + (lane >> 5)) ^ sw) << 4);
+    const uint32_t offA = wm * 128 * 64, offB = G_BM * 64 + wn * 64 * 64;
+    auto mma4 = [&](const f16x8* fa, const f16x8* fb, int m0) {
+#pragma unroll
+        for (int m = m0; m < m0 + 2; ++m)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+                acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+    };
+    // one stage: 2 k-steps of 8 MFMAs; the producer's 4 pieces go out 2 per k-step
+    auto compute = [&](int st, bool issue, int pst) {
+        const uint32_t rb = ring_lds + st * S_BUF;
+        const uint32_t va0 = rb + offA + lo0, vb0 = rb + offB + lo0, va1 = rb + offA + lo1, vb1 = rb + offB + lo1;
+        f16x8 fa0[4], fb0[2], fa1[4], fb1[2];
+        MH_DSR(fa0[0], va0, 0);
+        MH_DSR(fa0[1], va0, 2048);
+        MH_DSR(fa0[2], va0, 4096);
+        MH_DSR(fa0[3], va0, 6144);
+        MH_DSR(fb0[0], vb0, 0);
+        MH_DSR(fb0[1], vb0, 2048);
+        MH_LGKM0(fa0[0], fa0[1], fa0[2], fa0[3], fb0[0], fb0[1]);
+        MH_DSR(fa1[0], va1, 0);
+        MH_DSR(fa1[1], va1, 2048);
+        MH_DSR(fa1[2], va1, 4096);
+        MH_DSR(fa1[3], va1, 6144);
+        MH_DSR(fb1[0], vb1, 0);
+        MH_DSR(fb1[1], vb1, 2048);
+        __builtin_amdgcn_sched_barrier(0);
+        mma4(fa0, fb0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (DIAG < 3 && issue) {
+            piece(pst, 0);
+            piece(pst, 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma4(fa0, fb0, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        MH_LGKM0(fa1[0], fa1[1], fa1[2], fa1[3], fb1[0], fb1[1]);
+        mma4(fa1, fb1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (DIAG < 3 && issue) {
+            piece(pst, 2);
+            piece(pst, 3);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma4(fa1, fb1, 2);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    const int li = lane & 31, lh = lane >> 5;
+    float keep = 0.f;  // DIAG: keeps the MFMAs live
+    // the epilogue of the consumer's tile L (accumulator acc[mb][nb]: column =
+    // lane & 31 (base row), row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) (query))
+    auto epilogue = [&](int64_t L) {
+        const int64_t qt = L % nqt, nt = L / nqt;
+        const int64_t q0 = qt * G_BM;
+        const int64_t n0 = (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
+        if constexpr (DIAG > 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) keep += acc[i][j][r];
+        } else if constexpr (EPI == 0) {
+            const int64_t col0 = a.nsample_tiles > 0 ? nt * G_BN : n0;  // sample: compact columns
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                const int ro = wn * 64 + nb * 32 + li;
+                const int64_t xr = n0 + ro;
+                if (xr >= a.N) continue;
+                const bool xok = !(a.dead && a.dead[xr]);
+                const float xn = a.xnorm[xr], xi = a.xinv[xr];
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int64_t qr = q0 + wm * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                        if (qr >= a.B) continue;
+                        float sc = split_score(RING_H1, a.metric, acc[mb][nb][r], xi, a.qinv[qr], a.qnorm[qr], xn);
+                        if (!xok) sc = __int_as_float(0x7f800000);
+                        a.scores[(size_t)qr * a.ldS + col0 + ro] = sc;
+                    }
+            }
+        } else {
+            // the fused filter of k_scores_ring (same constants, same test, same entries)
+            bool rok[2];
+            float w0[2], w1[2];
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                const int64_t xr = n0 + wn * 64 + nb * 32 + li;
+                rok[nb] = xr < a.N && !(a.dead && a.dead[xr]);
+                const int64_t xc = xr < a.N ? xr : a.N - 1;
+                const float xi = a.xinv[xc], xn = a.xnorm[xc];
+                if (a.metric == COSINE) {
+                    w0[nb] = xn / xi;
+                    w1[nb] = 0.f;
+                } else {
+                    w0[nb] = 1.f / xi;
+                    w1[nb] = xn * xn * 0.5f * (1.0f - 0x1p-20f) / xi;
+                }
+            }
+            uint2* reg = a.region + L * (int64_t)a.rcap;
+            // the entry keys below are loop-invariant: laundering the lane id keeps
+            // the compiler from hoisting all 128 of them out of the stream (spills)
+            int lid = lane;
+            asm volatile("" : "+v"(lid));
+            const int eli = lid & 31, elh = lid >> 5;
+            unsigned long long rokm[2];
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) rokm[nb] = __builtin_amdgcn_ballot_w64(rok[nb]);
+            auto epi = [&](auto cos_tag) {
+                constexpr bool COS = decltype(cos_tag)::value;
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+                    for (int r4 = 0; r4 < 4; ++r4) {
+                        const int64_t qb = q0 + wm * 128 + mb * 32 + 8 * r4 + 4 * lh;  // 4 consecutive queries
+                        const float4 c4 = *reinterpret_cast<const float4*>(a.ring_c + qb);
+                        const float cq[4] = {c4.x, c4.y, c4.z, c4.w};
+                        float sq[4] = {0.f, 0.f, 0.f, 0.f};
+                        if constexpr (!COS) {
+                            const float4 s4 = *reinterpret_cast<const float4*>(a.ring_s + qb);
+                            sq[0] = s4.x, sq[1] = s4.y, sq[2] = s4.z, sq[3] = s4.w;
+                        }
+#pragma unroll
+                        for (int r1 = 0; r1 < 4; ++r1) {
+#pragma unroll
+                            for (int nb = 0; nb < 2; ++nb) {
+                                const int r = r4 * 4 + r1;
+                                const float v = acc[mb][nb][r];
+                                float t;
+                                if constexpr (COS)
+                                    t = fmaf(-cq[r1], w0[nb], v);
+                                else
+                                    t = v - fmaf(cq[r1], w0[nb], w1[nb] * sq[r1]);
+                                const unsigned long long m = __builtin_amdgcn_ballot_w64(!(t < 0.f)) & rokm[nb];
+                                if (m) {
+                                    const bool pass = (m >> lane) & 1ull;
+                                    const int fl = __ffsll((long long)m) - 1;
+                                    int base = 0;
+                                    if (lane == fl) base = atomicAdd(&tile_ctr, __popcll(m));
+                                    base = __shfl(base, fl, 64);
+                                    if (pass) {
+                                        const int e = base + __builtin_amdgcn_mbcnt_hi(
+                                                                 (uint32_t)(m >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                                        const int qo = wm * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * elh;
+                                        const int ro = wn * 64 + nb * 32 + eli;
+                                        if (e < a.rcap)
+                                            reg[e] = make_uint2((uint32_t)ro | ((uint32_t)qo << 16), __float_as_uint(v));
+                                    }
+                                }
+                            }
+                        }
+                    }
+                }
+            };
+            if (a.metric == COSINE)
+                epi(std::true_type{});
+            else
+                epi(std::false_type{});
+            __syncthreads();
+            if (tid == 0) {
+                a.region_cnt[L] = tile_ctr;
+                tile_ctr = 0;  // the next tile's atomics come after at least one more barrier
+            }
+        }
+    };
+
+    constexpr int VMCNT0 = 0x0F70, VMCNT8 = 0x0F78;  // s_waitcnt vmcnt(0) / vmcnt(8) = 2 stages x 4 pieces
+    static_assert(S_NB == 4, "VMCNT8 is 4 x (S_NB - 2)");
+    if (ntile > 0) p_set();
+    int64_t ps = 0;  // stages issued
+    for (; ps < S_NB - 1 && ps < S; ++ps) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (DIAG < 3) piece((int)ps, i);
+        p_next();
+    }
+    int64_t c_tile = 0;
+    int c_kt = 0;
+    for (int64_t s = 0; s < S; ++s) {
+        if (DIAG < 2) {
+            if (s + S_NB - 2 < S)
+                __builtin_amdgcn_s_waitcnt(VMCNT8);
+            else
+                __builtin_amdgcn_s_waitcnt(VMCNT0);
+            __builtin_amdgcn_s_barrier();
+        }
+        const bool issue = ps < S;
+        __builtin_amdgcn_s_setprio(1);
+        compute((int)(s & (S_NB - 1)), issue, (int)(ps & (S_NB - 1)));
+        __builtin_amdgcn_s_setprio(0);
+        if (issue) {
+            p_next();
+            ++ps;
+        }
+        if (++c_kt == nkt) {
+            epilogue(first + c_tile * wx);
+            zero();
+            c_kt = 0;
+            ++c_tile;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(VMCNT0);  // no DMA may land after the workgroup ends
+    if constexpr (DIAG > 0) {
+        __syncthreads();
+        if (tid == 0 && blockIdx.x < nblk) a.region_cnt[blockIdx.x] = keep == -1.0e38f ? 1 : 0;
+    }
+}
+#undef MH_DSR
+#undef MH_LGKM0
+
+static int device_cus() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            cus = v;
+        else
+            cus = 256;
+    }
+    return cus;
+}
+
+template <int EPI, int DIAG = 0>
+static int launch_h1_stream_t(const ExactArgs& a, hipStream_t s) {
+    if (a.pitch % S_SK) return -5;
+    if ((a.ldQs + G_BM) * 32 >= ((int64_t)1 << 32) || (a.ldXs + G_BN) * 32 >= ((int64_t)1 << 32))
+        return -5;  // per-lane 32-bit DMA offsets
+    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
+    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
+    const int64_t nblk = nqt * nnt;
+    const int64_t W = std::min<int64_t>(nblk, std::max(8, device_cus() / 8 * 8));
+    hipLaunchKernelGGL((k_h1_stream<EPI, DIAG>), dim3((unsigned)W), dim3(512), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------
+// k_h1_pp: the 256 x 256 fp16 1-product tile as a persistent, two-group
+// ping-pong stream.  Waves 0-3 (group 0, query rows 0-127) and 4-7 (group 1,
+// rows 128-255) each hold one wave on every SIMD; group 1 runs one barrier
+// behind group 0, so in every barrier interval one wave of a SIMD multiplies
+// (8 x v_mfma_f32_32x32x16_f16, s_setprio 1) while the other reads its next
+// fragments and issues its share of the LDS-DMA, and the roles swap at the
+// barrier.  Per wave and K-slice (16 deep):
+//   R: 6 ds_read_b128 (4 A, 2 B fragments) from the slice's ring slot, 2 DMA
+//      pieces of slice x + D (group 0 the A image, group 1 the B image), barrier
+//   M: lgkmcnt(0), 8 MFMAs, the tile's epilogue after its last slice, barrier
+// The counted vmcnt(2 (D - 1)) before the barrier that precedes group 0's R
+// phase (group 0: end of M, group 1: end of R) retires slice x + 1 for every
+// wave while D - 1 younger slices stay in flight across the barriers.
+//   ring: NS slots of one K-slice (16 KiB: A 256 rows x 32 B, then B); chunk c
+//         of image row r at slot c ^ ((r >> 3) & 1): the four 16-lane groups of
+//         a fragment read (rows {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31})
+//         hit 16 distinct 16-B slots of the bank row.
+//   DMA:  a piece = 32 image rows x 32 B = one contiguous 1 KiB run of the
+//         16-blocked plane (lane l: row 32 P + l / 2, chunk (l & 1) ^ ((l >> 4) & 1)).
+//   WAR:  slice x + D overwrites the slot of slice x + D - NS, whose last reads
+//         (group 1) retired two barrier intervals earlier: NS >= D + 2.
+// The EPI 1 filter has no barrier of its own (the groups are out of step): each
+// wave appends to its own eighth of the tile's region, region_cnt[8 L + wave].
+// Tile order as k_h1_stream.  DIAG: 1 no epilogue, 3 no DMA.
+// ---------------------------------------------------------------------------
+// s_waitcnt vmcnt(v) (6-bit count: bits 3:0 and 15:14; lgkm / exp untouched)
+constexpr int vmcnt_imm(int v) { return 0x0F70 | (v & 15) | (((v >> 4) & 3) << 14); }
+// s_waitcnt vmcnt(BASE + extra) for a wave-uniform extra in [0, sizeof...(I)); a
+// larger extra waits vmcnt(BASE) (more than needed, never less)
+template <int BASE, int... I>
+__device__ __forceinline__ void wait_vm_plus(int extra, std::integer_sequence<int, I...>) {
+    const bool done = ((extra == I ? (__builtin_amdgcn_s_waitcnt(vmcnt_imm(BASE + I)), true) : false) || ...);
+    if (!done) __builtin_amdgcn_s_waitcnt(vmcnt_imm(BASE));
+}
+
+#define MH_DSR(dst, addr, off) asm volatile("ds_read_b128 %0, %1 offset:" #off : "=v"(dst) : "v"(addr))
+#define MH_LGKM0(f0, f1, f2, f3, f4, f5) \
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3), "+v"(f4), "+v"(f5))
+
+template <int EPI, int DIAG, int NS, int D, int PS>
+__global__ __launch_bounds__(512) void k_h1_pp(ExactArgs a) {
+    static_assert(NS >= D + 2 && D >= 1, "ring depth");
+    static_assert(PS == 1 || PS == 2, "slice depth 16 or 32");
+    constexpr int RB = 32 * PS;                // image row bytes (16 PS halves of K)
+    constexpr int SL = (G_BM + G_BN) * RB;     // one slice: A then B image
+    constexpr int CPR = 2 * PS, RPP = 32 / PS;  // 16-B chunks per row, rows per 1-KiB piece
+    // EPI 1: per tile (double-buffered by tile parity) the filter constants, by
+    // LDS-DMA: 256 rows x {w0, w1, dead, -} (4 KiB), then c and s of 256 queries
+    constexpr int CST = 6144, CSTB = NS * SL;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[NS * SL + (EPI == 1 ? 2 * CST : 0)];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int g = __builtin_amdgcn_readfirstlane(wr);
+    const int wcs = __builtin_amdgcn_readfirstlane(wc);
+    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
+    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
+    const int64_t nblk = nqt * nnt;
+    const int W = gridDim.x, xcd = blockIdx.x % 8, jx = blockIdx.x / 8;
+    const int wx = W / 8 + (xcd < W % 8 ? 1 : 0);
+    const int64_t per = nblk / 8, rem = nblk % 8;
+    const int64_t lo = xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per;
+    const int64_t hi = lo + per + (xcd < rem ? 1 : 0);
+    const int64_t first = lo + jx;
+    const int64_t ntile = first < hi ? (hi - first + wx - 1) / wx : 0;
+    const int nkt = a.pitch / (X3K * PS);  // K-slices per tile
+    const int64_t S = ntile * nkt;
+    if (S == 0) return;  // uniform over the workgroup
+
+    // DMA: this wave's 2 PS pieces of a slice's A (group 0) or B (group 1) image;
+    // lane l: row RPP P + l / CPR, chunk (l % CPR) ^ swizzle(row) = K-block c / 2, half c % 2
+    const int rr0 = wcs * 2 * PS * RPP + lane / CPR;  // piece i: + RPP i
+    const int64_t ld = g == 0 ? a.ldQs : a.ldXs;
+    const int dc = (lane % CPR) ^ (PS == 1 ? (lane >> 4) & 1 : (lane >> 4) & 3);
+    const uint32_t pk = (uint32_t)((dc >> 1) * ld * 32 + (dc & 1) * 16);
+    const char* const plane = reinterpret_cast<const char*>(g == 0 ? a.Qh : a.Xh);
+    auto sbase = [](const char* p) {
+        const uint64_t u = reinterpret_cast<uint64_t>(p);
+        return reinterpret_cast<const char*>((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u) |
+                                             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32))
+                                              << 32));
+    };
+    int64_t p_tile = 0;
+    int p_kt = 0, p_slot = 0;
+    const char* p_base = nullptr;  // the producer tile's first row in K-block 0
+    int p_lim = 0;                 // its last valid image row (rows past B / N clamp to it)
+    auto p_set = [&]() {
+        const int64_t L = first + p_tile * wx;
+        const int64_t qt = L % nqt, nt = L / nqt;
+        const int64_t r0 = g == 0 ? qt * G_BM : (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
+        p_base = plane + r0 * 32;
+        p_lim = (int)min<int64_t>(255, (g == 0 ? a.B : a.N) - 1 - r0);
+    };
+    auto produce = [&]() {  // this wave's pieces of the producer slice, then advance it
+        if (DIAG < 3) {
+            const char* base = sbase(p_base + (int64_t)p_kt * PS * ld * 32);
+#pragma unroll
+            for (int i = 0; i < 2 * PS; ++i) {
+                const uint32_t off = (uint32_t)min(rr0 + RPP * i, p_lim) * 32 + pk;
+                uint8_t* dst = ring + p_slot * SL + g * (G_BM * RB) + (wcs * 2 * PS + i) * 1024;
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + off),
+                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+            }
+        }
+        if (++p_slot == NS) p_slot = 0;
+        if (++p_kt == nkt) {
+            p_kt = 0;
+            if (++p_tile < ntile) p_set();
+        }
+    };
+
+    f32x16 acc[4][2];
+    const f32x16 zacc = {};  // a tile's first MFMAs accumulate onto zero (no clearing pass)
+    const uint32_t ring_lds = (uint32_t)reinterpret_cast<uintptr_t>(ring);
+    // fragment of k-step j: row lane & 31 of a 32-row block, chunk 2 j + lane / 32
+    const int fsw = PS == 1 ? ((lane & 31) >> 3) & 1 : ((lane & 31) >> 2) & 3;
+    const uint32_t lfix0 = (lane & 31) * RB + (((lane >> 5) ^ fsw) << 4);
+    const uint32_t lfix1 = (lane & 31) * RB + (((2 + (lane >> 5)) ^ fsw) << 4);
+    const uint32_t offA = wr * 128 * RB, offB = G_BM * RB + wc * 64 * RB;
+    const int li = lane & 31, lh = lane >> 5;
+    float keep = 0.f;
+    // vector-memory ops this wave issued since its last counted wait besides the
+    // slice pieces (filter-constant DMA, region stores): with D = 2 they are all
+    // younger than the slice the next wait retires, so that wait adds them to its
+    // count instead of draining them
+    int nst = 0;
+
+    auto epilogue = [&](int64_t L, int64_t ctile) {
+        const int64_t qt = L % nqt, nt = L / nqt;
+        const int64_t q0 = qt * G_BM;
+        const int64_t n0 = (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
+        if constexpr (DIAG == 1) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) keep += acc[i][j][r];
+        } else if constexpr (EPI == 0) {
+            const int64_t col0 = a.nsample_tiles > 0 ? nt * G_BN : n0;  // sample: compact columns
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                const int ro = wc * 64 + nb * 32 + li;
+                const int64_t xr = n0 + ro;
+                if (xr >= a.N) continue;
+                const bool xok = !(a.dead && a.dead[xr]);
+                const float xn = a.xnorm[xr], xi = a.xinv[xr];
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int64_t qr = q0 + wr * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                        if (qr >= a.B) continue;
+                        float sc = split_score(RING_H1, a.metric, acc[mb][nb][r], xi, a.qinv[qr], a.qnorm[qr], xn);
+                        if (!xok) sc = __int_as_float(0x7f800000);
+                        a.scores[(size_t)qr * a.ldS + col0 + ro] = sc;
+                    }
+            }
+        } else {
+            // the fused filter of k_scores_ring (same constants, same test, same
+            // entries).  Constants from LDS (staged by DMA at the tile's first
+            // slice); per 32 x 32 block the 16 tests OR their ballots, and only a
+            // block with a passing pair takes the append path.
+            const uint32_t cb = ring_lds + CSTB + (uint32_t)(ctile & 1) * CST;
+            f32x4 xw[2];
+            asm volatile("ds_read_b128 %0, %1" : "=v"(xw[0]) : "v"(cb + (uint32_t)(wc * 64 + li) * 16));
+            asm volatile("ds_read_b128 %0, %1" : "=v"(xw[1]) : "v"(cb + (uint32_t)(wc * 64 + 32 + li) * 16));
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xw[0]), "+v"(xw[1]));
+            __builtin_amdgcn_sched_barrier(0);
+            bool rok[2];
+            unsigned long long rokm[2];
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                rok[nb] = n0 + wc * 64 + nb * 32 + li < a.N && xw[nb][2] == 0.f;
+                rokm[nb] = __builtin_amdgcn_ballot_w64(rok[nb]);
+            }
+            // this wave's eighth of the region: cap entries, then one trash slot that
+            // the lanes without an entry store to (every append is one store
+            // instruction with all lanes on: the count of them is exact)
+            const int cap = a.rcap / 8 - 1;
+            uint2* reg = a.region + (L * 8 + wave) * (int64_t)(cap + 1);
+            int cnt = 0;  // wave-uniform
+            // the entry keys below are loop-invariant: laundering the lane id keeps
+            // the compiler from hoisting all 128 of them out of the stream (spills)
+            int lid = lane;
+            asm volatile("" : "+v"(lid));
+            const int eli = lid & 31, elh = lid >> 5;
+            auto filt = [&](auto cos_tag) {
+                constexpr bool COS = decltype(cos_tag)::value;
+                auto test = [&](int mb, int nb, int r, const f32x4* c4, const f32x4* s4) {
+                    const float v = acc[mb][nb][r];
+                    const float cq = c4[r >> 2][r & 3];
+                    float t;
+                    if constexpr (COS)
+                        t = fmaf(-cq, xw[nb][0], v);
+                    else
+                        t = v - fmaf(cq, xw[nb][0], xw[nb][1] * s4[r >> 2][r & 3]);
+                    return !(t < 0.f);
+                };
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb) {
+                    __builtin_amdgcn_sched_barrier(0);  // one block's constants live at a time
+                    // queries wr 128 + mb 32 + 8 r4 + 4 lh + 0..3 (accumulator rows r = 4 r4 + 0..3)
+                    f32x4 c4[4], s4[4];
+                    const uint32_t qa = cb + 4096 + (uint32_t)(wr * 128 + mb * 32 + 4 * lh) * 4;
+                    asm volatile("ds_read_b128 %0, %1" : "=v"(c4[0]) : "v"(qa));
+                    asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(c4[1]) : "v"(qa));
+                    asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(c4[2]) : "v"(qa));
+                    asm volatile("ds_read_b128 %0, %1 offset:96" : "=v"(c4[3]) : "v"(qa));
+                    if constexpr (!COS) {
+                        asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(s4[0]) : "v"(qa));
+                        asm volatile("ds_read_b128 %0, %1 offset:1056" : "=v"(s4[1]) : "v"(qa));
+                        asm volatile("ds_read_b128 %0, %1 offset:1088" : "=v"(s4[2]) : "v"(qa));
+                        asm volatile("ds_read_b128 %0, %1 offset:1120" : "=v"(s4[3]) : "v"(qa));
+                        asm volatile("s_waitcnt lgkmcnt(0)"
+                                     : "+v"(c4[0]), "+v"(c4[1]), "+v"(c4[2]), "+v"(c4[3]), "+v"(s4[0]), "+v"(s4[1]),
+                                       "+v"(s4[2]), "+v"(s4[3]));
+                    } else {
+                        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c4[0]), "+v"(c4[1]), "+v"(c4[2]), "+v"(c4[3]));
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int nb = 0; nb < 2; ++nb) {
+                        unsigned long long any = 0;
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) any |= __builtin_amdgcn_ballot_w64(test(mb, nb, r, c4, s4));
+                        if (DIAG == 4) keep += (float)(any & rokm[nb]);  // diagnostic: the tests without the appends
+                        if (DIAG != 4 && (any & rokm[nb])) {
+#pragma unroll
+                            for (int r = 0; r < 16; ++r) {
+                                const bool pass = test(mb, nb, r, c4, s4) && rok[nb];
+                                const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
+                                if (m) {
+                                    const int e = cnt + (int)__builtin_amdgcn_mbcnt_hi(
+                                                            (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                                    const int qo = wr * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * elh;
+                                    const int ro = wc * 64 + nb * 32 + eli;
+                                    reg[pass && e < cap ? e : cap] = make_uint2((uint32_t)ro | ((uint32_t)qo << 16),
+                                                                                __float_as_uint(acc[mb][nb][r]));
+                                    ++nst;
+                                    cnt += __popcll(m);
+                                }
+                            }
+                        }
+                    }
+                }
+            };
+            if (a.metric == COSINE)
+                filt(std::true_type{});
+            else
+                filt(std::false_type{});
+            if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;
+            ++nst;
+            if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;
+        }
+    };
+
+    constexpr int VMC = vmcnt_imm(2 * PS * (D - 1));  // D - 1 slices (2 PS pieces each) stay in flight
+    static_assert(2 * PS * (D - 1) < 64, "vmcnt range");
+    constexpr int VMCNT0 = 0x0F70;
+    auto wait_vmc = [&]() {  // the counted wait: D - 1 slices (+ the extra ops, D = 2) stay in flight
+        if (D == 2 && nst > 0)
+            wait_vm_plus<2 * PS * (D - 1)>(nst, std::make_integer_sequence<int, 40>{});
+        else
+            __builtin_amdgcn_s_waitcnt(VMC);
+    };
+    // prologue: slices 0 .. D-1 (each wave its pieces), slice 0 landed everywhere
+    p_set();
+    int64_t ps = 0;
+    for (; ps < D && ps < S; ++ps) produce();
+    if (D <= S)
+        __builtin_amdgcn_s_waitcnt(VMC);
+    else
+        __builtin_amdgcn_s_waitcnt(VMCNT0);
+    __builtin_amdgcn_s_barrier();
+    if (g == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
+
+    int64_t c_tile = 0;
+    int c_kt = 0, c_slot = 0;
+    for (int64_t x = 0; x < S; ++x) {
+        // R: fragments of slice x, DMA of slice x + D
+        const uint32_t sb = ring_lds + (uint32_t)c_slot * SL;
+        if (++c_slot == NS) c_slot = 0;
+        f16x8 fa[PS][4], fb[PS][2];
+        {
+            const uint32_t va = sb + offA + lfix0, vb = sb + offB + lfix0;
+            if constexpr (PS == 1) {
+                MH_DSR(fa[0][0], va, 0);
+                MH_DSR(fa[0][1], va, 1024);
+                MH_DSR(fa[0][2], va, 2048);
+                MH_DSR(fa[0][3], va, 3072);
+                MH_DSR(fb[0][0], vb, 0);
+                MH_DSR(fb[0][1], vb, 1024);
+            } else {
+                const uint32_t va1 = sb + offA + lfix1, vb1 = sb + offB + lfix1;
+                MH_DSR(fa[0][0], va, 0);
+                MH_DSR(fa[0][1], va, 2048);
+                MH_DSR(fa[0][2], va, 4096);
+                MH_DSR(fa[0][3], va, 6144);
+                MH_DSR(fb[0][0], vb, 0);
+                MH_DSR(fb[0][1], vb, 2048);
+                MH_DSR(fa[PS - 1][0], va1, 0);
+                MH_DSR(fa[PS - 1][1], va1, 2048);
+                MH_DSR(fa[PS - 1][2], va1, 4096);
+                MH_DSR(fa[PS - 1][3], va1, 6144);
+                MH_DSR(fb[PS - 1][0], vb1, 0);
+                MH_DSR(fb[PS - 1][1], vb1, 2048);
+            }
+        }
+        if (EPI == 1 && DIAG < 3 && c_kt == 0) {
+            // the filter constants of this tile (read by its epilogue, nkt - 1 >= D
+            // slices later: retired by the counted waits in between)
+            const int64_t L = first + c_tile * wx;
+            const int64_t q0 = (L % nqt) * G_BM, n0 = (L / nqt) * G_BN;
+            uint8_t* cd = ring + CSTB + (int)(c_tile & 1) * CST;
+            const float* src;
+            uint8_t* dst;
+            if (g == 0) {
+                src = (wcs & 1 ? a.ring_s : a.ring_c) + q0 + lane * 4;
+                dst = cd + 4096 + (wcs & 1) * 1024;
+            } else {
+                src = reinterpret_cast<const float*>(a.xw + min<int64_t>(n0 + wcs * 64 + lane, a.N - 1));
+                dst = cd + wcs * 1024;
+            }
+            if (g == 1 || wcs < 2) {
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+                ++nst;
+            }
+        }
+        if (ps < S) {
+            produce();
+            ++ps;
+        }
+        const bool tail = x + 1 + D > S;  // fewer than D slices left in flight: retire them all
+        if (g == 1) {
+            if (tail)
+                __builtin_amdgcn_s_waitcnt(VMCNT0);
+            else
+                wait_vmc();
+            nst = 0;
+        }
+        __builtin_amdgcn_s_barrier();
+        // M: 8 PS MFMAs (+ the epilogue after a tile's last slice)
+#pragma unroll
+        for (int j = 0; j < PS; ++j) MH_LGKM0(fa[j][0], fa[j][1], fa[j][2], fa[j][3], fb[j][0], fb[j][1]);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        if (c_kt == 0) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int n = 0; n < 2; ++n)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0][m], fb[0][n], zacc, 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int n = 0; n < 2; ++n)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0][m], fb[0][n], acc[m][n], 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 1; j < PS; ++j)
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int n = 0; n < 2; ++n)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[j][m], fb[j][n], acc[m][n], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (++c_kt == nkt) {
+            epilogue(first + c_tile * wx, c_tile);
+            c_kt = 0;
+            ++c_tile;
+        }
+        if (g == 0) {
+            if (tail)
+                __builtin_amdgcn_s_waitcnt(VMCNT0);
+            else
+                wait_vmc();
+            nst = 0;
+        }
+        __builtin_amdgcn_s_barrier();
+    }
+    if (g == 0) __builtin_amdgcn_s_barrier();  // evens the barrier count
+    __builtin_amdgcn_s_waitcnt(VMCNT0);
+    if constexpr (DIAG == 1 || DIAG == 4) {
+        if (lane == 0 && keep == -1.0e38f) a.region_cnt[0] = 1;
+    }
+}
+#undef MH_DSR
+#undef MH_LGKM0
+
+template <int EPI, int DIAG = 0, int NS = 8, int D = 6, int PS = 1>
+static int launch_h1_pp_t(const ExactArgs& a, hipStream_t s) {
+    if (a.pitch % (X3K * PS)) return -5;
+    if ((PS - 1) * std::max(a.ldQs, a.ldXs) * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return -5;  // 32-bit DMA offsets
+    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
+    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
+    const int64_t nblk = nqt * nnt;
+    const int64_t W = std::min<int64_t>(nblk, std::max(8, device_cus() / 8 * 8));
+    hipLaunchKernelGGL((k_h1_pp<EPI, DIAG, NS, D, PS>), dim3((unsigned)W), dim3(512), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------
 // fp16 1-product path with the fused preselection (exact_precision 3)
 // ---------------------------------------------------------------------------
 // ring variants (exact_tile for precision 3; 0 = 5): 1 = 256 x 256, 32-deep stages,
@@ -689,8 +1737,25 @@ int launch_exact_scores_x2h(const ExactArgs& a, int tile, hipStream_t s) { retur
 template <int EPI>
 static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
     if (a.B <= 0 || a.N <= 0) return 0;
-    if (variant == 0) variant = 5;  // measured best on config 5 (profiles/r02_cfg5_*)
+    if (variant == 0) variant = 23;
     switch (variant) {
+        case 10: return launch_h1_gemm_t<EPI>(a, s);
+        case 11: return launch_h1_gemm_t<EPI, EPI ? 1 : 0>(a, s);
+        case 12: return launch_h1_gemm_t<EPI, EPI ? 2 : 0>(a, s);
+        case 13: return launch_h1_gemm_t<EPI, EPI ? 3 : 0>(a, s);
+        case 14: return launch_h1_stream_t<EPI>(a, s);
+        case 15: return launch_h1_stream_t<EPI, EPI ? 1 : 0>(a, s);
+        case 16: return launch_h1_stream_t<EPI, EPI ? 2 : 0>(a, s);
+        case 17: return launch_h1_stream_t<EPI, EPI ? 3 : 0>(a, s);
+        case 18: return launch_h1_pp_t<EPI>(a, s);
+        case 19: return launch_h1_pp_t<EPI, EPI ? 1 : 0>(a, s);
+        case 20: return launch_h1_pp_t<EPI, EPI ? 3 : 0>(a, s);
+        case 21: return launch_h1_pp_t<EPI, 0, 8, 4>(a, s);
+        case 22: return launch_h1_pp_t<EPI, 0, 9, 7>(a, s);
+        case 23: return launch_h1_pp_t<EPI, 0, 4, 2, 2>(a, s);
+        case 24: return launch_h1_pp_t<EPI, EPI ? 1 : 0, 4, 2, 2>(a, s);
+        case 25: return launch_h1_pp_t<EPI, EPI ? 3 : 0, 4, 2, 2>(a, s);
+        case 26: return launch_h1_pp_t<EPI, EPI ? 4 : 0, 4, 2, 2>(a, s);
         case 2: return launch_ring_t<2, 4, 4, 2, RING_H1, 4, 2, EPI>(a, s);
         case 3: return launch_ring_t<2, 4, 4, 2, RING_H1, 1, 4, EPI>(a, s);
         case 4: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 4, EPI>(a, s);
@@ -702,7 +1767,49 @@ static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
         default: return launch_ring_t<2, 4, 4, 2, RING_H1, 2, 4, EPI>(a, s);
     }
 }
-int h1_tile_bm(int variant) { return variant == 0 || (variant >= 4 && variant <= 9) ? 128 : 256; }
+int h1_tile_bm(int variant) { return variant >= 4 && variant <= 9 ? 128 : 256; }
+// The variant a search runs: 0 = the default (23); the k_h1_pp family needs K-slices
+// of its depth, at least D + 1 of them per tile (the filter constants staged at a
+// tile's first slice must have landed by its epilogue), and 32-bit DMA offsets --
+// otherwise k_h1_gemm (10).
+int h1_effective_variant(int variant, int pitch, int64_t ld) {
+    const int v = variant == 0 ? 23 : variant;
+    if (v < 18) return v;
+    const int ps = v >= 23 ? 2 : 1, d = v == 21 ? 4 : v == 22 ? 7 : v >= 23 ? 2 : 6;
+    if (pitch % (X3K * ps) || pitch / (X3K * ps) < d + 1 || (ps - 1) * ld * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return 10;
+    return v;
+}
+
+// Per row the fused filter's constants {w0, w1, dead, 0} (k_h1_pp stages them per
+// tile by DMA): cosine w0 = |x| / xi; L2 w0 = 1 / xi, w1 = |x|^2 (1 - 2^-20) / (2 xi)
+__global__ void k_h1_rowconst(const float* xinv, const float* xnorm, const uint8_t* dead, int64_t n, int metric,
+                              float4* xw) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float xi = xinv[i], xn = xnorm[i];
+    float w0, w1;
+    if (metric == COSINE) {
+        w0 = xn / xi;
+        w1 = 0.f;
+    } else {
+        w0 = 1.f / xi;
+        w1 = xn * xn * 0.5f * (1.0f - 0x1p-20f) / xi;
+    }
+    xw[i] = make_float4(w0, w1, dead && dead[i] ? 1.f : 0.f, 0.f);
+}
+int launch_h1_rowconst(const float* xinv, const float* xnorm, const uint8_t* dead, int64_t n, int metric, float4* xw,
+                       hipStream_t s) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_h1_rowconst, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, xinv, xnorm, dead, n, metric,
+                       xw);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+bool h1_timing_diag(int variant) {
+    return (variant >= 7 && variant <= 9) || (variant >= 11 && variant <= 13) || (variant >= 15 && variant <= 17) ||
+           variant == 19 || variant == 20 || (variant >= 24 && variant <= 26);
+}
+// regions per tile of a variant's fused filter (k_h1_pp: one per wave)
+int h1_region_split(int variant) { return variant >= 18 ? 8 : 1; }  // (an effective variant)
 int launch_h1_sample(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<0>(a, variant, s); }
 int launch_h1_filter(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<1>(a, variant, s); }
 
@@ -755,19 +1862,23 @@ int launch_ring_prep(const float* thr, const float* qnorm, const float* qinv, in
 // marked, and k_select_bucket sends it to the canonical fallback.
 __global__ __launch_bounds__(64) void k_bucket(const uint2* region, const int32_t* region_cnt, int rcap, int64_t ntiles,
                                                int64_t nqt, int BM, int BN, int64_t B, int32_t* qcnt, uint2* bucket,
-                                               int scap, uint8_t* qovf, ExactArgs a) {
-    const int64_t t = blockIdx.x;
-    if (t >= ntiles) return;
+                                               int scap, uint8_t* qovf, int rsub, ExactArgs a) {
+    // one wave per region: rsub regions of rcap / rsub entries per tile
+    const int64_t ri = blockIdx.x;
+    if (ri >= ntiles * rsub) return;
+    const int64_t t = ri / rsub;
+    rcap /= rsub;
+    const int cap = rsub > 1 ? rcap - 1 : rcap;  // k_h1_pp: the last slot of a wave's region is its trash slot
     const int lane = lane_id();
     const int64_t nt = t / nqt;
     const int64_t q0 = (t % nqt) * BM, n0 = nt * BN;
     const int sub = (int)(nt % H1_BSUB);
-    const int n = region_cnt[t];
-    if (n > rcap) {
+    const int n = region_cnt[ri];
+    if (n > cap) {
         for (int64_t q = q0 + lane; q < q0 + BM && q < B; q += 64) qovf[q] = 1;
     }
-    const int m = min(n, rcap);
-    const uint2* reg = region + t * (int64_t)rcap;
+    const int m = min(n, cap);
+    const uint2* reg = region + ri * (int64_t)rcap;
     for (int e = lane; e < m; e += 64) {
         const uint2 v = reg[e];
         const int64_t q = q0 + (v.x >> 16);
@@ -782,11 +1893,12 @@ __global__ __launch_bounds__(64) void k_bucket(const uint2* region, const int32_
 }
 
 int launch_bucket(const uint2* region, const int32_t* region_cnt, int rcap, int64_t ntiles, int64_t nqt, int BM,
-                  int BN, int64_t B, int32_t* qcnt, uint2* bucket, int scap, uint8_t* qovf, const ExactArgs& a,
+                  int BN, int64_t B, int32_t* qcnt, uint2* bucket, int scap, uint8_t* qovf, int rsub, const ExactArgs& a,
                   hipStream_t s) {
     if (ntiles <= 0) return 0;
-    hipLaunchKernelGGL(k_bucket, dim3((unsigned)ntiles), dim3(64), 0, s, region, region_cnt, rcap, ntiles, nqt, BM, BN,
-                       B, qcnt, bucket, scap, qovf, a);
+    if (rsub < 1 || rcap % rsub) return -5;
+    hipLaunchKernelGGL(k_bucket, dim3((unsigned)(ntiles * rsub)), dim3(64), 0, s, region, region_cnt, rcap, ntiles, nqt,
+                       BM, BN, B, qcnt, bucket, scap, qovf, rsub, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
