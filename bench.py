@@ -73,7 +73,7 @@ def parse():
     p.add_argument("--efc", type=int, default=400)
     p.add_argument("--keep-pruned", type=int, default=1)
     p.add_argument("--alpha", type=int, default=115, help="heuristic slack x100 (prune_alpha_pct; 100 = HNSW Alg. 4)")
-    p.add_argument("--build-expand", type=int, default=2, choices=[1, 2],
+    p.add_argument("--build-expand", type=int, default=2, choices=[1, 2, 3, 4],
                    help="entries expanded per step of the batched insert's layer searches")
     p.add_argument("--screen", type=int, default=1,
                    help="1: fp16 screening copy, 0: plain f32 evaluation of every candidate; same results")

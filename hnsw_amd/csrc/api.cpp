@@ -63,7 +63,7 @@ struct mhnsw_index {
     int efc = 0; // 0 => EfSearch
     int heuristic = 1;
     int keep_pruned = 0;
-    int build_expand = 2;     // batched insert: entries expanded per step of its layer searches (1 or 2)
+    int build_expand = 2;     // batched insert: entries expanded per step of its layer searches (1-4)
     int alpha_pct = 100;
     int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
     int vis_log2 = 12;
@@ -1615,7 +1615,7 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "keep_pruned") {
         h->keep_pruned = (int)(v != 0);
     } else if (n == "build_expand") {
-        if (v != 1 && v != 2) return fail(h, MHNSW_EINVAL, "build_expand must be 1 or 2");
+        if (v < 1 || v > 4) return fail(h, MHNSW_EINVAL, "build_expand must be in [1, 4]");
         h->build_expand = (int)v;
     } else if (n == "prune_alpha_pct") {
         if (v < 50 || v > 400) return fail(h, MHNSW_EINVAL, "prune_alpha_pct must be in [50, 400]");
@@ -1635,7 +1635,7 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "exact_kk") {
         h->exact_kk = (int)v;
     } else if (n == "exact_tile") {
-        if (v < 0 || v > 26) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 26]");
+        if (v < 0 || v > 33) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 33]");
         h->exact_tile = (int)v;
     } else if (n == "upper_ef") {
         if (v < 1 || v > 64) return fail(h, MHNSW_EINVAL, "upper_ef must be in [1, 64]");

@@ -1203,10 +1203,18 @@ static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
     if (n <= 0) return 0;
     // fp16 screening: same graph, fewer bytes per candidate; XW = a.expand as a
     // template argument (one search variant per kernel keeps it spill-free)
-    if (a.g.h16 && a.expand == 2)
+    if (a.g.h16 && a.expand == 4)
+        hipLaunchKernelGGL((k_batch_search<C, R, G, true, 4>), dim3((unsigned)n), dim3(64), lds, s, a);
+    else if (a.g.h16 && a.expand == 3)
+        hipLaunchKernelGGL((k_batch_search<C, R, G, true, 3>), dim3((unsigned)n), dim3(64), lds, s, a);
+    else if (a.g.h16 && a.expand == 2)
         hipLaunchKernelGGL((k_batch_search<C, R, G, true, 2>), dim3((unsigned)n), dim3(64), lds, s, a);
     else if (a.g.h16)
         hipLaunchKernelGGL((k_batch_search<C, R, G, true, 1>), dim3((unsigned)n), dim3(64), lds, s, a);
+    else if (a.expand == 4)
+        hipLaunchKernelGGL((k_batch_search<C, R, G, false, 4>), dim3((unsigned)n), dim3(64), lds, s, a);
+    else if (a.expand == 3)
+        hipLaunchKernelGGL((k_batch_search<C, R, G, false, 3>), dim3((unsigned)n), dim3(64), lds, s, a);
     else if (a.expand == 2)
         hipLaunchKernelGGL((k_batch_search<C, R, G, false, 2>), dim3((unsigned)n), dim3(64), lds, s, a);
     else

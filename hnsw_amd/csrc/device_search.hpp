@@ -317,13 +317,24 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
             vcount += __popcll(__ballot(pr == 1));
             cids[w] = compact(nb, pr != 0, cnts[w]);
         }
-        // one batch when the new neighbours fit the wave
-        if constexpr (XW == 2) {
-            if (cnts[0] + cnts[1] <= 64) {
-                const uint32_t c1 = shfl_u(cids[1], (lane - cnts[0]) & 63);
-                if (lane >= cnts[0]) cids[0] = c1;
-                cnts[0] += cnts[1];
-                cnts[1] = 0;
+        // the new neighbours of consecutive expanded entries share a batch while
+        // they fit the wave
+        if constexpr (XW >= 2) {
+            int b = 0;
+#pragma unroll
+            for (int w = 1; w < XW; ++w) {
+                if (cnts[b] + cnts[w] <= 64) {
+                    const uint32_t cw = shfl_u(cids[w], (lane - cnts[b]) & 63);
+#pragma unroll
+                    for (int v = 0; v < w; ++v)  // (static register indices)
+                        if (v == b && lane >= cnts[v]) cids[v] = cw;
+#pragma unroll
+                    for (int v = 0; v < w; ++v)
+                        if (v == b) cnts[v] += cnts[w];
+                    cnts[w] = 0;
+                } else {
+                    b = w;
+                }
             }
         }
         float wd = __int_as_float(0x7f800000);

@@ -1361,7 +1361,7 @@ __device__ __forceinline__ void wait_vm_plus(int extra, std::integer_sequence<in
 #define MH_LGKM0(f0, f1, f2, f3, f4, f5) \
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3), "+v"(f4), "+v"(f5))
 
-template <int EPI, int DIAG, int NS, int D, int PS>
+template <int EPI, int DIAG, int NS, int D, int PS, int ER>
 __global__ __launch_bounds__(512) void k_h1_pp(ExactArgs a) {
     static_assert(NS >= D + 2 && D >= 1, "ring depth");
     static_assert(PS == 1 || PS == 2, "slice depth 16 or 32");
@@ -1492,11 +1492,12 @@ __global__ __launch_bounds__(512) void k_h1_pp(ExactArgs a) {
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xw[0]), "+v"(xw[1]));
             __builtin_amdgcn_sched_barrier(0);
             bool rok[2];
-            unsigned long long rokm[2];
+            unsigned long long rokm[2], rspm[2];
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) {
                 rok[nb] = n0 + wc * 64 + nb * 32 + li < a.N && xw[nb][2] == 0.f;
                 rokm[nb] = __builtin_amdgcn_ballot_w64(rok[nb]);
+                rspm[nb] = __builtin_amdgcn_ballot_w64(!(fabsf(xw[nb][0]) < __builtin_inff()) || xw[nb][0] == 0.f);
             }
             // this wave's eighth of the region: cap entries, then one trash slot that
             // the lanes without an entry store to (every append is one store
@@ -1546,8 +1547,17 @@ __global__ __launch_bounds__(512) void k_h1_pp(ExactArgs a) {
 #pragma unroll
                     for (int nb = 0; nb < 2; ++nb) {
                         unsigned long long any = 0;
+                        if constexpr ((ER & 1) && COS) {
+                            // one ballot per block: the largest test value (a NaN test
+                            // comes only from a row whose w0 is not finite, in rspm)
+                            float mx = -__builtin_inff();
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) any |= __builtin_amdgcn_ballot_w64(test(mb, nb, r, c4, s4));
+                            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaf(-c4[r >> 2][r & 3], xw[nb][0], acc[mb][nb][r]));
+                            any = __builtin_amdgcn_ballot_w64(!(mx < 0.f)) | rspm[nb];
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < 16; ++r) any |= __builtin_amdgcn_ballot_w64(test(mb, nb, r, c4, s4));
+                        }
                         if (DIAG == 4) keep += (float)(any & rokm[nb]);  // diagnostic: the tests without the appends
                         if (DIAG != 4 && (any & rokm[nb])) {
 #pragma unroll
@@ -1559,7 +1569,8 @@ __global__ __launch_bounds__(512) void k_h1_pp(ExactArgs a) {
                                                             (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
                                     const int qo = wr * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * elh;
                                     const int ro = wc * 64 + nb * 32 + eli;
-                                    reg[pass && e < cap ? e : cap] = make_uint2((uint32_t)ro | ((uint32_t)qo << 16),
+                                    if (pass)  // (m != 0: the store runs for >= 1 lane, so nst counts it exactly)
+                                        reg[e < cap ? e : cap] = make_uint2((uint32_t)ro | ((uint32_t)qo << 16),
                                                                                 __float_as_uint(acc[mb][nb][r]));
                                     ++nst;
                                     cnt += __popcll(m);
@@ -1601,8 +1612,13 @@ __global__ __launch_bounds__(512) void k_h1_pp(ExactArgs a) {
 
     int64_t c_tile = 0;
     int c_kt = 0, c_slot = 0;
-    for (int64_t x = 0; x < S; ++x) {
+    for (int64_t x = 0;; ++x) {
         // R: fragments of slice x, DMA of slice x + D
+        if ((ER & 2) && c_kt == 0 && c_tile > 0) {  // the previous tile's epilogue, beside the partner's MFMAs
+            epilogue(first + (c_tile - 1) * wx, c_tile - 1);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (x == S) break;  // (after the last tile's epilogue: one call site keeps its loops unrolled)
         const uint32_t sb = ring_lds + (uint32_t)c_slot * SL;
         if (++c_slot == NS) c_slot = 0;
         f16x8 fa[PS][4], fb[PS][2];
@@ -1693,7 +1709,7 @@ __global__ __launch_bounds__(512) void k_h1_pp(ExactArgs a) {
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         if (++c_kt == nkt) {
-            epilogue(first + c_tile * wx, c_tile);
+            if (!(ER & 2)) epilogue(first + c_tile * wx, c_tile);  // (ER & 2: in the next R phase)
             c_kt = 0;
             ++c_tile;
         }
@@ -1712,10 +1728,398 @@ __global__ __launch_bounds__(512) void k_h1_pp(ExactArgs a) {
         if (lane == 0 && keep == -1.0e38f) a.region_cnt[0] = 1;
     }
 }
+// ---------------------------------------------------------------------------
+// k_h1_pp16: k_h1_pp (PS 2, NS 4, D 2) on v_mfma_f32_16x16x32_f16 -- the same ring,
+// DMA image and ping-pong; each wave's 128 x 64 tile is 8 x 4 blocks of 16 x 16,
+// 32 MFMAs per 32-deep slice from 8 A + 4 B fragment reads (the 16 x 16 shape
+// holds a higher clock than 32 x 32 on random operands: MI355X_MICROARCH.md DVFS (7)).
+// The fused filter tests a block's largest value first (one ballot per 16 queries).
+// ---------------------------------------------------------------------------
+template <int EPI, int DIAG>
+__global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
+    constexpr int NS = 4, D = 2, PS = 2;
+    static_assert(NS >= D + 2 && D >= 1, "ring depth");
+    static_assert(PS == 1 || PS == 2, "slice depth 16 or 32");
+    constexpr int RB = 32 * PS;                // image row bytes (16 PS halves of K)
+    constexpr int SL = (G_BM + G_BN) * RB;     // one slice: A then B image
+    constexpr int CPR = 2 * PS, RPP = 32 / PS;  // 16-B chunks per row, rows per 1-KiB piece
+    // EPI 1: per tile (double-buffered by tile parity) the filter constants, by
+    // LDS-DMA: 256 rows x {w0, w1, dead, -} (4 KiB), then c and s of 256 queries
+    constexpr int CST = 6144, CSTB = NS * SL;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[NS * SL + (EPI == 1 ? 2 * CST : 0)];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int g = __builtin_amdgcn_readfirstlane(wr);
+    const int wcs = __builtin_amdgcn_readfirstlane(wc);
+    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
+    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
+    const int64_t nblk = nqt * nnt;
+    const int W = gridDim.x, xcd = blockIdx.x % 8, jx = blockIdx.x / 8;
+    const int wx = W / 8 + (xcd < W % 8 ? 1 : 0);
+    const int64_t per = nblk / 8, rem = nblk % 8;
+    const int64_t lo = xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per;
+    const int64_t hi = lo + per + (xcd < rem ? 1 : 0);
+    const int64_t first = lo + jx;
+    const int64_t ntile = first < hi ? (hi - first + wx - 1) / wx : 0;
+    const int nkt = a.pitch / (X3K * PS);  // K-slices per tile
+    const int64_t S = ntile * nkt;
+    if (S == 0) return;  // uniform over the workgroup
+
+    // DMA: this wave's 2 PS pieces of a slice's A (group 0) or B (group 1) image;
+    // lane l: row RPP P + l / CPR, chunk (l % CPR) ^ swizzle(row) = K-block c / 2, half c % 2
+    const int rr0 = wcs * 2 * PS * RPP + lane / CPR;  // piece i: + RPP i
+    const int64_t ld = g == 0 ? a.ldQs : a.ldXs;
+    const int dc = (lane % CPR) ^ (PS == 1 ? (lane >> 4) & 1 : (lane >> 4) & 3);
+    const uint32_t pk = (uint32_t)((dc >> 1) * ld * 32 + (dc & 1) * 16);
+    const char* const plane = reinterpret_cast<const char*>(g == 0 ? a.Qh : a.Xh);
+    auto sbase = [](const char* p) {
+        const uint64_t u = reinterpret_cast<uint64_t>(p);
+        return reinterpret_cast<const char*>((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u) |
+                                             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32))
+                                              << 32));
+    };
+    int64_t p_tile = 0;
+    int p_kt = 0, p_slot = 0;
+    const char* p_base = nullptr;  // the producer tile's first row in K-block 0
+    int p_lim = 0;                 // its last valid image row (rows past B / N clamp to it)
+    auto p_set = [&]() {
+        const int64_t L = first + p_tile * wx;
+        const int64_t qt = L % nqt, nt = L / nqt;
+        const int64_t r0 = g == 0 ? qt * G_BM : (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
+        p_base = plane + r0 * 32;
+        p_lim = (int)min<int64_t>(255, (g == 0 ? a.B : a.N) - 1 - r0);
+    };
+    auto produce = [&]() {  // this wave's pieces of the producer slice, then advance it
+        if (DIAG < 3) {
+            const char* base = sbase(p_base + (int64_t)p_kt * PS * ld * 32);
+#pragma unroll
+            for (int i = 0; i < 2 * PS; ++i) {
+                const uint32_t off = (uint32_t)min(rr0 + RPP * i, p_lim) * 32 + pk;
+                uint8_t* dst = ring + p_slot * SL + g * (G_BM * RB) + (wcs * 2 * PS + i) * 1024;
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + off),
+                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+            }
+        }
+        if (++p_slot == NS) p_slot = 0;
+        if (++p_kt == nkt) {
+            p_kt = 0;
+            if (++p_tile < ntile) p_set();
+        }
+    };
+
+    f32x4 acc[8][4];  // 16 x 16 blocks: queries wr 128 + 16 mb .., rows wc 64 + 16 nb ..
+    const f32x4 zacc = {};  // a tile's first MFMAs accumulate onto zero (no clearing pass)
+    const uint32_t ring_lds = (uint32_t)reinterpret_cast<uintptr_t>(ring);
+    // fragment of a 16-row block (v_mfma_f32_16x16x32_f16): row lane & 15, logical
+    // chunk lane / 16 (halves 8 (lane / 16) .. of the 32-deep slice), swizzled like
+    // the DMA image: slot = chunk ^ ((row >> 2) & 3)
+    const uint32_t lfix = (lane & 15) * RB + ((((lane >> 4) ^ ((lane >> 2) & 3)) & 3) << 4);
+    const uint32_t offA = wr * 128 * RB, offB = G_BM * RB + wc * 64 * RB;
+    const int fr = lane & 15, fq = lane >> 4;  // accumulator: column (row) fr, queries 4 fq + j
+    float keep = 0.f;
+    int nst = 0;  // vector-memory ops besides the slice pieces since the last counted wait (as k_h1_pp)
+
+    auto epilogue = [&](int64_t L, int64_t ctile) {
+        const int64_t qt = L % nqt, nt = L / nqt;
+        const int64_t q0 = qt * G_BM;
+        const int64_t n0 = (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
+        if constexpr (DIAG == 1) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) keep += acc[i][j][r];
+        } else if constexpr (EPI == 0) {
+            const int64_t col0 = a.nsample_tiles > 0 ? nt * G_BN : n0;  // sample: compact columns
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) {
+                const int ro = wc * 64 + nb * 16 + fr;
+                const int64_t xr = n0 + ro;
+                if (xr >= a.N) continue;
+                const bool xok = !(a.dead && a.dead[xr]);
+                const float xn = a.xnorm[xr], xi = a.xinv[xr];
+#pragma unroll
+                for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int64_t qr = q0 + wr * 128 + mb * 16 + 4 * fq + r;
+                        if (qr >= a.B) continue;
+                        float sc = split_score(RING_H1, a.metric, acc[mb][nb][r], xi, a.qinv[qr], a.qnorm[qr], xn);
+                        if (!xok) sc = __int_as_float(0x7f800000);
+                        a.scores[(size_t)qr * a.ldS + col0 + ro] = sc;
+                    }
+            }
+        } else {
+            // the fused filter of k_h1_pp on the 16 x 16 accumulator layout: per lane
+            // four rows (nb) and, per block, four queries; constants from LDS
+            const uint32_t cb = ring_lds + CSTB + (uint32_t)(ctile & 1) * CST;
+            f32x4 xw[4];
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb)
+                asm volatile("ds_read_b128 %0, %1" : "=v"(xw[nb]) : "v"(cb + (uint32_t)(wc * 64 + nb * 16 + fr) * 16));
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xw[0]), "+v"(xw[1]), "+v"(xw[2]), "+v"(xw[3]));
+            __builtin_amdgcn_sched_barrier(0);
+            bool rok[4], rsp[4];
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) {
+                rok[nb] = n0 + wc * 64 + nb * 16 + fr < a.N && xw[nb][2] == 0.f;
+                // a row whose w0 is not finite (or 0) always takes the exact per-pair tests
+                rsp[nb] = rok[nb] && (!(fabsf(xw[nb][0]) < __builtin_inff()) || xw[nb][0] == 0.f);
+            }
+            const int cap = a.rcap / 8 - 1;
+            uint2* reg = a.region + (L * 8 + wave) * (int64_t)(cap + 1);
+            int cnt = 0;  // wave-uniform
+            uint32_t bx = 0, by = 0;  // buffered entries of the current chunk (lane j: entry 64 (cnt / 64) + j)
+            int lid = lane;
+            asm volatile("" : "+v"(lid));
+            const int efr = lid & 15, efq = lid >> 4;
+            auto filt = [&](auto cos_tag) {
+                constexpr bool COS = decltype(cos_tag)::value;
+                auto tval = [&](int mb, int nb, int r, const f32x4& c4, const f32x4& s4) {
+                    const float v = acc[mb][nb][r];
+                    if constexpr (COS)
+                        return fmaf(-c4[r], xw[nb][0], v);
+                    else
+                        return v - fmaf(c4[r], xw[nb][0], xw[nb][1] * s4[r]);
+                };
+#pragma unroll
+                for (int mb = 0; mb < 8; ++mb) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    // queries wr 128 + 16 mb + 4 fq + 0..3
+                    f32x4 c4, s4 = {};
+                    const uint32_t qa = cb + 4096 + (uint32_t)(wr * 128 + mb * 16 + 4 * fq) * 4;
+                    asm volatile("ds_read_b128 %0, %1" : "=v"(c4) : "v"(qa));
+                    if constexpr (!COS) {
+                        asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(s4) : "v"(qa));
+                        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c4), "+v"(s4));
+                    } else {
+                        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c4));
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    bool hit = false;
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb) {
+                        float mx = -__builtin_inff();
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, tval(mb, nb, r, c4, s4));
+                        hit |= (rok[nb] && !(mx < 0.f)) || rsp[nb];
+                    }
+                    if (DIAG == 4) keep += (float)__builtin_amdgcn_ballot_w64(hit);
+                    if (DIAG != 4 && __builtin_amdgcn_ballot_w64(hit)) {
+                        // the passing pairs of this block row, per lane a 16-bit mask
+                        // (bit 4 nb + r); each round appends every lane's lowest
+                        // pair, so the rounds are the largest count of one lane
+                        uint32_t pm = 0;
+#pragma unroll
+                        for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                pm |= (!(tval(mb, nb, r, c4, s4) < 0.f) && rok[nb]) ? 1u << (nb * 4 + r) : 0u;
+                        for (;;) {
+                            const bool pass = pm != 0;
+                            const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
+                            if (!m) break;
+                            const int b = pass ? __builtin_ctz(pm) : 0;
+                            pm &= pm - 1u;
+                            // acc[mb][b >> 2][b & 3] by a select tree (no dynamic register index)
+                            float v4[4];
+#pragma unroll
+                            for (int nb = 0; nb < 4; ++nb) {
+                                const float lo = (b & 1) ? acc[mb][nb][1] : acc[mb][nb][0];
+                                const float hi = (b & 1) ? acc[mb][nb][3] : acc[mb][nb][2];
+                                v4[nb] = (b & 2) ? hi : lo;
+                            }
+                            const float v01 = (b & 4) ? v4[1] : v4[0], v23 = (b & 4) ? v4[3] : v4[2];
+                            const float v = (b & 8) ? v23 : v01;
+                            const int pc = __popcll(m);
+                            const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                            // entry e goes to buffer lane e & 63 (one permutation of all lanes:
+                            // passing lanes to cnt + rank, the others behind them); each full
+                            // chunk of 64 is one coalesced store
+                            const int dst = (pass ? cnt + rk : cnt + pc + (lid - rk)) & 63;
+                            const int qo = wr * 128 + mb * 16 + 4 * efq + (b & 3);
+                            const int ro = wc * 64 + (b >> 2) * 16 + efr;
+                            uint32_t nx, ny;
+                            if constexpr (DIAG == 6) {  // diagnostic: no permutes
+                                nx = (uint32_t)ro | ((uint32_t)qo << 16);
+                                ny = __float_as_uint(v);
+                            } else {
+                                nx = push_to((uint32_t)ro | ((uint32_t)qo << 16), dst);
+                                ny = push_to(__float_as_uint(v), dst);
+                            }
+                            const int c0 = cnt & 63;
+                            const bool fresh = ((lid - c0) & 63) < pc;  // lanes receiving an entry
+                            if (c0 + pc >= 64) {  // chunk cnt / 64 complete: lanes >= c0 new, the rest buffered
+                                const int e = (cnt & ~63) + lid;
+                                const uint32_t sx = lid >= c0 ? nx : bx, sy = lid >= c0 ? ny : by;
+                                if constexpr (DIAG == 5) {  // diagnostic: no stores
+                                    keep += __uint_as_float(sx ^ sy);
+                                } else {
+                                    reg[e < cap ? e : cap] = make_uint2(sx, sy);  // (past cap: the trash slot; every lane stores, so nst is exact)
+                                    ++nst;
+                                }
+                            }
+                            if (fresh) {
+                                bx = nx;
+                                by = ny;
+                            }
+                            cnt += pc;
+                        }
+                    }
+                }
+            };
+            if (a.metric == COSINE)
+                filt(std::true_type{});
+            else
+                filt(std::false_type{});
+            if (cnt & 63) {  // the partial last chunk
+                const int e = (cnt & ~63) + lane;
+                if constexpr (DIAG == 5) {
+                    keep += __uint_as_float(bx ^ by);
+                } else {
+                    if (lane < (cnt & 63)) reg[e < cap ? e : cap] = make_uint2(bx, by);  // (lane 0 always stores)
+                    ++nst;
+                }
+            }
+            if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;
+            ++nst;
+        }
+    };
+
+    constexpr int VMC = vmcnt_imm(2 * PS * (D - 1));
+    constexpr int VMCNT0 = 0x0F70;
+    auto wait_vmc = [&]() {
+        if (nst > 0)
+            wait_vm_plus<2 * PS * (D - 1)>(nst, std::make_integer_sequence<int, 40>{});
+        else
+            __builtin_amdgcn_s_waitcnt(VMC);
+    };
+    p_set();
+    int64_t ps = 0;
+    for (; ps < D && ps < S; ++ps) produce();
+    if (D <= S)
+        __builtin_amdgcn_s_waitcnt(VMC);
+    else
+        __builtin_amdgcn_s_waitcnt(VMCNT0);
+    __builtin_amdgcn_s_barrier();
+    if (g == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
+
+    int64_t c_tile = 0;
+    int c_kt = 0, c_slot = 0;
+    for (int64_t x = 0; x < S; ++x) {
+        // R: fragments of slice x, DMA of slice x + D
+        const uint32_t sb = ring_lds + (uint32_t)c_slot * SL;
+        if (++c_slot == NS) c_slot = 0;
+        f16x8 fa[8], fb[4];
+        {
+            const uint32_t va = sb + offA + lfix, vb = sb + offB + lfix;
+            MH_DSR(fa[0], va, 0);
+            MH_DSR(fa[1], va, 1024);
+            MH_DSR(fa[2], va, 2048);
+            MH_DSR(fa[3], va, 3072);
+            MH_DSR(fa[4], va, 4096);
+            MH_DSR(fa[5], va, 5120);
+            MH_DSR(fa[6], va, 6144);
+            MH_DSR(fa[7], va, 7168);
+            MH_DSR(fb[0], vb, 0);
+            MH_DSR(fb[1], vb, 1024);
+            MH_DSR(fb[2], vb, 2048);
+            MH_DSR(fb[3], vb, 3072);
+        }
+        if (EPI == 1 && c_kt == 0) {
+            // the filter constants of this tile (read by its epilogue, nkt - 1 >= D
+            // slices later: retired by the counted waits in between)
+            const int64_t L = first + c_tile * wx;
+            const int64_t q0 = (L % nqt) * G_BM, n0 = (L / nqt) * G_BN;
+            uint8_t* cd = ring + CSTB + (int)(c_tile & 1) * CST;
+            const float* src;
+            uint8_t* dst;
+            if (g == 0) {
+                src = (wcs & 1 ? a.ring_s : a.ring_c) + q0 + lane * 4;
+                dst = cd + 4096 + (wcs & 1) * 1024;
+            } else {
+                src = reinterpret_cast<const float*>(a.xw + min<int64_t>(n0 + wcs * 64 + lane, a.N - 1));
+                dst = cd + wcs * 1024;
+            }
+            if (g == 1 || wcs < 2) {
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+                ++nst;
+            }
+        }
+        if (ps < S) {
+            produce();
+            ++ps;
+        }
+        const bool tail = x + 1 + D > S;  // fewer than D slices left in flight: retire them all
+        if (g == 1) {
+            if (tail)
+                __builtin_amdgcn_s_waitcnt(VMCNT0);
+            else
+                wait_vmc();
+            nst = 0;
+        }
+        __builtin_amdgcn_s_barrier();
+        // M: 32 MFMAs (+ the epilogue after a tile's last slice)
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]), "+v"(fa[6]),
+                       "+v"(fa[7]), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]));
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        if (c_kt == 0) {
+#pragma unroll
+            for (int m = 0; m < 8; ++m)
+#pragma unroll
+                for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[m], fb[n], zacc, 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int m = 0; m < 8; ++m)
+#pragma unroll
+                for (int n = 0; n < 4; ++n)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (++c_kt == nkt) {
+            epilogue(first + c_tile * wx, c_tile);
+            c_kt = 0;
+            ++c_tile;
+        }
+        if (g == 0) {
+            if (tail)
+                __builtin_amdgcn_s_waitcnt(VMCNT0);
+            else
+                wait_vmc();
+            nst = 0;
+        }
+        __builtin_amdgcn_s_barrier();
+    }
+    if (g == 0) __builtin_amdgcn_s_barrier();  // evens the barrier count
+    __builtin_amdgcn_s_waitcnt(VMCNT0);
+    if constexpr (DIAG == 1 || DIAG >= 4) {
+        if (lane == 0 && keep == -1.0e38f) a.region_cnt[0] = 1;
+    }
+}
+
+template <int EPI, int DIAG = 0>
+static int launch_h1_pp16_t(const ExactArgs& a, hipStream_t s) {
+    if (a.pitch % (X3K * 2)) return -5;
+    if (std::max(a.ldQs, a.ldXs) * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return -5;  // 32-bit DMA offsets
+    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
+    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
+    const int64_t nblk = nqt * nnt;
+    const int64_t W = std::min<int64_t>(nblk, std::max(8, device_cus() / 8 * 8));
+    hipLaunchKernelGGL((k_h1_pp16<EPI, DIAG>), dim3((unsigned)W), dim3(512), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 #undef MH_DSR
 #undef MH_LGKM0
 
-template <int EPI, int DIAG = 0, int NS = 8, int D = 6, int PS = 1>
+template <int EPI, int DIAG = 0, int NS = 8, int D = 6, int PS = 1, int ER = 0>
 static int launch_h1_pp_t(const ExactArgs& a, hipStream_t s) {
     if (a.pitch % (X3K * PS)) return -5;
     if ((PS - 1) * std::max(a.ldQs, a.ldXs) * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return -5;  // 32-bit DMA offsets
@@ -1723,7 +2127,7 @@ static int launch_h1_pp_t(const ExactArgs& a, hipStream_t s) {
     const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
     const int64_t nblk = nqt * nnt;
     const int64_t W = std::min<int64_t>(nblk, std::max(8, device_cus() / 8 * 8));
-    hipLaunchKernelGGL((k_h1_pp<EPI, DIAG, NS, D, PS>), dim3((unsigned)W), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((k_h1_pp<EPI, DIAG, NS, D, PS, ER>), dim3((unsigned)W), dim3(512), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1737,7 +2141,7 @@ static int launch_h1_pp_t(const ExactArgs& a, hipStream_t s) {
 template <int EPI>
 static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
     if (a.B <= 0 || a.N <= 0) return 0;
-    if (variant == 0) variant = 23;
+    if (variant == 0) variant = 29;
     switch (variant) {
         case 10: return launch_h1_gemm_t<EPI>(a, s);
         case 11: return launch_h1_gemm_t<EPI, EPI ? 1 : 0>(a, s);
@@ -1756,6 +2160,13 @@ static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
         case 24: return launch_h1_pp_t<EPI, EPI ? 1 : 0, 4, 2, 2>(a, s);
         case 25: return launch_h1_pp_t<EPI, EPI ? 3 : 0, 4, 2, 2>(a, s);
         case 26: return launch_h1_pp_t<EPI, EPI ? 4 : 0, 4, 2, 2>(a, s);
+        case 27: return launch_h1_pp_t<EPI, 0, 4, 2, 2, 3>(a, s);
+        case 28: return launch_h1_pp_t<EPI, 0, 4, 2, 2, 1>(a, s);
+        case 29: return launch_h1_pp16_t<EPI>(a, s);
+        case 30: return launch_h1_pp16_t<EPI, EPI ? 1 : 0>(a, s);
+        case 31: return launch_h1_pp16_t<EPI, EPI ? 4 : 0>(a, s);
+        case 32: return launch_h1_pp16_t<EPI, EPI ? 5 : 0>(a, s);
+        case 33: return launch_h1_pp16_t<EPI, EPI ? 6 : 0>(a, s);
         case 2: return launch_ring_t<2, 4, 4, 2, RING_H1, 4, 2, EPI>(a, s);
         case 3: return launch_ring_t<2, 4, 4, 2, RING_H1, 1, 4, EPI>(a, s);
         case 4: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 4, EPI>(a, s);
@@ -1773,7 +2184,7 @@ int h1_tile_bm(int variant) { return variant >= 4 && variant <= 9 ? 128 : 256; }
 // tile's first slice must have landed by its epilogue), and 32-bit DMA offsets --
 // otherwise k_h1_gemm (10).
 int h1_effective_variant(int variant, int pitch, int64_t ld) {
-    const int v = variant == 0 ? 23 : variant;
+    const int v = variant == 0 ? 29 : variant;
     if (v < 18) return v;
     const int ps = v >= 23 ? 2 : 1, d = v == 21 ? 4 : v == 22 ? 7 : v >= 23 ? 2 : 6;
     if (pitch % (X3K * ps) || pitch / (X3K * ps) < d + 1 || (ps - 1) * ld * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return 10;
@@ -1806,7 +2217,7 @@ int launch_h1_rowconst(const float* xinv, const float* xnorm, const uint8_t* dea
 }
 bool h1_timing_diag(int variant) {
     return (variant >= 7 && variant <= 9) || (variant >= 11 && variant <= 13) || (variant >= 15 && variant <= 17) ||
-           variant == 19 || variant == 20 || (variant >= 24 && variant <= 26);
+           variant == 19 || variant == 20 || (variant >= 24 && variant <= 26) || (variant >= 30 && variant <= 33);
 }
 // regions per tile of a variant's fused filter (k_h1_pp: one per wave)
 int h1_region_split(int variant) { return variant >= 18 ? 8 : 1; }  // (an effective variant)
