@@ -43,7 +43,7 @@ import hnsw_amd as H  # noqa: E402
 
 # revision of the search/build kernels the recorded PMC passes (profiles/*_pmc_*.json)
 # were taken on; a pass recorded on another revision is not attached as `traffic`
-KERNEL_REV = "r02-rowmajor-selection"
+KERNEL_REV = "r03"
 from hnsw_amd.shard import engine_local_search, shard_range, sharded_search  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -86,8 +86,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline time box (0 disables)")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
     p.add_argument("--one-gpu", action="store_true", help="map every rank to cuda:0 (multi-rank rehearsal)")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02_pmc_search.json"))
-    p.add_argument("--pmc-build-json", default=os.path.join(ROOT, "profiles", "r02_pmc_build.json"))
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03_pmc_search.json"))
+    p.add_argument("--pmc-build-json", default=os.path.join(ROOT, "profiles", "r03_pmc_build.json"))
     return p.parse_args()
 
 
@@ -300,7 +300,7 @@ def config4(device, steps=10):
     return {"workload": "1M x 1536-d cosine exact search, batch 1024, k=10 (recall 1.0: certified canonical top-k)",
             "queries_per_s": round(B / dt, 1), "ms_per_batch": round(dt * 1e3, 3),
             "exact_path_ms": round(float(np.mean(path)), 3), "uncertified_per_batch": unc,
-            "roofline": {"bound": "mfma", "kernel": "k_scores_ring (fp16 1-product, fused filter epilogue)",
+            "roofline": {"bound": "mfma", "kernel": "k_h1_pp16 (fp16 1-product, v_mfma_f32_16x16x32_f16, fused filter records)",
                          "kernel_ms": round(gm, 4), "flops_per_launch": flops,
                          "achieved": round(flops / (gm * 1e-3) / 1e12, 1), "peak": 2500.0, "unit": "TFLOP/s",
                          "frac": round(flops / (gm * 1e-3) / 1e12 / 2500.0, 4), "traffic": None}}

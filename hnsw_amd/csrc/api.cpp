@@ -69,6 +69,7 @@ struct mhnsw_index {
     int vis_log2 = 12;
     int vis_entries = 0;      // beam search's visited set; 0 = 1.25 * 2^vis_log2 (beam_vis_entries)
     int exact_kk = 0;
+    int exact_sample = 32;   // fused preselection: row tiles in the threshold sample (about; stride = tiles / this)
     int exact_precision = 3;  // scores: 0 f32-input MFMA, 1 bf16x3 split, 2 fp16 2-product split,
                               // 3 fp16 1-product with the fused preselection (all certified, same results)
     int exact_tile = 0;       // bf16x3 GEMM tile variant (exact.hip launch_exact_scores_x3)
@@ -1177,7 +1178,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         const int ev = h1_effective_variant(h->exact_tile, h->pitch, std::max<int64_t>(qc, h->capn));
         const int bm = h1_tile_bm(ev);
         const int64_t nnt = (h->n + H1_BN - 1) / H1_BN, nqt = (qc + bm - 1) / bm;
-        const int stride = (int)std::max<int64_t>(1, std::min<int64_t>(128, nnt / 32));
+        const int stride = (int)std::max<int64_t>(1, std::min<int64_t>(128, nnt / h->exact_sample));
         const int64_t nsamp = h1 ? ((h->n / H1_BN) - 1) / stride + 1 : 0;  // sampled full tiles
         const int J = stride >= 8 ? std::max(k, kk / 4) : kk;
         int sseg = 1;
@@ -1190,7 +1191,11 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         // through on average (~J N / ns per query, ~bm J BN / ns per tile), with floors
         const int64_t ns = std::max<int64_t>(1, nsamp * H1_BN);
         // (a multiple of 8: k_h1_pp splits each tile's region among its 8 waves)
-        const int rcap = (int)std::min<int64_t>((int64_t)bm * H1_BN, std::max<int64_t>(2048, 4 * bm * J * H1_BN / ns) + 7) / 8 * 8;
+        // record-mode variants: per wave 4x the expected records (<= one per passing pair,
+        // at most 8 block rows x 64 lanes), H1_REC uint2 each
+        const int rcap = h1_records(ev)
+                             ? 8 * H1_REC * (int)std::min<int64_t>(512, std::max<int64_t>(64, 4 * bm * J * H1_BN / ns / 8))
+                             : (int)std::min<int64_t>((int64_t)bm * H1_BN, std::max<int64_t>(2048, 4 * bm * J * H1_BN / ns) + 7) / 8 * 8;
         const int rsub = h1_region_split(ev);
         const int scap = (int)std::min<int64_t>(std::max<int64_t>(h->n, 1),
                                                 std::max<int64_t>(512, 8 * J * h->n / ns / H1_BSUB));
@@ -1347,7 +1352,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
                     h->have_gemm_timing = timing;
                     const int64_t bqt = (nb + bm - 1) / bm;
                     LCHK(h, launch_bucket(h->h1region.p, h->h1rcnt.p, rcap, bqt * nnt, bqt, bm, H1_BN, nb, h->h1qcnt.p,
-                                          h->h1bucket.p, scap, h->h1ovf.p, rsub, a, s));
+                                          h->h1bucket.p, scap, h->h1ovf.p, rsub, h1_records(ev) ? 1 : 0, a, s));
                     LCHK(h, launch_select_bucket(a, h->h1qcnt.p, h->h1bucket.p, scap, h->h1ovf.p, h->h1thr.p, s));
                 } else if (h2) {
                     a.xinv = h->xinv.p;
@@ -1632,10 +1637,13 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "vis_log2") {
         if (v < 6 || v > 15) return fail(h, MHNSW_EINVAL, "vis_log2 must be in [6, 15]");
         h->vis_log2 = (int)v;
+    } else if (n == "exact_sample") {
+        if (v < 1 || v > 1 << 20) return fail(h, MHNSW_EINVAL, "exact_sample must be in [1, 2^20]");
+        h->exact_sample = (int)v;
     } else if (n == "exact_kk") {
         h->exact_kk = (int)v;
     } else if (n == "exact_tile") {
-        if (v < 0 || v > 33) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 33]");
+        if (v < 0 || v > 34) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 34]");
         h->exact_tile = (int)v;
     } else if (n == "upper_ef") {
         if (v < 1 || v > 64) return fail(h, MHNSW_EINVAL, "upper_ef must be in [1, 64]");
@@ -1695,6 +1703,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "vis_log2") *v = h->vis_log2;
     else if (n == "vis_entries") *v = beam_vis_entries(h);
     else if (n == "exact_kk") *v = h->exact_kk;
+    else if (n == "exact_sample") *v = h->exact_sample;
     else if (n == "exact_precision") *v = h->exact_precision;
     else if (n == "exact_tile") *v = h->exact_tile;
     else if (n == "compat_waves") *v = h->compat_waves;

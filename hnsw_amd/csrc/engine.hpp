@@ -196,9 +196,11 @@ int launch_h1_filter(const ExactArgs& a, int variant, hipStream_t s);
 constexpr int H1_BN = 256;   // row tile of every launch_h1_* variant
 constexpr int H1_BSUB = 16;     // sub-buckets per query (k_bucket)
 constexpr int H1_CSTRIDE = 32;  // sub-bucket counters one 128-B line apart (no same-line atomics)
+constexpr int H1_REC = 10;      // uint2 per record of the record-mode filter: {mb | lane << 8, 0}, pad, 16 accumulators
 int h1_tile_bm(int variant);  // query tile of a variant (128 or 256)
 bool h1_timing_diag(int variant);   // exact_tile 7-9, 11-13, 15-17, 19-20: timing diagnostics (no results)
 int h1_region_split(int variant);   // regions per tile of the fused filter (rcap is split evenly)
+bool h1_records(int variant);       // the variant's regions hold records (k_h1_pp16 REC), not pairs
 int h1_effective_variant(int variant, int pitch, int64_t ld);  // the variant a search runs (0 -> default)
 int launch_h1_rowconst(const float* xinv, const float* xnorm, const uint8_t* dead, int64_t n, int metric, float4* xw,
                        hipStream_t s);
@@ -206,7 +208,7 @@ int launch_ring_prep(const float* thr, const float* qnorm, const float* qinv, in
                      float* sq, hipStream_t s);
 // qcnt [B * H1_BSUB * H1_CSTRIDE], bucket [B * H1_BSUB * scap]
 int launch_bucket(const uint2* region, const int32_t* region_cnt, int rcap, int64_t ntiles, int64_t nqt, int BM,
-                  int BN, int64_t B, int32_t* qcnt, uint2* bucket, int scap, uint8_t* qovf, int rsub,
+                  int BN, int64_t B, int32_t* qcnt, uint2* bucket, int scap, uint8_t* qovf, int rsub, int rec,
                   const ExactArgs& a, hipStream_t s);
 int launch_select_bucket(const ExactArgs& a, const int32_t* qcnt, const uint2* bucket, int scap, const uint8_t* qovf,
                          const float* thr, hipStream_t s);

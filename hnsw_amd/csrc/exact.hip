@@ -1735,7 +1735,7 @@ __global__ __launch_bounds__(512) void k_h1_pp(ExactArgs a) {
 // holds a higher clock than 32 x 32 on random operands: MI355X_MICROARCH.md DVFS (7)).
 // The fused filter tests a block's largest value first (one ballot per 16 queries).
 // ---------------------------------------------------------------------------
-template <int EPI, int DIAG>
+template <int EPI, int DIAG, int REC = 0>
 __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     constexpr int NS = 4, D = 2, PS = 2;
     static_assert(NS >= D + 2 && D >= 1, "ring depth");
@@ -1872,6 +1872,8 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
             uint2* reg = a.region + (L * 8 + wave) * (int64_t)(cap + 1);
             int cnt = 0;  // wave-uniform
             uint32_t bx = 0, by = 0;  // buffered entries of the current chunk (lane j: entry 64 (cnt / 64) + j)
+            const int rcw = a.rcap / (8 * H1_REC);  // REC: records per wave region
+            uint2* regr = a.region + (L * 8 + wave) * (int64_t)(rcw * H1_REC);
             int lid = lane;
             asm volatile("" : "+v"(lid));
             const int efr = lid & 15, efq = lid >> 4;
@@ -1907,7 +1909,26 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                         hit |= (rok[nb] && !(mx < 0.f)) || rsp[nb];
                     }
                     if (DIAG == 4) keep += (float)__builtin_amdgcn_ballot_w64(hit);
-                    if (DIAG != 4 && __builtin_amdgcn_ballot_w64(hit)) {
+                    if constexpr (REC) {
+                        // record mode: a lane with a passing pair in this block row
+                        // stores its 16 accumulators (k_bucket applies the same tests)
+                        const unsigned long long m = __builtin_amdgcn_ballot_w64(hit);
+                        if (m) {
+                            const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                            if (hit) {
+                                const int slot = min(cnt + rk, rcw - 1);  // past the capacity: the last record (flagged)
+                                uint2* rec = regr + (int64_t)slot * H1_REC;
+                                rec[0] = make_uint2((uint32_t)mb | ((uint32_t)lid << 8), 0u);
+                                float4* ra = reinterpret_cast<float4*>(rec + 2);
+#pragma unroll
+                                for (int nb = 0; nb < 4; ++nb)
+                                    ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
+                            }
+                            nst += 5;  // (at least 5 store instructions: never an over-count)
+                            cnt += __popcll(m);
+                        }
+                    } else if (DIAG != 4 && __builtin_amdgcn_ballot_w64(hit)) {
                         // the passing pairs of this block row, per lane a 16-bit mask
                         // (bit 4 nb + r); each round appends every lane's lowest
                         // pair, so the rounds are the largest count of one lane
@@ -1975,7 +1996,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                 filt(std::true_type{});
             else
                 filt(std::false_type{});
-            if (cnt & 63) {  // the partial last chunk
+            if (!REC && (cnt & 63)) {  // the partial last chunk
                 const int e = (cnt & ~63) + lane;
                 if constexpr (DIAG == 5) {
                     keep += __uint_as_float(bx ^ by);
@@ -1993,7 +2014,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     constexpr int VMCNT0 = 0x0F70;
     auto wait_vmc = [&]() {
         if (nst > 0)
-            wait_vm_plus<2 * PS * (D - 1)>(nst, std::make_integer_sequence<int, 40>{});
+            wait_vm_plus<2 * PS * (D - 1)>(nst, std::make_integer_sequence<int, 60>{});  // (vmcnt <= 63)
         else
             __builtin_amdgcn_s_waitcnt(VMC);
     };
@@ -2104,7 +2125,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     }
 }
 
-template <int EPI, int DIAG = 0>
+template <int EPI, int DIAG = 0, int REC = 0>
 static int launch_h1_pp16_t(const ExactArgs& a, hipStream_t s) {
     if (a.pitch % (X3K * 2)) return -5;
     if (std::max(a.ldQs, a.ldXs) * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return -5;  // 32-bit DMA offsets
@@ -2112,7 +2133,7 @@ static int launch_h1_pp16_t(const ExactArgs& a, hipStream_t s) {
     const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
     const int64_t nblk = nqt * nnt;
     const int64_t W = std::min<int64_t>(nblk, std::max(8, device_cus() / 8 * 8));
-    hipLaunchKernelGGL((k_h1_pp16<EPI, DIAG>), dim3((unsigned)W), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((k_h1_pp16<EPI, DIAG, REC>), dim3((unsigned)W), dim3(512), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2141,7 +2162,7 @@ static int launch_h1_pp_t(const ExactArgs& a, hipStream_t s) {
 template <int EPI>
 static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
     if (a.B <= 0 || a.N <= 0) return 0;
-    if (variant == 0) variant = 29;
+    if (variant == 0) variant = 34;
     switch (variant) {
         case 10: return launch_h1_gemm_t<EPI>(a, s);
         case 11: return launch_h1_gemm_t<EPI, EPI ? 1 : 0>(a, s);
@@ -2167,6 +2188,7 @@ static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
         case 31: return launch_h1_pp16_t<EPI, EPI ? 4 : 0>(a, s);
         case 32: return launch_h1_pp16_t<EPI, EPI ? 5 : 0>(a, s);
         case 33: return launch_h1_pp16_t<EPI, EPI ? 6 : 0>(a, s);
+        case 34: return launch_h1_pp16_t<EPI, 0, EPI>(a, s);
         case 2: return launch_ring_t<2, 4, 4, 2, RING_H1, 4, 2, EPI>(a, s);
         case 3: return launch_ring_t<2, 4, 4, 2, RING_H1, 1, 4, EPI>(a, s);
         case 4: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 4, EPI>(a, s);
@@ -2184,7 +2206,7 @@ int h1_tile_bm(int variant) { return variant >= 4 && variant <= 9 ? 128 : 256; }
 // tile's first slice must have landed by its epilogue), and 32-bit DMA offsets --
 // otherwise k_h1_gemm (10).
 int h1_effective_variant(int variant, int pitch, int64_t ld) {
-    const int v = variant == 0 ? 29 : variant;
+    const int v = variant == 0 ? 34 : variant;
     if (v < 18) return v;
     const int ps = v >= 23 ? 2 : 1, d = v == 21 ? 4 : v == 22 ? 7 : v >= 23 ? 2 : 6;
     if (pitch % (X3K * ps) || pitch / (X3K * ps) < d + 1 || (ps - 1) * ld * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return 10;
@@ -2221,6 +2243,9 @@ bool h1_timing_diag(int variant) {
 }
 // regions per tile of a variant's fused filter (k_h1_pp: one per wave)
 int h1_region_split(int variant) { return variant >= 18 ? 8 : 1; }  // (an effective variant)
+// the variant's regions hold records (H1_REC uint2 each: a lane's 16 accumulators of one
+// block row, tested by k_bucket) instead of passing pairs
+bool h1_records(int variant) { return variant == 34; }
 int launch_h1_sample(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<0>(a, variant, s); }
 int launch_h1_filter(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<1>(a, variant, s); }
 
@@ -2273,7 +2298,7 @@ int launch_ring_prep(const float* thr, const float* qnorm, const float* qinv, in
 // marked, and k_select_bucket sends it to the canonical fallback.
 __global__ __launch_bounds__(64) void k_bucket(const uint2* region, const int32_t* region_cnt, int rcap, int64_t ntiles,
                                                int64_t nqt, int BM, int BN, int64_t B, int32_t* qcnt, uint2* bucket,
-                                               int scap, uint8_t* qovf, int rsub, ExactArgs a) {
+                                               int scap, uint8_t* qovf, int rsub, int rec, ExactArgs a) {
     // one wave per region: rsub regions of rcap / rsub entries per tile
     const int64_t ri = blockIdx.x;
     if (ri >= ntiles * rsub) return;
@@ -2303,13 +2328,73 @@ __global__ __launch_bounds__(64) void k_bucket(const uint2* region, const int32_
     }
 }
 
+// Record mode (k_h1_pp16<1, 0, 1>): one workgroup per tile, wave w takes region w
+// (the tile's wave w: queries 128 (w / 4) .., rows 64 (w % 4) ..).  The tile's
+// filter constants are staged in LDS once; 16 lanes take one record (lane
+// 4 nb + r: accumulator r of row block nb), apply the GEMM's test to it and
+// append the passing pairs as k_bucket does.
+__global__ __launch_bounds__(512) void k_bucket_rec(const uint2* region, const int32_t* region_cnt, int rcap,
+                                                    int64_t nqt, int64_t B, int32_t* qcnt, uint2* bucket, int scap,
+                                                    uint8_t* qovf, ExactArgs a) {
+    __shared__ float sc_c[256], sc_s[256];
+    __shared__ float4 sc_w[256];
+    const int64_t t = blockIdx.x;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int64_t nt = t / nqt;
+    const int64_t q0 = (t % nqt) * 256, n0 = nt * 256;
+    const int sub = (int)(nt % H1_BSUB);
+    if (tid < 256) {
+        sc_c[tid] = a.ring_c[q0 + tid];  // (ring_c / ring_s are padded to the 256-query tile)
+        sc_s[tid] = a.metric == COSINE ? 0.f : a.ring_s[q0 + tid];
+        const int64_t row = n0 + tid;
+        sc_w[tid] = a.xw[row < a.N ? row : a.N - 1];
+    }
+    __syncthreads();
+    const int rpw = rcap / 8, rcw = rpw / H1_REC;  // uint2 / records per wave region
+    const int64_t ri = t * 8 + w;
+    const int n = region_cnt[ri];
+    if (n > rcw) {
+        for (int64_t q = q0 + (w >> 2) * 128 + lane; q < q0 + (w >> 2) * 128 + 128 && q < B; q += 64) qovf[q] = 1;
+    }
+    const int m = min(n, rcw);
+    const uint2* reg = region + ri * (int64_t)rpw;
+    const int wr = w >> 2, wc = w & 3, pr = lane & 15, nb = pr >> 2, r = pr & 3;
+    for (int e0 = 0; e0 < m; e0 += 4) {
+        const int e = e0 + (lane >> 4);
+        if (e >= m) break;
+        const uint2* rec = reg + (int64_t)e * H1_REC;
+        const uint32_t hd = rec[0].x;
+        const float v = reinterpret_cast<const float*>(rec + 2)[pr];
+        const int mb = (int)(hd & 0xFFu), sl = (int)(hd >> 8);
+        const int ro = wc * 64 + nb * 16 + (sl & 15), qo = wr * 128 + mb * 16 + 4 * (sl >> 4) + r;
+        const int64_t row = n0 + ro, q = q0 + qo;
+        const float4 xw = sc_w[ro];
+        // the fused filter's test (k_h1_pp16), on the same accumulator and constants
+        float tv;
+        if (a.metric == COSINE)
+            tv = fmaf(-sc_c[qo], xw.x, v);
+        else
+            tv = v - fmaf(sc_c[qo], xw.x, xw.y * sc_s[qo]);
+        if (!(tv < 0.f) && row < a.N && xw.z == 0.f && q < B) {
+            const float sc = split_score(RING_H1, a.metric, v, a.xinv[row], a.qinv[q], a.qnorm[q], a.xnorm[row]);
+            const int pos = atomicAdd(&qcnt[(q * H1_BSUB + sub) * H1_CSTRIDE], 1);
+            if (pos < scap) bucket[(q * H1_BSUB + sub) * scap + pos] = make_uint2((uint32_t)row, __float_as_uint(sc));
+        }
+    }
+}
+
 int launch_bucket(const uint2* region, const int32_t* region_cnt, int rcap, int64_t ntiles, int64_t nqt, int BM,
-                  int BN, int64_t B, int32_t* qcnt, uint2* bucket, int scap, uint8_t* qovf, int rsub, const ExactArgs& a,
-                  hipStream_t s) {
+                  int BN, int64_t B, int32_t* qcnt, uint2* bucket, int scap, uint8_t* qovf, int rsub, int rec,
+                  const ExactArgs& a, hipStream_t s) {
     if (ntiles <= 0) return 0;
-    if (rsub < 1 || rcap % rsub) return -5;
+    if (rsub < 1 || rcap % rsub || (rec && (rsub != 8 || BM != 256 || BN != 256 || (rcap / rsub) % H1_REC))) return -5;
+    if (rec) {
+        hipLaunchKernelGGL(k_bucket_rec, dim3((unsigned)ntiles), dim3(512), 0, s, region, region_cnt, rcap, nqt, B, qcnt,
+                           bucket, scap, qovf, a);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     hipLaunchKernelGGL(k_bucket, dim3((unsigned)(ntiles * rsub)), dim3(64), 0, s, region, region_cnt, rcap, ntiles, nqt,
-                       BM, BN, B, qcnt, bucket, scap, qovf, rsub, a);
+                       BM, BN, B, qcnt, bucket, scap, qovf, rsub, rec, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -26,6 +26,8 @@ g.add_device(np.arange(n), X.data_ptr(), n, d)
 del X
 g.set_option("exact_precision", prec)
 g.set_option("exact_tile", tile)
+if os.environ.get("EXACT_SAMPLE"):
+    g.set_option("exact_sample", int(os.environ["EXACT_SAMPLE"]))
 S = Searcher(g, B, 10, d, dev)
 
 

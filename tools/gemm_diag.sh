@@ -8,7 +8,7 @@ mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 TILES=${*:-23 24 25 10}
 for T in $TILES; do
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/t$T -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/exact_probe.py 3 $T ${REPS:-5} > $O/t$T.log 2>&1 || { echo FAIL $T; tail -20 $O/t$T.log; exit 1; }
-  grep ms_per_batch $O/t$T.log
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/t$T$SFX -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/exact_probe.py 3 $T ${REPS:-5} > $O/t$T$SFX.log 2>&1 || { echo FAIL $T; tail -20 $O/t$T$SFX.log; exit 1; }
+  grep ms_per_batch $O/t$T$SFX.log
 done
 echo ALL_OK
