@@ -1919,11 +1919,20 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                             if (hit) {
                                 const int slot = min(cnt + rk, rcw - 1);  // past the capacity: the last record (flagged)
                                 uint2* rec = regr + (int64_t)slot * H1_REC;
-                                rec[0] = make_uint2((uint32_t)mb | ((uint32_t)lid << 8), 0u);
                                 float4* ra = reinterpret_cast<float4*>(rec + 2);
+                                if constexpr (REC == 2) {  // non-temporal record stores
+                                    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+                                    const u32x2 hd = {(uint32_t)mb | ((uint32_t)lid << 8), 0u};
+                                    __builtin_nontemporal_store(hd, reinterpret_cast<u32x2*>(rec));
 #pragma unroll
-                                for (int nb = 0; nb < 4; ++nb)
-                                    ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
+                                    for (int nb = 0; nb < 4; ++nb)
+                                        __builtin_nontemporal_store(acc[mb][nb], reinterpret_cast<f32x4*>(ra + nb));
+                                } else {
+                                    rec[0] = make_uint2((uint32_t)mb | ((uint32_t)lid << 8), 0u);
+#pragma unroll
+                                    for (int nb = 0; nb < 4; ++nb)
+                                        ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
+                                }
                             }
                             nst += 5;  // (at least 5 store instructions: never an over-count)
                             cnt += __popcll(m);
@@ -2189,6 +2198,7 @@ static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
         case 32: return launch_h1_pp16_t<EPI, EPI ? 5 : 0>(a, s);
         case 33: return launch_h1_pp16_t<EPI, EPI ? 6 : 0>(a, s);
         case 34: return launch_h1_pp16_t<EPI, 0, EPI>(a, s);
+        case 35: return launch_h1_pp16_t<EPI, 0, EPI ? 2 : 0>(a, s);
         case 2: return launch_ring_t<2, 4, 4, 2, RING_H1, 4, 2, EPI>(a, s);
         case 3: return launch_ring_t<2, 4, 4, 2, RING_H1, 1, 4, EPI>(a, s);
         case 4: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 4, EPI>(a, s);
@@ -2245,7 +2255,7 @@ bool h1_timing_diag(int variant) {
 int h1_region_split(int variant) { return variant >= 18 ? 8 : 1; }  // (an effective variant)
 // the variant's regions hold records (H1_REC uint2 each: a lane's 16 accumulators of one
 // block row, tested by k_bucket) instead of passing pairs
-bool h1_records(int variant) { return variant == 34; }
+bool h1_records(int variant) { return variant == 34 || variant == 35; }
 int launch_h1_sample(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<0>(a, variant, s); }
 int launch_h1_filter(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<1>(a, variant, s); }
 

@@ -93,7 +93,8 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * (23) K-slices on 32x32x16 MFMAs, 27/28 23 with a max-first filter test (27
  * also runs the epilogue in the next R phase), 29 the same stream on 16x16x32
  * MFMAs appending passing pairs, 34 (the default) 29 storing per-lane
- * records of a block row's accumulators that k_bucket tests -- a shape the
+ * records of a block row's accumulators that k_bucket tests, 35 34 with
+ * non-temporal record stores -- a shape the
  * stream does not admit (fewer than 3 slices per tile) runs 10; 7-9 / 11-13 /
  * 15-17 / 19-20, 24-26, 30-33 timing diagnostics of 5 / 10 / 14 / 18, 23, 29
  * that let no pair pass, so every query takes the canonical
