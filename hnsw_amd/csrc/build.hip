@@ -735,8 +735,11 @@ __global__ __launch_bounds__(64) void k_batch_descend(BatchBuildArgs a) {
     }
 }
 
+#ifndef MH_BUILD_WPS
+#define MH_BUILD_WPS 1
+#endif
 template <class C, int R, int G, bool SCREEN, int XW>
-__global__ __launch_bounds__(64) void k_batch_search(BatchBuildArgs a) {
+__global__ __launch_bounds__(64, MH_BUILD_WPS) void k_batch_search(BatchBuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t u;
     if (a.order) {
