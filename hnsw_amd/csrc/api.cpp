@@ -1643,7 +1643,7 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "exact_kk") {
         h->exact_kk = (int)v;
     } else if (n == "exact_tile") {
-        if (v < 0 || v > 35) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 35]");
+        if (v < 0 || v > 37) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 37]");
         h->exact_tile = (int)v;
     } else if (n == "upper_ef") {
         if (v < 1 || v > 64) return fail(h, MHNSW_EINVAL, "upper_ef must be in [1, 64]");

@@ -1747,6 +1747,10 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     // LDS-DMA: 256 rows x {w0, w1, dead, -} (4 KiB), then c and s of 256 queries
     constexpr int CST = 6144, CSTB = NS * SL;
     __shared__ __attribute__((aligned(16))) uint8_t ring[NS * SL + (EPI == 1 ? 2 * CST : 0)];
+    // REC 3: per wave an LDS buffer of H1_LRC records (80 B each), written out in
+    // coalesced 16-B chunks (the ring and constants leave exactly 20 KiB of the 160)
+    constexpr int H1_LRC = 32;
+    __shared__ __attribute__((aligned(16))) uint8_t lrec[REC == 3 && EPI == 1 ? 8 * H1_LRC * 80 : 16];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 2, wc = wave & 3;
@@ -1820,6 +1824,12 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     float keep = 0.f;
     int nst = 0;  // vector-memory ops besides the slice pieces since the last counted wait (as k_h1_pp)
 
+    // REC 4: the epilogue only tests; per lane a mask of the block rows with a
+    // passing pair (hm), and the tile's record stores are issued in the next R phase
+    // (while the partner group multiplies; acc holds the tile until the next M phase)
+    uint32_t hm = 0;
+    int pend = 0;  // wave-uniform: a tested tile's records are pending
+    int64_t pend_L = 0;
     auto epilogue = [&](int64_t L, int64_t ctile) {
         const int64_t qt = L % nqt, nt = L / nqt;
         const int64_t q0 = qt * G_BM;
@@ -1877,6 +1887,22 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
             int lid = lane;
             asm volatile("" : "+v"(lid));
             const int efr = lid & 15, efq = lid >> 4;
+            int lcnt = 0;  // REC 3: records buffered in LDS (wave-uniform; they are cnt - lcnt ..)
+            // the buffered records to their slots, 64 chunks per store; returns the
+            // store instructions issued (values in: no captured counters)
+            auto flush_rec = [lid, wave, rcw, regr](int base, int n) -> int {
+                const int nch = n * 5;
+                const uint4* src = reinterpret_cast<const uint4*>(lrec + wave * H1_LRC * 80);
+                int st = 0;
+                for (int c0 = 0; c0 < nch; c0 += 64, ++st) {
+                    const int c = c0 + lid;
+                    if (c < nch) {
+                        const int i = c / 5, j = c - 5 * i;
+                        reinterpret_cast<uint4*>(regr + (int64_t)min(base + i, rcw - 1) * H1_REC)[j] = src[c];
+                    }
+                }
+                return st;
+            };
             auto filt = [&](auto cos_tag) {
                 constexpr bool COS = decltype(cos_tag)::value;
                 auto tval = [&](int mb, int nb, int r, const f32x4& c4, const f32x4& s4) {
@@ -1909,7 +1935,45 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                         hit |= (rok[nb] && !(mx < 0.f)) || rsp[nb];
                     }
                     if (DIAG == 4) keep += (float)__builtin_amdgcn_ballot_w64(hit);
-                    if constexpr (REC) {
+                    if constexpr (REC == 4) {
+                        hm |= hit ? 1u << mb : 0u;
+                    } else if constexpr (REC == 3) {
+                        // record mode through the wave's LDS buffer: the block row's
+                        // records are staged at lcnt + rank; a full buffer is written
+                        // out first; a block row larger than the buffer stores directly
+                        const unsigned long long m = __builtin_amdgcn_ballot_w64(hit);
+                        if (m) {
+                            const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                            const int pc = __popcll(m);
+                            if (lcnt + pc > H1_LRC) {
+                                nst += flush_rec(cnt - lcnt, lcnt);
+                                lcnt = 0;
+                            }
+                            if (pc <= H1_LRC) {
+                                if (hit) {
+                                    uint4* d = reinterpret_cast<uint4*>(lrec + (wave * H1_LRC + lcnt + rk) * 80);
+                                    d[0] = make_uint4((uint32_t)mb | ((uint32_t)lid << 8), 0u, 0u, 0u);
+#pragma unroll
+                                    for (int nb = 0; nb < 4; ++nb)
+                                        d[1 + nb] = make_uint4(__float_as_uint(acc[mb][nb][0]), __float_as_uint(acc[mb][nb][1]),
+                                                               __float_as_uint(acc[mb][nb][2]), __float_as_uint(acc[mb][nb][3]));
+                                }
+                                lcnt += pc;
+                            } else {
+                                if (hit) {
+                                    uint2* rec = regr + (int64_t)min(cnt + rk, rcw - 1) * H1_REC;
+                                    rec[0] = make_uint2((uint32_t)mb | ((uint32_t)lid << 8), 0u);
+                                    float4* ra = reinterpret_cast<float4*>(rec + 2);
+#pragma unroll
+                                    for (int nb = 0; nb < 4; ++nb)
+                                        ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
+                                }
+                                nst += 5;
+                            }
+                            cnt += pc;
+                        }
+                    } else if constexpr (REC) {
                         // record mode: a lane with a passing pair in this block row
                         // stores its 16 accumulators (k_bucket applies the same tests)
                         const unsigned long long m = __builtin_amdgcn_ballot_w64(hit);
@@ -2005,6 +2069,9 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                 filt(std::true_type{});
             else
                 filt(std::false_type{});
+            if constexpr (REC == 3) {
+                if (lcnt) nst += flush_rec(cnt - lcnt, lcnt);
+            }
             if (!REC && (cnt & 63)) {  // the partial last chunk
                 const int e = (cnt & ~63) + lane;
                 if constexpr (DIAG == 5) {
@@ -2014,9 +2081,41 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                     ++nst;
                 }
             }
-            if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;
-            ++nst;
+            if constexpr (REC == 4) {
+                pend = 1;
+                pend_L = L;
+            } else {
+                if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;
+                ++nst;
+            }
         }
+    };
+    auto store_pending = [&]() {  // REC 4: the pending tile's records (as REC 1 stores them)
+        const int rcw = a.rcap / (8 * H1_REC);
+        uint2* regr = a.region + (pend_L * 8 + wave) * (int64_t)(rcw * H1_REC);
+        int cnt = 0;
+#pragma unroll
+        for (int mb = 0; mb < 8; ++mb) {
+            const bool hit = (hm >> mb) & 1u;
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(hit);
+            if (m) {
+                const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                if (hit) {
+                    uint2* rec = regr + (int64_t)min(cnt + rk, rcw - 1) * H1_REC;
+                    rec[0] = make_uint2((uint32_t)mb | ((uint32_t)lane << 8), 0u);
+                    float4* ra = reinterpret_cast<float4*>(rec + 2);
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb)
+                        ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
+                }
+                nst += 5;
+                cnt += __popcll(m);
+            }
+        }
+        if (lane == 0) a.region_cnt[pend_L * 8 + wave] = cnt;
+        ++nst;
+        hm = 0;
+        pend = 0;
     };
 
     constexpr int VMC = vmcnt_imm(2 * PS * (D - 1));
@@ -2084,6 +2183,9 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
             produce();
             ++ps;
         }
+        if constexpr (EPI == 1 && REC == 4) {
+            if (pend) store_pending();
+        }
         const bool tail = x + 1 + D > S;  // fewer than D slices left in flight: retire them all
         if (g == 1) {
             if (tail)
@@ -2126,6 +2228,9 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
             nst = 0;
         }
         __builtin_amdgcn_s_barrier();
+    }
+    if constexpr (EPI == 1 && REC == 4) {
+        if (pend) store_pending();  // the last tile's records
     }
     if (g == 0) __builtin_amdgcn_s_barrier();  // evens the barrier count
     __builtin_amdgcn_s_waitcnt(VMCNT0);
@@ -2199,6 +2304,8 @@ static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
         case 33: return launch_h1_pp16_t<EPI, EPI ? 6 : 0>(a, s);
         case 34: return launch_h1_pp16_t<EPI, 0, EPI>(a, s);
         case 35: return launch_h1_pp16_t<EPI, 0, EPI ? 2 : 0>(a, s);
+        case 36: return launch_h1_pp16_t<EPI, 0, EPI ? 3 : 0>(a, s);
+        case 37: return launch_h1_pp16_t<EPI, 0, EPI ? 4 : 0>(a, s);
         case 2: return launch_ring_t<2, 4, 4, 2, RING_H1, 4, 2, EPI>(a, s);
         case 3: return launch_ring_t<2, 4, 4, 2, RING_H1, 1, 4, EPI>(a, s);
         case 4: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 4, EPI>(a, s);
@@ -2255,7 +2362,7 @@ bool h1_timing_diag(int variant) {
 int h1_region_split(int variant) { return variant >= 18 ? 8 : 1; }  // (an effective variant)
 // the variant's regions hold records (H1_REC uint2 each: a lane's 16 accumulators of one
 // block row, tested by k_bucket) instead of passing pairs
-bool h1_records(int variant) { return variant == 34 || variant == 35; }
+bool h1_records(int variant) { return variant >= 34 && variant <= 37; }
 int launch_h1_sample(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<0>(a, variant, s); }
 int launch_h1_filter(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<1>(a, variant, s); }
 

@@ -140,3 +140,29 @@ def test_fullsize_c5_exact(H, O):
     for b, want in _check_oracle_distances(O, 0, X, Q, keys, cnt, rows=64):
         assert np.array_equal(dist[b, : cnt[b]].view(np.uint32), want.view(np.uint32)), b
     g.close()
+
+
+@pytest.mark.parametrize("tile", [34, 36, 37])
+@pytest.mark.parametrize("metric,k", [("cosine", 10), ("cosine", 256), ("l2", 64)])
+def test_exact_record_variants(H, O, tile, metric, k):
+    """The record-mode fused filters -- direct record stores (34) and records
+    staged in a per-wave LDS buffer, written out coalesced (36) -- certify to the
+    f32-input results bitwise.  Ragged row and query tiles; k = 256 widens the
+    threshold so block rows exceed the 32-record LDS buffer (its direct path)."""
+    n, d, B = 300_007, 1536, 700
+    X = _gen(n, d, 57, metric)
+    Q = _gen(B, d, 58, metric)
+    dist = H.CosineDistance if metric == "cosine" else H.EuclideanDistance
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=dist, Rng=5, build_mode=H.BUILD_FLAT)
+    g.reserve(n, d)
+    g.add_device(np.arange(n), X.data_ptr(), n, d)
+    g.set_option("exact_precision", 0)
+    ref = _search(g, Q, k, H.MODE_EXACT, 0)
+    g.set_option("exact_precision", 3)
+    g.set_option("exact_tile", tile)
+    g.reset_stats()
+    got = _search(g, Q, k, H.MODE_EXACT, 0)
+    for a, b in zip(ref, got):
+        assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8)), tile
+    assert (got[2] == k).all()
+    g.close()
