@@ -69,7 +69,8 @@ struct mhnsw_index {
     int vis_log2 = 12;
     int vis_entries = 0;      // beam search's visited set; 0 = 1.25 * 2^vis_log2 (beam_vis_entries)
     int exact_kk = 0;
-    int exact_sample = 32;   // fused preselection: row tiles in the threshold sample (about; stride = tiles / this)
+    int exact_sample = 64;   // fused preselection: row tiles in the threshold sample (at most; stride = ceil(tiles / this))
+    int exact_thr_rank = 0;  // fused preselection: the sample's J-th best is the threshold (0 = max(k, kk / 8))
     int exact_precision = 3;  // scores: 0 f32-input MFMA, 1 bf16x3 split, 2 fp16 2-product split,
                               // 3 fp16 1-product with the fused preselection (all certified, same results)
     int exact_tile = 0;       // bf16x3 GEMM tile variant (exact.hip launch_exact_scores_x3)
@@ -1178,9 +1179,9 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         const int ev = h1_effective_variant(h->exact_tile, h->pitch, std::max<int64_t>(qc, h->capn));
         const int bm = h1_tile_bm(ev);
         const int64_t nnt = (h->n + H1_BN - 1) / H1_BN, nqt = (qc + bm - 1) / bm;
-        const int stride = (int)std::max<int64_t>(1, std::min<int64_t>(128, nnt / h->exact_sample));
+        const int stride = (int)std::max<int64_t>(1, std::min<int64_t>(128, (nnt + h->exact_sample - 1) / h->exact_sample));
         const int64_t nsamp = h1 ? ((h->n / H1_BN) - 1) / stride + 1 : 0;  // sampled full tiles
-        const int J = stride >= 8 ? std::max(k, kk / 4) : kk;
+        const int J = stride < 8 ? kk : h->exact_thr_rank > 0 ? std::min(kk, std::max(k, h->exact_thr_rank)) : std::max(k, kk / 8);
         int sseg = 1;
         int64_t sseglen = 0;
         if (h1) {
@@ -1637,6 +1638,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "vis_log2") {
         if (v < 6 || v > 15) return fail(h, MHNSW_EINVAL, "vis_log2 must be in [6, 15]");
         h->vis_log2 = (int)v;
+    } else if (n == "exact_thr_rank") {
+        if (v < 0 || v > 256) return fail(h, MHNSW_EINVAL, "exact_thr_rank must be in [0, 256]");
+        h->exact_thr_rank = (int)v;
     } else if (n == "exact_sample") {
         if (v < 1 || v > 1 << 20) return fail(h, MHNSW_EINVAL, "exact_sample must be in [1, 2^20]");
         h->exact_sample = (int)v;
@@ -1704,6 +1708,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "vis_entries") *v = beam_vis_entries(h);
     else if (n == "exact_kk") *v = h->exact_kk;
     else if (n == "exact_sample") *v = h->exact_sample;
+    else if (n == "exact_thr_rank") *v = h->exact_thr_rank;
     else if (n == "exact_precision") *v = h->exact_precision;
     else if (n == "exact_tile") *v = h->exact_tile;
     else if (n == "compat_waves") *v = h->compat_waves;

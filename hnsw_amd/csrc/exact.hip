@@ -2453,49 +2453,76 @@ __global__ __launch_bounds__(64) void k_bucket(const uint2* region, const int32_
 __global__ __launch_bounds__(512) void k_bucket_rec(const uint2* region, const int32_t* region_cnt, int rcap,
                                                     int64_t nqt, int64_t B, int32_t* qcnt, uint2* bucket, int scap,
                                                     uint8_t* qovf, ExactArgs a) {
-    __shared__ float sc_c[256], sc_s[256];
+    // the tile's constants, row and query norms in LDS; the wave's count and its
+    // first 16 records are loaded beside them (a region holds >= 64 records, so
+    // the loads past the count stay inside it and are discarded): one round trip
+    // before the tests instead of a chain of dependent loads per record
+    constexpr int U = 4;  // records per lane group in flight (16 per wave)
+    __shared__ float sc_c[256], sc_s[256], sx_i[256], sx_n[256], sq_i[256], sq_n[256];
     __shared__ float4 sc_w[256];
     const int64_t t = blockIdx.x;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int64_t nt = t / nqt;
     const int64_t q0 = (t % nqt) * 256, n0 = nt * 256;
     const int sub = (int)(nt % H1_BSUB);
-    if (tid < 256) {
-        sc_c[tid] = a.ring_c[q0 + tid];  // (ring_c / ring_s are padded to the 256-query tile)
-        sc_s[tid] = a.metric == COSINE ? 0.f : a.ring_s[q0 + tid];
-        const int64_t row = n0 + tid;
-        sc_w[tid] = a.xw[row < a.N ? row : a.N - 1];
-    }
-    __syncthreads();
     const int rpw = rcap / 8, rcw = rpw / H1_REC;  // uint2 / records per wave region
     const int64_t ri = t * 8 + w;
     const int n = region_cnt[ri];
+    const uint2* reg = region + ri * (int64_t)rpw;
+    const int pr = lane & 15;
+    uint32_t hd[U];
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint2* rec = reg + (int64_t)((lane >> 4) + 4 * u) * H1_REC;
+        hd[u] = rec[0].x;
+        v[u] = reinterpret_cast<const float*>(rec + 2)[pr];
+    }
+    if (tid < 256) {
+        sc_c[tid] = a.ring_c[q0 + tid];  // (ring_c / ring_s are padded to the 256-query tile)
+        sc_s[tid] = a.metric == COSINE ? 0.f : a.ring_s[q0 + tid];
+        const int64_t row = min<int64_t>(n0 + tid, a.N - 1), q = min<int64_t>(q0 + tid, B - 1);
+        sc_w[tid] = a.xw[row];
+        sx_i[tid] = a.xinv[row];
+        sx_n[tid] = a.xnorm[row];
+        sq_i[tid] = a.qinv[q];
+        sq_n[tid] = a.qnorm[q];
+    }
+    __syncthreads();
     if (n > rcw) {
         for (int64_t q = q0 + (w >> 2) * 128 + lane; q < q0 + (w >> 2) * 128 + 128 && q < B; q += 64) qovf[q] = 1;
     }
     const int m = min(n, rcw);
-    const uint2* reg = region + ri * (int64_t)rpw;
-    const int wr = w >> 2, wc = w & 3, pr = lane & 15, nb = pr >> 2, r = pr & 3;
-    for (int e0 = 0; e0 < m; e0 += 4) {
-        const int e = e0 + (lane >> 4);
-        if (e >= m) break;
-        const uint2* rec = reg + (int64_t)e * H1_REC;
-        const uint32_t hd = rec[0].x;
-        const float v = reinterpret_cast<const float*>(rec + 2)[pr];
-        const int mb = (int)(hd & 0xFFu), sl = (int)(hd >> 8);
-        const int ro = wc * 64 + nb * 16 + (sl & 15), qo = wr * 128 + mb * 16 + 4 * (sl >> 4) + r;
-        const int64_t row = n0 + ro, q = q0 + qo;
-        const float4 xw = sc_w[ro];
-        // the fused filter's test (k_h1_pp16), on the same accumulator and constants
-        float tv;
-        if (a.metric == COSINE)
-            tv = fmaf(-sc_c[qo], xw.x, v);
-        else
-            tv = v - fmaf(sc_c[qo], xw.x, xw.y * sc_s[qo]);
-        if (!(tv < 0.f) && row < a.N && xw.z == 0.f && q < B) {
-            const float sc = split_score(RING_H1, a.metric, v, a.xinv[row], a.qinv[q], a.qnorm[q], a.xnorm[row]);
-            const int pos = atomicAdd(&qcnt[(q * H1_BSUB + sub) * H1_CSTRIDE], 1);
-            if (pos < scap) bucket[(q * H1_BSUB + sub) * scap + pos] = make_uint2((uint32_t)row, __float_as_uint(sc));
+    const int wr = w >> 2, wc = w & 3, nb = pr >> 2, r = pr & 3;
+    for (int e0 = 0; e0 < m; e0 += 4 * U) {
+        if (e0 > 0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = min(e0 + (lane >> 4) + 4 * u, rcw - 1);
+                const uint2* rec = reg + (int64_t)e * H1_REC;
+                hd[u] = rec[0].x;
+                v[u] = reinterpret_cast<const float*>(rec + 2)[pr];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = e0 + (lane >> 4) + 4 * u;
+            if (e >= m) break;
+            const int mb = (int)(hd[u] & 0xFFu), sl = (int)(hd[u] >> 8);
+            const int ro = wc * 64 + nb * 16 + (sl & 15), qo = wr * 128 + mb * 16 + 4 * (sl >> 4) + r;
+            const int64_t row = n0 + ro, q = q0 + qo;
+            const float4 xw = sc_w[ro];
+            // the fused filter's test (k_h1_pp16), on the same accumulator and constants
+            float tv;
+            if (a.metric == COSINE)
+                tv = fmaf(-sc_c[qo], xw.x, v[u]);
+            else
+                tv = v[u] - fmaf(sc_c[qo], xw.x, xw.y * sc_s[qo]);
+            if (!(tv < 0.f) && row < a.N && xw.z == 0.f && q < B) {
+                const float sc = split_score(RING_H1, a.metric, v[u], sx_i[ro], sq_i[qo], sq_n[qo], sx_n[ro]);
+                const int pos = atomicAdd(&qcnt[(q * H1_BSUB + sub) * H1_CSTRIDE], 1);
+                if (pos < scap) bucket[(q * H1_BSUB + sub) * scap + pos] = make_uint2((uint32_t)row, __float_as_uint(sc));
+            }
         }
     }
 }

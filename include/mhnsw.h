@@ -77,8 +77,10 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * "build_expand" (batched insert: entries expanded per step of its layer
  * searches, 1-4, default 2 -- they fetch their adjacency rows in one round
  * trip and evaluate their new neighbours as one batch), "exact_kk",
- * "exact_sample" (precision 3: about this many row tiles form the threshold
- * sample, default 32),
+ * "exact_thr_rank" (precision 3: the threshold is the sample's J-th best score,
+ * J = max(k, this) capped at kk; 0 (default) = max(k, kk / 8)),
+ * "exact_sample" (precision 3: at most this many row tiles form the threshold
+ * sample, every ceil(tiles / this)-th, default 64),
  * "exact_precision" (exact-mode scoring: 0 f32-input MFMA, 1 bf16x3 split MFMA,
  * 2 fp16 2-product split MFMA, 3 (default) fp16 1-product MFMA with the top-kk
  * preselection fused into the GEMM epilogue; all preselect, re-rank canonically

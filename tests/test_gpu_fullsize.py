@@ -166,3 +166,25 @@ def test_exact_record_variants(H, O, tile, metric, k):
         assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8)), tile
     assert (got[2] == k).all()
     g.close()
+
+
+@pytest.mark.parametrize("metric,k,rank", [("cosine", 10, 10), ("l2", 64, 16), ("cosine", 1, 1)])
+def test_exact_threshold_rank(H, O, metric, k, rank):
+    """A lower threshold rank (exact_thr_rank: the sample's J-th best, J >= k)
+    passes fewer pairs through the fused filter; results stay bit-identical to
+    the f32-input exact path (certified, or redone by the canonical sweep)."""
+    n, d, B = 200_003, 1536, 513
+    X = _gen(n, d, 61, metric)
+    Q = _gen(B, d, 62, metric)
+    dist = H.CosineDistance if metric == "cosine" else H.EuclideanDistance
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=dist, Rng=5, build_mode=H.BUILD_FLAT)
+    g.reserve(n, d)
+    g.add_device(np.arange(n), X.data_ptr(), n, d)
+    g.set_option("exact_precision", 0)
+    ref = _search(g, Q, k, H.MODE_EXACT, 0)
+    g.set_option("exact_precision", 3)
+    g.set_option("exact_thr_rank", rank)
+    got = _search(g, Q, k, H.MODE_EXACT, 0)
+    for a, b in zip(ref, got):
+        assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8)), rank
+    g.close()

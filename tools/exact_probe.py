@@ -28,6 +28,8 @@ g.set_option("exact_precision", prec)
 g.set_option("exact_tile", tile)
 if os.environ.get("EXACT_SAMPLE"):
     g.set_option("exact_sample", int(os.environ["EXACT_SAMPLE"]))
+if os.environ.get("EXACT_THR_RANK"):
+    g.set_option("exact_thr_rank", int(os.environ["EXACT_THR_RANK"]))
 S = Searcher(g, B, 10, d, dev)
 
 
@@ -42,8 +44,11 @@ def run():
 
 run()
 torch.cuda.synchronize()
+g.reset_stats()
 t0 = time.perf_counter()
 for _ in range(reps):
     run()
 torch.cuda.synchronize()
-print(f"precision={prec} tile={tile} ms_per_batch={(time.perf_counter() - t0) / reps * 1e3:.3f}", flush=True)
+dt = (time.perf_counter() - t0) / reps
+print(f"precision={prec} tile={tile} thr_rank={g.get_option('exact_thr_rank')} ms_per_batch={dt * 1e3:.3f} "
+      f"uncertified={g.stats().get('exact_uncertified')}", flush=True)
