@@ -60,7 +60,7 @@ def parse():
     p.add_argument("--nbase", type=int, default=1_000_000, help="vectors of the replica index")
     p.add_argument("--total-rows", type=int, default=10_000_000,
                    help="rows of the sharded index over all ranks (BASELINE configs[3]: 10M, 1.25M per rank at 8)")
-    p.add_argument("--configs", default="0,2,4,h",
+    p.add_argument("--configs", default="0,2,4",
                    help="secondary BASELINE configs measured at N=1 (configs[0] reference shape, [2] L2 build, "
                         "[4] exact, h harder data: latent 32 at ef up to 512); '' disables")
     p.add_argument("--dim", type=int, default=768)
