@@ -60,7 +60,7 @@ def parse():
     p.add_argument("--nbase", type=int, default=1_000_000, help="vectors of the replica index")
     p.add_argument("--total-rows", type=int, default=10_000_000,
                    help="rows of the sharded index over all ranks (BASELINE configs[3]: 10M, 1.25M per rank at 8)")
-    p.add_argument("--configs", default="0,2,4",
+    p.add_argument("--configs", default="0,2,4,h",
                    help="secondary BASELINE configs measured at N=1 (configs[0] reference shape, [2] L2 build, "
                         "[4] exact, h harder data: latent 32 at ef up to 512); '' disables")
     p.add_argument("--dim", type=int, default=768)
@@ -79,6 +79,8 @@ def parse():
                    help="1: fp16 screening copy, 0: plain f32 evaluation of every candidate; same results")
     p.add_argument("--ef-sweep", default="32,48,64,72,80,96,128,256",
                    help="extra operating points (ef values) reported at N=1; '' disables")
+    p.add_argument("--batch-sweep", default="1,1024,10000",
+                   help="query batch sizes re-measured at ef --ef on the same graph at N=1 (SURVEY 8(d) C2); '' disables")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--intrinsic", type=int, default=12)
     p.add_argument("--clusters", type=int, default=1000)
@@ -587,6 +589,22 @@ def main():
                            "kernel_ms": round(km, 4), "dist_evals_per_query": round(e_ / a.batch, 1),
                            "roofline_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
     at99 = next((p for p in points if p["recall_at_10"] >= 0.99), None)
+    # batch-size points (B in {1, 1024, 10000}): the same graph and ef,
+    # queries resident in HBM, wall time per batch over a fixed number of batches
+    bpoints = []
+    if world == 1 and a.batch_sweep:
+        for B in [int(x) for x in a.batch_sweep.split(",") if x]:
+            B = min(B, a.batch)
+            Sb = Searcher(g, B, a.k, a.dim, device)
+            Qb = Q[:B].contiguous()
+            reps = max(5, min(500, 200_000 // max(B, 1)))
+            Sb.run(Qb, H.MODE_BEAM, a.ef)
+            dt, _ = timed(lambda: Sb.run(Qb, H.MODE_BEAM, a.ef), reps=reps)
+            kb, _, nb = (x.clone() for x in Sb.run(Qb, H.MODE_BEAM, a.ef))
+            r = recall_at_k(kb[:ngt], nb[:ngt], tk[:B], tn[:B], a.k) if B <= ngt else None
+            bpoints.append({"batch": B, "ms_per_batch": round(dt * 1e3, 4), "qps": round(B / dt, 1),
+                            "batches_timed": reps, "recall_at_10": None if r is None else round(r, 4)})
+        g.device_status()
     traffic = None
     if os.path.exists(a.pmc_json):
         try:
@@ -644,6 +662,7 @@ def main():
         "cpu_baseline": None,
         "operating_points": points,
         "at_recall_0.99": at99,
+        "batch_points": bpoints,
     }
     if shard_out is not None and not shard_only:
         out["shard"] = shard_out

@@ -79,6 +79,7 @@ struct mhnsw_index {
     int screen = 1;           // beam search / batched insert fp16 screening copy (results unchanged)
     int fuse_descent = 1;     // batched insert: all greedy descents of a batch in one launch (same graph)
     int time_build = 0;       // batched insert: time its search kernels with HIP events (stats [12])
+    int64_t max_rows = 0;     // row capacity limit (0 = none): an Add past it fails with MHNSW_ENOMEM, index unchanged
     std::vector<hipEvent_t> tev;  // event pairs around the timed launches of the current Add
     size_t tev_used = 0;
     double build_search_us = 0;
@@ -154,6 +155,8 @@ struct mhnsw_index {
     DevBuf<uint8_t> xflag;
     DevBuf<uint8_t> xgone;     // exact path: rows to skip when some live row is not in layer 0
     int64_t partial_rows = 0;  // rows neither deleted nor in layer 0 (left by failed inserts, graph.go:1009)
+    uint64_t mut_epoch = 0;            // bumped by every Add / Delete / Import: row membership may have changed
+    uint64_t xgone_epoch = ~0ull;      // the epoch xgone was built at
     DevBuf<int32_t> xflagged, xnflag;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t gev0 = nullptr, gev1 = nullptr;  // the exact path's score GEMM (first query chunk)
@@ -328,6 +331,9 @@ int ensure_caps(mhnsw_index* h) {
 }
 
 int ensure_capacity(mhnsw_index* h, int64_t need) {
+    if (h->max_rows > 0 && need > h->max_rows)
+        return fail(h, MHNSW_ENOMEM, "row capacity limit: %lld rows > max_rows %lld", (long long)need,
+                    (long long)h->max_rows);
     if (need <= h->capn) return 0;
     int64_t nc = std::max<int64_t>(need, std::max<int64_t>(1024, h->capn * 2));
     if (h->capn > 0) nc = std::max<int64_t>(need, h->capn + h->capn / 2);
@@ -711,6 +717,7 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     int r = validate(h);
     if (r) return r;
     if (n <= 0) return 0;
+    ++h->mut_epoch;
     if (h->layers_exist && h->dim != dim)  // graph.go:955-960
         return fail(h, MHNSW_EDIM, "embedding dimension mismatch: %d != %d", h->dim, dim);
     if (!h->layers_exist && (r = set_shape(h, dim))) return r;
@@ -771,6 +778,8 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
         auto it = h->key2id.find(keys[i]);
         snap_key2id.emplace(keys[i], it == h->key2id.end() ? -1 : it->second);
     }
+    const size_t hm0 = h->hmask.size(), hd0 = h->hdead.size(), hl0 = h->hlevels.size(), hk0 = h->hkid.size();
+    const size_t nlay0 = h->layers.size();
     h->hmask.resize(n0 + n + 1, 0u);
     h->hdead.resize(n0 + n + 1, 0);
     int nl = top0 + 1;
@@ -822,6 +831,43 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     int64_t rep = -1, nfresh = 0;
     int rep_i0 = -1;
     int32_t old = -1;
+    // A host-detected failure after the bookkeeping began (a drawn level past
+    // MH_MAXL, a layer, capacity or staging allocation) leaves the index as it
+    // was: records, key maps, layers created by this call and the Rng back to
+    // their state before it (the reference has no such failure: Go panics on OOM).
+    // Nothing has reached the device yet when these can fail.
+    auto abort_add = [&](int rc) -> int {
+        for (size_t l = nlay0; l < h->layers.size(); ++l) {
+            Layer& L = h->layers[l];
+            (void)hipFree(L.deg);
+            (void)hipFree(L.adj);
+            (void)hipFree(L.adjd);
+        }
+        h->layers.resize(nlay0);
+        for (size_t l = 0; l < nlay0; ++l) {
+            h->layers[l].count = l < snap_layers.size() ? snap_layers[l].first : 0;
+            h->layers[l].entry = l < snap_layers.size() ? snap_layers[l].second : -1;
+        }
+        h->any_dead = snap_any_dead;
+        if (compat) {
+            for (auto& kv : snap_key2id) {
+                if (kv.second < 0)
+                    h->key2id.erase(kv.first);
+                else
+                    h->key2id[kv.first] = kv.second;
+            }
+        } else {
+            for (int64_t i = 0; i < nfresh; ++i) h->key2id.erase(keys[i]);  // all new (duplicates rejected above)
+        }
+        if (old >= 0 && (size_t)old < hd0) h->hdead[old] = 0;  // live until the sweep
+        for (auto& kv : snap_dead_kid) h->dead_kid[kv.first] = kv.second;
+        h->hlevels.resize(hl0);
+        h->hkid.resize(hk0);
+        h->hmask.resize(hm0);
+        h->hdead.resize(hd0);
+        h->rng = rng0;
+        return rc;
+    };
     {
         bool le = h->layers_exist;
         for (int64_t i = 0; i < n; ++i) {
@@ -834,10 +880,10 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
             } else {
                 l_i = random_level(h->ml, le, live0 + i, &h->rng);
             }
-            if (l_i >= MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "level %d >= %d", l_i, MH_MAXL);
+            if (l_i >= MH_MAXL) return abort_add(fail(h, MHNSW_EUNSUPPORTED, "level %d >= %d", l_i, MH_MAXL));
             le = true;
             lv.push_back(l_i);
-            if ((r = ensure_layer(h, l_i))) return r;
+            if ((r = ensure_layer(h, l_i))) return abort_add(r);
             if (compat) {
                 auto it = h->key2id.find(keys[i]);
                 if (it != h->key2id.end()) {
@@ -985,9 +1031,10 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
         return 0;
     };
     const int64_t n1 = n0 + nrows;
+    if ((r = ensure_capacity(h, n1))) return abort_add(r);
+    if (!vecs_on_device && (r = ensure_buf(h, h->tmp, (size_t)nproc * dim))) return abort_add(r);
     h->hmask.resize(n1);
     h->hdead.resize(n1);
-    if ((r = ensure_capacity(h, n1))) return r;
     // upload keys, levels, vectors (padded), norms
     HIPCHK(h, hipMemcpyAsync(h->keys + n0, rowkey.data(), nrows * sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipMemcpyAsync(h->levels + n0, h->hlevels.data() + n0, nrows * sizeof(int32_t), hipMemcpyHostToDevice,
@@ -1000,7 +1047,6 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     }
     const float* src = vecs;
     if (!vecs_on_device) {
-        if ((r = ensure_buf(h, h->tmp, (size_t)nproc * dim))) return r;
         HIPCHK(h, hipMemcpyAsync(h->tmp.p, vecs, (size_t)nproc * dim * 4, hipMemcpyHostToDevice, h->stream));
         src = h->tmp.p;
     }
@@ -1094,6 +1140,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
                 int32_t* out_ids, bool sticky) {
     int r = validate(h);
     if (r) return r;
+    h->have_gemm_timing = false;  // last_gemm_ns describes this search or none
     if (k <= 0) return fail(h, MHNSW_EK, "k must be greater than 0, got %d", k);  // graph.go:542-544
     if (h->layers_exist && h->dim != dim) {                                          // graph.go:547-552
         if (B == 1) return fail(h, MHNSW_EDIM, "embedding dimension mismatch: %d != %d", h->dim, dim);
@@ -1232,12 +1279,15 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         // insert that never reached layer 0 (graph.go:1009 leaves them in upper
         // layers only; Search cannot return them)
         const uint8_t* xdead = h->any_dead ? h->dead : nullptr;
-        if (h->partial_rows) {
-            std::vector<uint8_t> gone((size_t)h->n);
-            for (int64_t i = 0; i < h->n; ++i) gone[i] = h->hdead[i] || !in_layer(h, i, 0);
-            if ((r = ensure_buf(h, h->xgone, (size_t)std::max<int64_t>(h->n, 1)))) return r;
-            HIPCHK(h, hipMemcpyAsync(h->xgone.p, gone.data(), (size_t)h->n, hipMemcpyHostToDevice, s));
-            HIPCHK(h, hipStreamSynchronize(s));
+        if (h->partial_rows) {  // rebuilt only after a mutation
+            if (h->xgone_epoch != h->mut_epoch) {
+                std::vector<uint8_t> gone((size_t)h->n);
+                for (int64_t i = 0; i < h->n; ++i) gone[i] = h->hdead[i] || !in_layer(h, i, 0);
+                if ((r = ensure_buf(h, h->xgone, (size_t)std::max<int64_t>(h->n, 1)))) return r;
+                HIPCHK(h, hipMemcpyAsync(h->xgone.p, gone.data(), (size_t)h->n, hipMemcpyHostToDevice, s));
+                HIPCHK(h, hipStreamSynchronize(s));
+                h->xgone_epoch = h->mut_epoch;
+            }
             xdead = h->xgone.p;
         }
         g.dead = xdead;
@@ -1349,8 +1399,10 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
                                                    reinterpret_cast<float4*>(h->h1xw.p), s));
                     if (timing && q0 == 0) HIPCHK(h, hipEventRecord(h->gev0, s));
                     LCHK(h, launch_h1_filter(a, ev, s));
-                    if (timing && q0 == 0) HIPCHK(h, hipEventRecord(h->gev1, s));
-                    h->have_gemm_timing = timing;
+                    if (timing && q0 == 0) {
+                        HIPCHK(h, hipEventRecord(h->gev1, s));
+                        h->have_gemm_timing = true;
+                    }
                     const int64_t bqt = (nb + bm - 1) / bm;
                     LCHK(h, launch_bucket(h->h1region.p, h->h1rcnt.p, rcap, bqt * nnt, bqt, bm, H1_BN, nb, h->h1qcnt.p,
                                           h->h1bucket.p, scap, h->h1ovf.p, rsub, h1_records(ev) ? 1 : 0, a, s));
@@ -1647,7 +1699,7 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "exact_kk") {
         h->exact_kk = (int)v;
     } else if (n == "exact_tile") {
-        if (v < 0 || v > 37) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 37]");
+        if (v < 0 || v > 38) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 38]");
         h->exact_tile = (int)v;
     } else if (n == "upper_ef") {
         if (v < 1 || v > 64) return fail(h, MHNSW_EINVAL, "upper_ef must be in [1, 64]");
@@ -1657,6 +1709,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
         h->fuse_descent = (int)v;
     } else if (n == "time_build") {
         h->time_build = (int)(v != 0);
+    } else if (n == "max_rows") {
+        if (v < 0) return fail(h, MHNSW_EINVAL, "max_rows must be >= 0");
+        h->max_rows = v;
     } else if (n == "screen") {
         if (v < 0 || v > 1) return fail(h, MHNSW_EINVAL, "screen must be 0 or 1");
         if ((int)v == h->screen) return MHNSW_OK;
@@ -1716,6 +1771,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "screen") *v = h->screen;
     else if (n == "fuse_descent") *v = h->fuse_descent;
     else if (n == "time_build") *v = h->time_build;
+    else if (n == "max_rows") *v = h->max_rows;
     else if (n == "strkey_relabels") *v = h->relabels;
     else if (n == "strkeys") *v = (int64_t)h->s2l.size();
     else if (n == "pitch") *v = h->pitch;
@@ -1961,6 +2017,8 @@ void reset_graph(mhnsw_index* h) {
     h->hdead.clear();
     h->s2l.clear();
     h->l2s.clear();
+    h->partial_rows = 0;
+    h->xgone_epoch = ~0ull;
 }
 
 int import_csr(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t* keys, const float* vecs,
@@ -2040,6 +2098,11 @@ int import_csr(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t
         HIPCHK(h, hipMemcpy(h->kid, h->hkid.data(), (size_t)N * 4, hipMemcpyHostToDevice));
         HIPCHK(h, hipMemcpy(h->kidlive, live.data(), (size_t)N * 4, hipMemcpyHostToDevice));
     }
+    // live rows outside layer 0 (an exported graph keeps a failed insert's upper rows):
+    // the brute force skips them as the reference's Search cannot reach them
+    h->partial_rows = 0;
+    for (int64_t i = 0; i < N; ++i) h->partial_rows += !h->hdead[i] && !in_layer(h, i, 0);
+    ++h->mut_epoch;
     return 0;
 }
 
@@ -2516,6 +2579,7 @@ int mhnsw_delete(mhnsw_index* h, const int64_t* keys, int64_t n, uint8_t* out) {
     if (n > 0 && (!keys || !out)) return fail(h, MHNSW_EINVAL, "keys and out must be non-NULL");
     for (int64_t i = 0; i < n; ++i) out[i] = 0;
     if (n <= 0 || h->layers.empty()) return 0;
+    ++h->mut_epoch;
     std::vector<uint32_t> ids;
     for (int64_t i = 0; i < n; ++i) {
         auto it = h->key2id.find(keys[i]);

@@ -1751,6 +1751,17 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     // coalesced 16-B chunks (the ring and constants leave exactly 20 KiB of the 160)
     constexpr int H1_LRC = 32;
     __shared__ __attribute__((aligned(16))) uint8_t lrec[REC == 3 && EPI == 1 ? 8 * H1_LRC * 80 : 16];
+    // REC 5 (split roles): group 0 issues every LDS-DMA piece and never a global
+    // store on the fast path; its records go to an LDS buffer that its group-1
+    // partner (same wc) writes out, and group 1, which then waits on no DMA,
+    // stores its own records directly.  vmcnt retires in issue order
+    // (MI355X_MICROARCH.md), so a store issued by a wave that later waits for its
+    // own DMA stalls that wait until the store is acknowledged (~3k cycles under
+    // load); here no waiting wave has a store in flight.  SPC records per group-0
+    // wave (the ring and constants leave 20 KiB); more spill to direct stores.
+    constexpr bool SPL = REC == 5;
+    constexpr int SPC = 63;
+    __shared__ __attribute__((aligned(16))) uint8_t srec[SPL && EPI == 1 ? 4 * SPC * 80 + 16 : 16];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 2, wc = wave & 3;
@@ -1787,15 +1798,44 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     int p_kt = 0, p_slot = 0;
     const char* p_base = nullptr;  // the producer tile's first row in K-block 0
     int p_lim = 0;                 // its last valid image row (rows past B / N clamp to it)
+    // SPL: group 0 loads both images (its wave wcs the pieces group 1's wave wcs
+    // loads otherwise); the B image's base and limit
+    const int64_t ldB = a.ldXs;
+    const uint32_t pkB = (uint32_t)((dc >> 1) * ldB * 32 + (dc & 1) * 16);
+    const char* const planeB = reinterpret_cast<const char*>(a.Xh);
+    const char* pB_base = nullptr;
+    int pB_lim = 0;
     auto p_set = [&]() {
         const int64_t L = first + p_tile * wx;
         const int64_t qt = L % nqt, nt = L / nqt;
         const int64_t r0 = g == 0 ? qt * G_BM : (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
         p_base = plane + r0 * 32;
         p_lim = (int)min<int64_t>(255, (g == 0 ? a.B : a.N) - 1 - r0);
+        if constexpr (SPL) {
+            const int64_t rB = (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
+            pB_base = planeB + rB * 32;
+            pB_lim = (int)min<int64_t>(255, a.N - 1 - rB);
+        }
     };
     auto produce = [&]() {  // this wave's pieces of the producer slice, then advance it
-        if (DIAG < 3) {
+        if (SPL && DIAG < 3 && g == 0) {
+            const char* base = sbase(p_base + (int64_t)p_kt * PS * ld * 32);
+            const char* baseB = sbase(pB_base + (int64_t)p_kt * PS * ldB * 32);
+#pragma unroll
+            for (int i = 0; i < 2 * PS; ++i) {
+                const uint32_t off = (uint32_t)min(rr0 + RPP * i, p_lim) * 32 + pk;
+                uint8_t* dst = ring + p_slot * SL + (wcs * 2 * PS + i) * 1024;
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + off),
+                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 2 * PS; ++i) {
+                const uint32_t off = (uint32_t)min(rr0 + RPP * i, pB_lim) * 32 + pkB;
+                uint8_t* dst = ring + p_slot * SL + G_BM * RB + (wcs * 2 * PS + i) * 1024;
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(baseB + off),
+                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+            }
+        } else if (!SPL && DIAG < 3) {
             const char* base = sbase(p_base + (int64_t)p_kt * PS * ld * 32);
 #pragma unroll
             for (int i = 0; i < 2 * PS; ++i) {
@@ -1980,7 +2020,28 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                         if (m) {
                             const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                            if (hit) {
+                            if (SPL && g == 0) {
+                                // to the LDS buffer; past it (rare), stored directly
+                                if (hit) {
+                                    const int slot = cnt + rk;
+                                    if (slot < SPC) {
+                                        uint4* d = reinterpret_cast<uint4*>(srec + (wcs * SPC + slot) * 80);
+                                        d[0] = make_uint4((uint32_t)mb | ((uint32_t)lid << 8), 0u, 0u, 0u);
+#pragma unroll
+                                        for (int nb = 0; nb < 4; ++nb)
+                                            d[1 + nb] = make_uint4(__float_as_uint(acc[mb][nb][0]), __float_as_uint(acc[mb][nb][1]),
+                                                                   __float_as_uint(acc[mb][nb][2]), __float_as_uint(acc[mb][nb][3]));
+                                    } else {
+                                        uint2* rec = regr + (int64_t)min(slot, rcw - 1) * H1_REC;
+                                        rec[0] = make_uint2((uint32_t)mb | ((uint32_t)lid << 8), 0u);
+                                        float4* ra = reinterpret_cast<float4*>(rec + 2);
+#pragma unroll
+                                        for (int nb = 0; nb < 4; ++nb)
+                                            ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
+                                    }
+                                }
+                                if (cnt + __popcll(m) > SPC) nst += 5;
+                            } else if (hit) {
                                 const int slot = min(cnt + rk, rcw - 1);  // past the capacity: the last record (flagged)
                                 uint2* rec = regr + (int64_t)slot * H1_REC;
                                 float4* ra = reinterpret_cast<float4*>(rec + 2);
@@ -1998,7 +2059,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                                         ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
                                 }
                             }
-                            nst += 5;  // (at least 5 store instructions: never an over-count)
+                            if (!SPL) nst += 5;  // (at least 5 store instructions: never an over-count)
                             cnt += __popcll(m);
                         }
                     } else if (DIAG != 4 && __builtin_amdgcn_ballot_w64(hit)) {
@@ -2084,6 +2145,28 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
             if constexpr (REC == 4) {
                 pend = 1;
                 pend_L = L;
+            } else if constexpr (SPL) {
+                uint8_t* const cnts = srec + 4 * SPC * 80;
+                if (g == 0) {
+                    // the count beside the records; both visible to group 1 after the barrier
+                    if (lane == 0) *reinterpret_cast<int*>(cnts + wcs * 4) = cnt;
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                } else {
+                    if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;
+                    // the partner's records (group 0, wave wcs) of this tile, 64 chunks per store
+                    const int pc = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(cnts + wcs * 4));
+                    const int nch = min(pc, SPC) * 5;
+                    const uint4* src = reinterpret_cast<const uint4*>(srec + wcs * SPC * 80);
+                    uint2* regp = a.region + (L * 8 + wcs) * (int64_t)(rcw * H1_REC);
+                    for (int c0 = 0; c0 < nch; c0 += 64) {
+                        const int c = c0 + lid;
+                        if (c < nch) {
+                            const int i = c / 5, j = c - 5 * i;
+                            reinterpret_cast<uint4*>(regp + (int64_t)i * H1_REC)[j] = src[c];
+                        }
+                    }
+                    if (lane == 0) a.region_cnt[L * 8 + wcs] = pc;
+                }
             } else {
                 if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;
                 ++nst;
@@ -2118,11 +2201,12 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
         pend = 0;
     };
 
-    constexpr int VMC = vmcnt_imm(2 * PS * (D - 1));
+    constexpr int PIECES = (SPL ? 2 : 1) * 2 * PS;  // DMA pieces per slice of a loading wave
+    constexpr int VMC = vmcnt_imm(PIECES * (D - 1));
     constexpr int VMCNT0 = 0x0F70;
     auto wait_vmc = [&]() {
         if (nst > 0)
-            wait_vm_plus<2 * PS * (D - 1)>(nst, std::make_integer_sequence<int, 60>{});  // (vmcnt <= 63)
+            wait_vm_plus<PIECES * (D - 1)>(nst, std::make_integer_sequence<int, 52>{});  // (vmcnt <= 63)
         else
             __builtin_amdgcn_s_waitcnt(VMC);
     };
@@ -2173,7 +2257,19 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                 src = reinterpret_cast<const float*>(a.xw + min<int64_t>(n0 + wcs * 64 + lane, a.N - 1));
                 dst = cd + wcs * 1024;
             }
-            if (g == 1 || wcs < 2) {
+            if (SPL) {  // group 0 loads the row constants too
+                if (g == 0) {
+                    if (wcs < 2) {
+                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+                        ++nst;
+                    }
+                    const float* srcx = reinterpret_cast<const float*>(a.xw + min<int64_t>(n0 + wcs * 64 + lane, a.N - 1));
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(srcx),
+                                                     (__attribute__((address_space(3))) void*)(cd + wcs * 1024), 16, 0, 0);
+                    ++nst;
+                }
+            } else if (g == 1 || wcs < 2) {
                 __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
                                                  (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
                 ++nst;
@@ -2187,7 +2283,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
             if (pend) store_pending();
         }
         const bool tail = x + 1 + D > S;  // fewer than D slices left in flight: retire them all
-        if (g == 1) {
+        if (g == 1 && !SPL) {  // (SPL: group 1 loads nothing)
             if (tail)
                 __builtin_amdgcn_s_waitcnt(VMCNT0);
             else
@@ -2306,6 +2402,7 @@ static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
         case 35: return launch_h1_pp16_t<EPI, 0, EPI ? 2 : 0>(a, s);
         case 36: return launch_h1_pp16_t<EPI, 0, EPI ? 3 : 0>(a, s);
         case 37: return launch_h1_pp16_t<EPI, 0, EPI ? 4 : 0>(a, s);
+        case 38: return launch_h1_pp16_t<EPI, 0, EPI ? 5 : 0>(a, s);
         case 2: return launch_ring_t<2, 4, 4, 2, RING_H1, 4, 2, EPI>(a, s);
         case 3: return launch_ring_t<2, 4, 4, 2, RING_H1, 1, 4, EPI>(a, s);
         case 4: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 4, EPI>(a, s);
@@ -2362,7 +2459,7 @@ bool h1_timing_diag(int variant) {
 int h1_region_split(int variant) { return variant >= 18 ? 8 : 1; }  // (an effective variant)
 // the variant's regions hold records (H1_REC uint2 each: a lane's 16 accumulators of one
 // block row, tested by k_bucket) instead of passing pairs
-bool h1_records(int variant) { return variant >= 34 && variant <= 37; }
+bool h1_records(int variant) { return variant >= 34 && variant <= 38; }
 int launch_h1_sample(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<0>(a, variant, s); }
 int launch_h1_filter(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<1>(a, variant, s); }
 

@@ -107,6 +107,9 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * greedy), "screen" (beam mode and batched insert, default 1: keep an fp16
  * copy of the rows; a candidate is skipped only when the copy proves the f32
  * distance rejects it, so results are unchanged);
+ * "max_rows" (row capacity limit, 0 = none: an Add that would need more rows
+ * fails with MHNSW_ENOMEM and leaves the index, its key maps and its Rng as
+ * they were);
  * read-only: "pitch", "capacity", "strkeys", "strkey_relabels", "last_gemm_ns" (device
  *            time of the last timed exact search's fused fp16 score GEMM, first query chunk),
  *            "screen_err_ppb" (the fp16 screening copy's measured max relative

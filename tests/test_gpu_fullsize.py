@@ -1,18 +1,23 @@
-"""GPU parity at BASELINE.json's full sizes, through size-independent
-properties (the oracle itself only finishes small cases in seconds):
+"""GPU parity at BASELINE.json's full sizes, against the oracle on the same
+graph, plus size-independent properties:
 
-  configs[1]  1M x 768 cosine graph (the bench.py index): the fp16 screen never
-              changes a result (screen on == off, bitwise); every reported
-              distance equals the oracle's canonical distance of that pair
-              (sampled); lists sorted, keys unique; self-queries find
-              themselves; beam recall against the certified exact path.
+  configs[1]  1M x 768 cosine graph (the bench.py index): the engine's beam
+              result lists (keys, counts, distance bits) == the oracle's beam
+              search (graph.go:1047-1110 BatchSearch loop, ORDER_DEV) on the
+              exported graph for all 2048 queries, and its exact lists == the
+              oracle's brute force on 64 of them; the fp16 screen never changes
+              a result (screen on == off, bitwise); lists sorted, keys unique;
+              self-queries find themselves; beam recall vs the exact path.
   configs[2]  1M x 768 Euclidean batched insert (efConstruction 64): a
               well-formed graph (ids in range, no self loops, sets, degree
-              caps) reaching recall@10 >= 0.99 at ef 64.
-  configs[4]  1M x 1536 cosine exact path, batch 1024: f32-input and bf16x3
-              scores certify to the same results, equal to the oracle's
-              canonical distances on sampled pairs, self-queries first.
-Each builds in seconds on the GPU; vectors come from bench.gen_vectors."""
+              caps), beam lists == the oracle's on 1024 queries, exact == the
+              oracle's brute force on 32, recall@10 >= 0.99 at ef 64.
+  configs[4]  1M x 1536 cosine exact path, batch 1024: every precision
+              certifies to the same results, == the oracle's brute force
+              (keys + distance bits) on 32 queries, self-queries first.
+The oracle runs multi-threaded on the host's usable cores (bench.host_threads,
+the same concurrent Search as graph_benchmark_test.go:70-89).  Vectors come
+from bench.gen_vectors."""
 import numpy as np
 import pytest
 import torch
@@ -31,6 +36,30 @@ def _search(g, Q, k, mode, ef):
 
     S = Searcher(g, Q.shape[0], k, Q.shape[1], torch.device("cuda"))
     return [x.clone().cpu().numpy() for x in S.run(Q, mode, ef)]
+
+
+def _threads():
+    from bench import host_threads
+
+    return max(1, min(64, host_threads()))
+
+
+def _oracle_of(O, g, metric, M, M0, ef):
+    """the engine's graph exported (rows, layers, adjacency, entries) into the
+    oracle, which then searches it with the reference's algorithm"""
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, M0=M0, Ml=0.25, EfSearch=ef)
+    o.import_graph(**g.export())
+    return o
+
+
+def _same_lists(got, want, tag):
+    gk, gd, gn = got
+    rk, rd, rn = want
+    assert np.array_equal(gn, rn), tag
+    for b in range(len(gn)):
+        m = gn[b]
+        assert np.array_equal(gk[b, :m], rk[b, :m]), (tag, b)
+        assert np.array_equal(gd[b, :m].view(np.uint32), rd[b, :m].view(np.uint32)), (tag, b)
 
 
 def _check_lists(keys, dist, n, N):
@@ -76,6 +105,13 @@ def test_fullsize_c2_beam(H, O):
     _check_lists(ek, ed, en, n)
     rec = np.mean([len(set(keys[b]) & set(ek[b, : en[b]])) / 10 for b in range(B)])
     assert rec >= 0.98, rec
+    # the oracle's BatchSearch on the same graph: every list identical
+    o = _oracle_of(O, g, O.COSINE, 16, 40, 64)
+    Qh = Q.cpu().numpy()
+    _same_lists(on, o.search(Qh, 10, mode=O.MODE_BEAM, ef=64, threads=_threads()), "beam")
+    sub = np.arange(0, B, B // 64)[:64]
+    _same_lists((ek[sub], ed[sub], en[sub]), o.search(Qh[sub], 10, mode=O.MODE_EXACT, threads=_threads()), "exact")
+    del o
     # self-queries: a stored row finds itself first (distance 0 or the -1.19e-7 of parallel vectors)
     ids = np.random.default_rng(5).choice(n, 512, replace=False)
     sk, sd, sn = _search(g, X[torch.from_numpy(ids).cuda()].contiguous(), 10, H.MODE_BEAM, 64)
@@ -84,7 +120,7 @@ def test_fullsize_c2_beam(H, O):
     g.close()
 
 
-def test_fullsize_c3_build(H):
+def test_fullsize_c3_build(H, O):
     n, d, B = 1_000_000, 768, 1024
     X = _gen(n, d, 77, "euclidean")
     Q = _gen(B, d, 78, "euclidean")
@@ -111,6 +147,12 @@ def test_fullsize_c3_build(H):
     _check_lists(bk, bd, bn, n)
     rec = np.mean([len(set(bk[b, : bn[b]]) & set(ek[b, : en[b]])) / 10 for b in range(B)])
     assert rec >= 0.99, rec
+    o = _oracle_of(O, g, O.EUCLIDEAN, 16, 48, 64)
+    Qh = Q.cpu().numpy()
+    _same_lists((bk, bd, bn), o.search(Qh, 10, mode=O.MODE_BEAM, ef=64, threads=_threads()), "beam")
+    sub = np.arange(0, B, B // 32)[:32]
+    _same_lists((ek[sub], ed[sub], en[sub]), o.search(Qh[sub], 10, mode=O.MODE_EXACT, threads=_threads()), "exact")
+    del o
     g.close()
 
 
@@ -139,16 +181,25 @@ def test_fullsize_c5_exact(H, O):
     assert (keys[:16, 0] == ids).all()
     for b, want in _check_oracle_distances(O, 0, X, Q, keys, cnt, rows=64):
         assert np.array_equal(dist[b, : cnt[b]].view(np.uint32), want.view(np.uint32)), b
+    # the oracle's brute force (every row, canonical distances) on 32 queries, 16 of them self-queries
+    del X
+    o = _oracle_of(O, g, O.COSINE, 16, 16, 64)
+    sub = np.concatenate([np.arange(8), np.arange(16, B, (B - 16) // 24)[:24]])
+    want = o.search(Q.cpu().numpy()[sub], 10, mode=O.MODE_EXACT, threads=_threads())
+    del o
+    for p in (0, 3):
+        _same_lists(tuple(np.asarray(x)[sub] for x in res[p]), want, ("exact", p))
     g.close()
 
 
-@pytest.mark.parametrize("tile", [34, 36, 37])
+@pytest.mark.parametrize("tile", [34, 38])
 @pytest.mark.parametrize("metric,k", [("cosine", 10), ("cosine", 256), ("l2", 64)])
 def test_exact_record_variants(H, O, tile, metric, k):
-    """The record-mode fused filters -- direct record stores (34) and records
-    staged in a per-wave LDS buffer, written out coalesced (36) -- certify to the
-    f32-input results bitwise.  Ragged row and query tiles; k = 256 widens the
-    threshold so block rows exceed the 32-record LDS buffer (its direct path)."""
+    """The record-mode fused filters -- direct record stores (34) and split roles
+    (38: group 0 loads every slice and stages its records in LDS, group 1
+    stores both groups' records) -- certify to the f32-input results bitwise.
+    Ragged row and query tiles; k = 256 widens the threshold so group-0 waves
+    overflow their 63-record LDS buffer (its direct-store path)."""
     n, d, B = 300_007, 1536, 700
     X = _gen(n, d, 57, metric)
     Q = _gen(B, d, 58, metric)

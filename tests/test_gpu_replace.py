@@ -213,3 +213,55 @@ def test_batch_mode_rejects_present_keys(H):
     with pytest.raises(H.HnswError, match="compat build mode"):
         g.add_arrays(np.array([3]), X[:1])
     assert g.Len() == 50
+
+
+@pytest.mark.parametrize("compat,dup", [(True, False), (True, True), (False, False)])
+def test_add_capacity_failure_leaves_index_unchanged(H, O, compat, dup):
+    """An Add that fails on the host after its bookkeeping began (here the row
+    capacity limit, `max_rows`; in practice a device allocation) leaves the
+    index as it was: Len, layers, key maps and the engine's Rng.  The same Add
+    afterwards -- and every search -- then agrees with a twin index that never
+    saw the failure (the compat twin is also the oracle's graph: same levels,
+    same walk).  With `dup` the failing batch ends in a present key, so the
+    failure comes after the replacement's bookkeeping."""
+    rng = np.random.default_rng(31 + compat + 2 * dup)
+    n, m, d = 400, 40, 24
+    X = rng.uniform(-1, 1, (n + m, d)).astype(np.float32)
+    keys = np.arange(n + m, dtype=np.int64) * 3 + 7
+    Q = rng.uniform(-1, 1, (24, d)).astype(np.float32)
+    kw = {} if compat else dict(build_mode=H.BUILD_BATCH, m0=16, ef_construction=40, heuristic=2)
+    a = H.Graph(M=8, Ml=0.25, EfSearch=20, Distance=H.CosineDistance, Rng=9, **kw)
+    b = H.Graph(M=8, Ml=0.25, EfSearch=20, Distance=H.CosineDistance, Rng=9, **kw)
+    bk, bx = keys[n:], X[n:]
+    if dup:
+        bk, bx = np.concatenate([bk, keys[:1]]), np.concatenate([bx, X[:1]])
+    for g in (a, b):
+        g.add_arrays(keys[:n], X[:n])
+    a.set_option("max_rows", n + 10)
+    with pytest.raises(H.HnswError) as e:
+        a.add_arrays(bk, bx)
+    assert "max_rows" in str(e.value)
+    assert a.Len() == n and a.Topography() == b.Topography()
+    a.set_option("max_rows", 0)
+    errs = []
+    for g in (a, b):
+        try:
+            g.add_arrays(bk, bx)
+            errs.append(None)
+        except H.HnswError as e2:
+            errs.append(str(e2))
+    assert errs[0] == errs[1] and errs[0] == ("node not added" if dup else None), errs
+    ea, eb = a.export(), b.export()
+    for name in ("keys", "vecs", "deg", "adj", "entry", "dead"):
+        assert np.array_equal(np.asarray(ea[name]), np.asarray(eb[name])), name
+    modes = (H.MODE_COMPAT, H.MODE_BEAM, H.MODE_EXACT) if compat else (H.MODE_BEAM, H.MODE_EXACT)
+    for mode in modes:
+        ra, rb = a.search_arrays(Q, 10, mode=mode), b.search_arrays(Q, 10, mode=mode)
+        for x, y in zip(ra, rb):
+            assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8)), mode
+    if compat:  # and the twin is the oracle's graph
+        o = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=8, Ml=0.25, EfSearch=20)
+        o.import_graph(**eb)
+        _search_parity(H, O, b, o, Q)
+    a.close()
+    b.close()

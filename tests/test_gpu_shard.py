@@ -162,13 +162,15 @@ def test_sharded_engine_gloo_world2(H, O):
             _same_results(r0[0], r0[1], r0[2], fk, fd, fn)
 
 
-def test_config3_full_size(H):
+def test_config3_full_size(H, O):
     """BASELINE configs[3] at its stated size on one GPU: 10M x 768-d cosine in
     8 node-ID range shards of 1.25M rows, each built by the batched insert with
     the bench's graph recipe; every query searched on every shard and the
     per-shard top-k merged (the 8-GPU layout, each shard a separate handle).
     Sharded exact == the exact top-k of one flat index over all 10M rows,
-    bitwise; sharded beam (ef 64) recall@10 >= 0.99 against it."""
+    bitwise; sharded beam (ef 64) recall@10 >= 0.99 against it; the first and
+    last shards' beam lists == the oracle's beam search (graph.go:1047-1110) on
+    each exported shard graph for 512 queries (keys, counts, distance bits)."""
     torch = pytest.importorskip("torch")
     from bench import gen_vectors
     from hnsw_amd.shard import engine_local_search, merge_topk, shard_range
@@ -204,6 +206,17 @@ def test_config3_full_size(H):
         mk, md, mn = merge_topk(torch.stack([x[0] for x in lists]), torch.stack([x[1] for x in lists]),
                                 torch.stack([x[2] for x in lists]), k)
         res[name] = (mk.cpu().numpy(), md.cpu().numpy(), mn.cpu().numpy())
+        if mode == H.MODE_BEAM:
+            from bench import host_threads
+
+            Qh = Q[:512].cpu().numpy()
+            for s in (0, S - 1):
+                o = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=16, M0=40, Ml=0.25, EfSearch=64)
+                o.import_graph(**shards[s].export())
+                want = o.search(Qh, k, mode=O.MODE_BEAM, ef=64, threads=max(1, min(64, host_threads())))
+                del o
+                _same_results(*(x[:512].cpu().numpy() for x in lists[s]), *want)
+                print(f"shard {s}: 512 beam lists == oracle", flush=True)
     _same_results(*res["exact"], fk, fd, fn)
     mk, _, mn = res["beam"]
     rec = np.mean([len(set(mk[b, : mn[b]]) & set(fk[b, : fn[b]])) / k for b in range(B)])
