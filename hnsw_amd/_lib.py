@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmhnsw.so")
+# MHNSW_LIB: another build of the same ABI (tools/Makefile.diag's diagnostic library)
+LIB_PATH = os.environ.get("MHNSW_LIB") or os.path.join(_HERE, "libmhnsw.so")
 
 COSINE, EUCLIDEAN, NO_DISTANCE = 0, 1, -1
 MODE_COMPAT, MODE_BEAM, MODE_EXACT = 0, 1, 2

@@ -73,7 +73,7 @@ struct mhnsw_index {
     int exact_thr_rank = 0;  // fused preselection: the sample's J-th best is the threshold (0 = max(k, kk / 8))
     int exact_precision = 3;  // scores: 0 f32-input MFMA, 1 bf16x3 split, 2 fp16 2-product split,
                               // 3 fp16 1-product with the fused preselection (all certified, same results)
-    int exact_tile = 0;       // bf16x3 GEMM tile variant (exact.hip launch_exact_scores_x3)
+    int exact_tile = 0;       // GEMM variant (exact.hip: launch_split_scores, launch_h1)
     int compat_waves = 8;     // compat insert: waves scoring each distance batch (1 = the walking wave alone)
     int upper_ef = 1;         // beam search: upper-layer descent width
     int screen = 1;           // beam search / batched insert fp16 screening copy (results unchanged)
@@ -146,7 +146,7 @@ struct mhnsw_index {
     // exact_precision 3 (fp16 1-product, fused preselection): sample thresholds,
     // filter constants, tile regions + counts, per-query buckets, the queries' rounding
     DevBuf<float> h1thr, h1c, h1s, qerr;
-    DevBuf<float> h1xw;  // [4 capn] per-row filter constants of k_h1_pp (k_h1_rowconst)
+    DevBuf<float> h1xw;  // [4 capn] per-row filter constants of k_h1_pp16 (k_h1_rowconst)
     DevBuf<uint2> h1region, h1bucket;
     DevBuf<int32_t> h1rcnt, h1qcnt;
     DevBuf<uint8_t> h1ovf;
@@ -1221,8 +1221,8 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         // fused preselection (h1): the sample = every stride-th full row tile (about 32
         // tiles), its J-th best score per query is the threshold (J = kk when the
         // sample is every tile); a row passes at a rate of ~J / sample rows
-        // the GEMM variant this search runs (exact_tile 0: the default; a variant the
-        // shape does not admit falls back to k_h1_gemm)
+        // the GEMM variant this search runs (exact_tile 0: the default, k_h1_pp16; a shape
+        // it does not admit runs the ring kernel's filter)
         const int ev = h1_effective_variant(h->exact_tile, h->pitch, std::max<int64_t>(qc, h->capn));
         const int bm = h1_tile_bm(ev);
         const int64_t nnt = (h->n + H1_BN - 1) / H1_BN, nqt = (qc + bm - 1) / bm;
@@ -1238,7 +1238,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         // pairs per tile region / per query sub-bucket: 4x what the threshold lets
         // through on average (~J N / ns per query, ~bm J BN / ns per tile), with floors
         const int64_t ns = std::max<int64_t>(1, nsamp * H1_BN);
-        // (a multiple of 8: k_h1_pp splits each tile's region among its 8 waves)
+        // (a multiple of 8: k_h1_pp16 splits each tile's region among its 8 waves)
         // record-mode variants: per wave 4x the expected records (<= one per passing pair,
         // at most 8 block rows x 64 lanes), H1_REC uint2 each
         const int rcap = h1_records(ev)
@@ -1699,7 +1699,13 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "exact_kk") {
         h->exact_kk = (int)v;
     } else if (n == "exact_tile") {
-        if (v < 0 || v > 38) return fail(h, MHNSW_EINVAL, "exact_tile must be in [0, 38]");
+        // precisions 1 / 2: 0-3 (the split GEMM's tiles); precision 3: 0, 5 or 34 (the
+        // tools build, MH_EXACT_DIAG, also 30 / 31: timing diagnostics)
+        bool ok = (v >= 0 && v <= 3) || v == 5 || v == 34;
+#ifdef MH_EXACT_DIAG
+        ok = ok || v == 30 || v == 31;
+#endif
+        if (!ok) return fail(h, MHNSW_EINVAL, "exact_tile must be 0-3, 5 or 34");
         h->exact_tile = (int)v;
     } else if (n == "upper_ef") {
         if (v < 1 || v > 64) return fail(h, MHNSW_EINVAL, "upper_ef must be in [1, 64]");

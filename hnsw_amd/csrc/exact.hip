@@ -402,10 +402,7 @@ __device__ __forceinline__ float split_score(int mode, int metric, float acc, fl
 // tile_stride, 2 tile_stride, ..., into a compact [B x ns] sample matrix); EPI 1 keeps
 // only the pairs that can beat the query's threshold (RingFilter, below) --
 // the fused top-k: no score matrix.
-// DIAG (timing diagnostics, exact_tile 7-9; no pair passes, so every query
-// goes to the canonical fallback and results stay exact): 1 no epilogue, 2 also
-// no waits / barriers in the main loop, 3 also no DMA.
-template <int WAVES_M, int WAVES_N, int TM, int TN, int MODE, int S, int R, int EPI, int DIAG = 0>
+template <int WAVES_M, int WAVES_N, int TM, int TN, int MODE, int S, int R, int EPI>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_ring(ExactArgs a) {
     using T = RingTile<WAVES_M, WAVES_N, TM, TN, MODE, S>;
     static_assert(R >= 2 && R <= 4, "ring depth");
@@ -509,32 +506,17 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_ring(ExactArg
     constexpr int WAIT = (NWT & 15) | ((NWT >> 4) << 14) | (0x7 << 4) | (0xF << 8);
     uint16_t* const bufs[4] = {B0, B1, B2, B3};
 #pragma unroll
-    for (int p = 0; p < R - 1; ++p)
-        if (DIAG < 3) issue(bufs[p], p);
+    for (int p = 0; p < R - 1; ++p) issue(bufs[p], p);
     for (int kt = 0; kt < nst; kt += R) {
 #pragma unroll
         for (int u = 0; u < R; ++u) {
-            if (DIAG < 2) {
-                __builtin_amdgcn_s_waitcnt(WAIT);
-                __builtin_amdgcn_s_barrier();
-            }
-            if (DIAG < 3) issue(bufs[(u + R - 1) % R], kt + u + R - 1);
+            __builtin_amdgcn_s_waitcnt(WAIT);
+            __builtin_amdgcn_s_barrier();
+            issue(bufs[(u + R - 1) % R], kt + u + R - 1);
             if (u == 0 || kt + u < nst) stage(bufs[u]);
         }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no DMA may land after the workgroup ends
-    if constexpr (DIAG > 0) {
-        float keep = 0.f;  // keeps the MFMAs live
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) keep += acc[i][j][r];
-        __syncthreads();
-        if (tid == 0) a.region_cnt[logical] = keep == -1.0e38f ? 1 : 0;
-        return;
-    }
     // accumulator layout: D col = lane&31 (base row), row = (r&3) + 8*(r>>2) + 4*(lane>>5) (query)
     if constexpr (EPI == 0) {
         const int64_t col0 = EPI == 0 && a.nsample_tiles > 0 ? nt * T::BN : n0;  // sample: compact columns
@@ -654,13 +636,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void k_scores_ring(ExactArg
     }
 }
 
-template <int WM_, int WN_, int TM_, int TN_, int MODE, int S, int R, int EPI, int DIAG = 0>
+template <int WM_, int WN_, int TM_, int TN_, int MODE, int S, int R, int EPI>
 static int launch_ring_t(const ExactArgs& a, hipStream_t s) {
     using T = RingTile<WM_, WN_, TM_, TN_, MODE, S>;
     if (a.pitch % (X3K * S)) return -5;
     const int64_t nqt = (a.B + T::BM - 1) / T::BM;
     const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + T::BN - 1) / T::BN;
-    hipLaunchKernelGGL((k_scores_ring<WM_, WN_, TM_, TN_, MODE, S, R, EPI, DIAG>), dim3((unsigned)(nqt * nnt)), dim3(T::NT),
+    hipLaunchKernelGGL((k_scores_ring<WM_, WN_, TM_, TN_, MODE, S, R, EPI>), dim3((unsigned)(nqt * nnt)), dim3(T::NT),
                        0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -680,620 +662,9 @@ static int launch_split_scores(const ExactArgs& a, int tile, hipStream_t s) {
 int launch_exact_scores_x3(const ExactArgs& a, int tile, hipStream_t s) { return launch_split_scores<RING_X3>(a, tile, s); }
 int launch_exact_scores_x2h(const ExactArgs& a, int tile, hipStream_t s) { return launch_split_scores<RING_H2>(a, tile, s); }
 
-// ---------------------------------------------------------------------------
-// k_h1_gemm: the fp16 1-product scores (exact_precision 3) on a 256 x 256 block
-// tile (queries x rows) with 64-deep K-tiles, 8 waves of 128 x 64 on
-// v_mfma_f32_32x32x16_f16 (8 accumulators of 16 per lane).  Each block reads
-// 256 query rows and 256 base rows per K-tile: 2 x fewer L2 -> LDS bytes per
-// flop than the 128 x 256 ring.  Two 64-KiB LDS buffers, each a whole K-tile
-// (A then B, 128-B rows, 16-B chunk kc of row r at slot kc ^ ((r >> 1) & 7):
-// every 16-lane group of a fragment ds_read_b128 hits 16 distinct slots),
-// filled by LDS-DMA (global_load_lds_dwordx4, 8 per thread per K-tile: a
-// piece = 8 rows x 128 B, source pre-swizzled so the linear DMA image is the
-// swizzled one).  K-tile t + 1 streams into one buffer while the waves multiply
-// K-tile t out of the other; one wait + barrier per K-tile.  Per lane the
-// DMA source offsets are fixed; a K-tile only advances two scalar bases.
-// Epilogues as k_scores_ring's (EPI 0 sample scores, EPI 1 fused filter).
-// DIAG as k_scores_ring's (exact_tile 11-13: 1 no epilogue, 2 also no waits /
-// barriers, 3 also no DMA).
-// ---------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-constexpr int G_BM = 256, G_BN = 256, G_BK = 64;
-constexpr int G_BUF = (G_BM + G_BN) * G_BK * 2;  // 64 KiB per K-tile buffer
-
-template <int EPI, int DIAG = 0>
-__global__ __launch_bounds__(512) void k_h1_gemm(ExactArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t L0[G_BUF + 16];  // tail: the tile's region counter
-    __shared__ __attribute__((aligned(16))) uint8_t L1[G_BUF];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 2, wn = wave & 3;  // wave tile: queries wm*128.., rows wn*64..
-    // XCD-aware tile order (as k_scores_ring): each XCD walks a contiguous run of
-    // logical tiles, query tiles fastest, so a base tile enters its L2 once
-    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
-    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
-    const int64_t nblk = nqt * nnt;
-    const int64_t per = nblk / 8, rem = nblk % 8;
-    const int64_t xcd = blockIdx.x % 8, idx = blockIdx.x / 8;
-    const int64_t logical = xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
-    const int64_t qt = logical % nqt, nt = logical / nqt;
-    const int64_t q0 = qt * G_BM;
-    const int64_t n0 = (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
-    int* const tile_ctr = reinterpret_cast<int*>(L0 + G_BUF);
-    if (EPI == 1 && tid == 0) *tile_ctr = 0;  // ordered before the epilogue by the main loop's barriers
-
-    // DMA pieces of this wave: A pieces wv*4 + i and B pieces wv*4 + i (i < 4), a
-    // piece = image rows 8P .. 8P+7 (1 KiB).  Lane l: image row rr = 8P + l/8,
-    // slot l%8 holds chunk kc = (l%8) ^ ((rr >> 1) & 7) = halves 8kc .. 8kc+7 of
-    // the K-tile, which sit in K-block 2 kc'/.. of the 16-blocked plane: byte
-    // ((kc/2) ld + row) 32 + (kc%2) 16 from the tile's base.  Rows past B / N
-    // are clamped to the last row (valid loads; those outputs are never kept).
-    const int wv = __builtin_amdgcn_readfirstlane(wave);
-    uint32_t poff[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const bool isA = i < 4;
-        const int P = wv * 4 + (i & 3);
-        const int rr = P * 8 + (lane >> 3);
-        const int kc = (lane & 7) ^ ((rr >> 1) & 7);
-        const int64_t row0 = isA ? q0 : n0, rmax = isA ? a.B - 1 : a.N - 1, ld = isA ? a.ldQs : a.ldXs;
-        const int64_t rc = min(row0 + rr, rmax) - row0;
-        poff[i] = (uint32_t)((((int64_t)(kc >> 1)) * ld + rc) * 32 + (kc & 1) * 16);
-    }
-    const char* const abase = reinterpret_cast<const char*>(a.Qh + q0 * X3K);
-    const char* const bbase = reinterpret_cast<const char*>(a.Xh + n0 * X3K);
-    const int64_t astep = a.ldQs * X3K * 4 * 2, bstep = a.ldXs * X3K * 4 * 2;  // bytes per K-tile (4 K-blocks)
-    const int nkt = a.pitch / G_BK;
-    auto sbase = [](const char* p) {  // a wave-uniform pointer in scalar registers
-        const uint64_t u = reinterpret_cast<uint64_t>(p);
-        return reinterpret_cast<const char*>((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u) |
-                                             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32))
-                                              << 32));
-    };
-    // global_load_lds with the K-tile's base in scalar registers and the lane's
-    // 32-bit offset in a VGPR (saddr + voffset addressing)
-    // piece i of K-tile t into buf (i < 4: A, else B)
-    auto piece = [&](int t, uint8_t* buf, int i) {
-        const char* src = sbase((i < 4 ? abase + (int64_t)t * astep : bbase + (int64_t)t * bstep)) + poff[i];
-        uint8_t* dst = buf + (i < 4 ? 0 : G_BM * 128) + (wv * 4 + (i & 3)) * 1024;
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src), (__attribute__((address_space(3))) void*)dst,
-                                         16, 0, 0);
-    };
-    auto issue = [&](int t, uint8_t* buf) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) piece(t, buf, i);
-    };
-
-    f32x16 acc[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    // fragment of a 32-row block at k-step ks (16 deep): row lane & 31, chunk
-    // 2 ks + lane / 32; the block's first row is a multiple of 32, so the
-    // swizzle is ((lane & 31) >> 1) & 7
-    const int sw = ((lane & 31) >> 1) & 7;
-    int foff[4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) foff[ks] = (lane & 31) * 128 + (((2 * ks + (lane >> 5)) ^ sw) << 4);
-    const int arow = wm * 128 * 128, brow = G_BM * 128 + wn * 64 * 128;
-    // One K-tile per wave: 4 k-steps of 8 MFMAs (4 query blocks x 2 row blocks of
-    // 32); the next k-step's 6 fragments are read before this k-step's MFMAs
-    // (48 fragment registers live at most); sched_barrier keeps the steps apart
-    // so the scheduler cannot hoist every read of the tile.
-    // compute(buf, t, nbuf): multiply the K-tile in buf; with t >= 0 the 8 DMA
-    // pieces of K-tile t into nbuf go out two per k-step, between its MFMAs, so
-    // the vector-memory path drains while the wave keeps issuing MFMAs
-    auto compute = [&](const uint8_t* buf, int tn, uint8_t* nbuf) {
-        f16x8 fa[2][4], fb[2][2];
-        auto ld = [&](int ks, int slot) {
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-                fa[slot][m] = *reinterpret_cast<const f16x8*>(buf + arow + m * 32 * 128 + foff[ks]);
-#pragma unroll
-            for (int n = 0; n < 2; ++n)
-                fb[slot][n] = *reinterpret_cast<const f16x8*>(buf + brow + n * 32 * 128 + foff[ks]);
-        };
-        auto mma = [&](int slot, int m0) {
-#pragma unroll
-            for (int m = m0; m < m0 + 2; ++m)
-#pragma unroll
-                for (int n = 0; n < 2; ++n)
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[slot][m], fb[slot][n], acc[m][n], 0, 0, 0);
-        };
-        ld(0, 0);
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            __builtin_amdgcn_sched_barrier(0);
-            if (ks + 1 < 4) ld(ks + 1, (ks + 1) & 1);
-            mma(ks & 1, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            if (DIAG < 3 && tn >= 0) {
-                piece(tn, nbuf, 2 * ks);
-                piece(tn, nbuf, 2 * ks + 1);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            mma(ks & 1, 2);
-        }
-    };
-    constexpr int VMCNT0 = 0x0F70;  // s_waitcnt vmcnt(0) (lgkm / exp counters untouched)
-    auto sync = [&]() {
-        if (DIAG < 2) {
-            __builtin_amdgcn_s_waitcnt(VMCNT0);
-            __builtin_amdgcn_s_barrier();
-        }
-    };
-    if (DIAG < 3) issue(0, L0);
-    __builtin_amdgcn_s_waitcnt(VMCNT0);
-    __builtin_amdgcn_s_barrier();
-    // pairs of K-tiles (L0 then L1); an odd last K-tile runs after the loop (one
-    // loop exit keeps the accumulators in one register assignment)
-    int t = 0;
-    for (; t + 1 < nkt; t += 2) {  // (the DMA issued up front: spreading it over the k-steps measured slower)
-        if (DIAG < 3) issue(t + 1, L1);
-        compute(L0, -1, L1);
-        sync();
-        if (DIAG < 3 && t + 2 < nkt) issue(t + 2, L0);
-        compute(L1, -1, L0);
-        sync();
-    }
-    if (t < nkt) compute(L0, -1, L1);
-    if constexpr (DIAG > 0) {
-        __builtin_amdgcn_s_waitcnt(VMCNT0);  // no DMA may land after the workgroup ends
-        float keep = 0.f;                    // keeps the MFMAs live
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) keep += acc[i][j][r];
-        __syncthreads();
-        if (tid == 0) a.region_cnt[logical] = keep == -1.0e38f ? 1 : 0;
-        return;
-    }
-    // accumulator acc[mb][nb] (32 x 32): column = lane & 31 (base row), row =
-    // (r & 3) + 8 (r >> 2) + 4 (lane >> 5) (query)
-    const int li = lane & 31, lh = lane >> 5;
-    if constexpr (EPI == 0) {
-        const int64_t col0 = a.nsample_tiles > 0 ? nt * G_BN : n0;  // sample: compact columns
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-            const int ro = wn * 64 + nb * 32 + li;
-            const int64_t xr = n0 + ro;
-            if (xr >= a.N) continue;
-            const bool xok = !(a.dead && a.dead[xr]);
-            const float xn = a.xnorm[xr], xi = a.xinv[xr];
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int64_t qr = q0 + wm * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                    if (qr >= a.B) continue;
-                    float sc = split_score(RING_H1, a.metric, acc[mb][nb][r], xi, a.qinv[qr], a.qnorm[qr], xn);
-                    if (!xok) sc = __int_as_float(0x7f800000);
-                    a.scores[(size_t)qr * a.ldS + col0 + ro] = sc;
-                }
-        }
-    } else {
-        // the fused filter of k_scores_ring (same constants, same test, same entries)
-        bool rok[2];
-        float w0[2], w1[2];
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-            const int64_t xr = n0 + wn * 64 + nb * 32 + li;
-            rok[nb] = xr < a.N && !(a.dead && a.dead[xr]);
-            const int64_t xc = xr < a.N ? xr : a.N - 1;
-            const float xi = a.xinv[xc], xn = a.xnorm[xc];
-            if (a.metric == COSINE) {
-                w0[nb] = xn / xi;
-                w1[nb] = 0.f;
-            } else {
-                w0[nb] = 1.f / xi;
-                w1[nb] = xn * xn * 0.5f * (1.0f - 0x1p-20f) / xi;
-            }
-        }
-        uint2* reg = a.region + logical * (int64_t)a.rcap;
-        unsigned long long rokm[2];
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) rokm[nb] = __builtin_amdgcn_ballot_w64(rok[nb]);
-        auto epi = [&](auto cos_tag) {
-            constexpr bool COS = decltype(cos_tag)::value;
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb) {
-#pragma unroll
-                for (int r4 = 0; r4 < 4; ++r4) {
-                    const int64_t qb = q0 + wm * 128 + mb * 32 + 8 * r4 + 4 * lh;  // 4 consecutive queries
-                    const float4 c4 = *reinterpret_cast<const float4*>(a.ring_c + qb);
-                    const float cq[4] = {c4.x, c4.y, c4.z, c4.w};
-                    float sq[4] = {0.f, 0.f, 0.f, 0.f};
-                    if constexpr (!COS) {
-                        const float4 s4 = *reinterpret_cast<const float4*>(a.ring_s + qb);
-                        sq[0] = s4.x, sq[1] = s4.y, sq[2] = s4.z, sq[3] = s4.w;
-                    }
-#pragma unroll
-                    for (int r1 = 0; r1 < 4; ++r1) {
-#pragma unroll
-                        for (int nb = 0; nb < 2; ++nb) {
-                            const int r = r4 * 4 + r1;
-                            const float v = acc[mb][nb][r];
-                            float t;
-                            if constexpr (COS)
-                                t = fmaf(-cq[r1], w0[nb], v);
-                            else
-                                t = v - fmaf(cq[r1], w0[nb], w1[nb] * sq[r1]);
-                            const unsigned long long m = __builtin_amdgcn_ballot_w64(!(t < 0.f)) & rokm[nb];
-                            if (m) {
-                                const bool pass = (m >> lane) & 1ull;
-                                const int first = __ffsll((long long)m) - 1;
-                                int base = 0;
-                                if (lane == first) base = atomicAdd(tile_ctr, __popcll(m));
-                                base = __shfl(base, first, 64);
-                                if (pass) {
-                                    const int e = base + __builtin_amdgcn_mbcnt_hi(
-                                                             (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                                    const int qo = wm * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                                    const int ro = wn * 64 + nb * 32 + li;
-                                    if (e < a.rcap)
-                                        reg[e] = make_uint2((uint32_t)ro | ((uint32_t)qo << 16), __float_as_uint(v));
-                                }
-                            }
-                        }
-                    }
-                }
-            }
-        };
-        if (a.metric == COSINE)
-            epi(std::true_type{});
-        else
-            epi(std::false_type{});
-        __syncthreads();
-        if (tid == 0) a.region_cnt[logical] = *tile_ctr;
-    }
-}
-
-template <int EPI, int DIAG = 0>
-static int launch_h1_gemm_t(const ExactArgs& a, hipStream_t s) {
-    if (a.pitch % G_BK) return -5;
-    if ((3 * std::max(a.ldQs, a.ldXs) + G_BM) * 32 >= ((int64_t)1 << 32)) return -5;  // per-lane 32-bit DMA offsets
-    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
-    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
-    hipLaunchKernelGGL((k_h1_gemm<EPI, DIAG>), dim3((unsigned)(nqt * nnt)), dim3(512), 0, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// ---------------------------------------------------------------------------
-// k_h1_stream: k_h1_gemm's 256 x 256 block tile (8 waves of 128 x 64 on
-// v_mfma_f32_32x32x16_f16) as a persistent stream.  One workgroup per CU walks
-// its tiles back to back, and the LDS-DMA runs as one ring of 32-deep stages
-// over all of them: stage s + 3 (possibly of the next tile) streams in while
-// stage s is multiplied, and a tile's epilogue runs while the first stages of
-// the next tile are already in flight -- no per-tile prologue, no per-tile
-// launch, no exposed epilogue latency beyond its own instructions.
-//   ring: 4 stages x 32 KiB (A 256 rows then B 256 rows, 64-B rows = 32 halves
-//         of K); 16-B chunk kc of image row r sits at slot kc ^ ((r >> 2) & 3),
-//         so each 16-lane group of a fragment ds_read_b128 (rows {0-3, 12-15,
-//         20-27} / {4-11, 16-19, 28-31} of a 32-row block) hits 16 distinct slots.
-//   DMA:  a piece = 16 image rows x 64 B (1 KiB, one global_load_lds_dwordx4);
-//         per stage and wave 2 A + 2 B pieces, issued 2 per k-step between the
-//         MFMAs; lane l loads row 16 P + l / 4, slot l % 4, i.e. chunk
-//         kc = (l % 4) ^ ((l / 16) % 4) -- two 512-B runs of the 16-blocked planes.
-//   sync: per stage one counted vmcnt (the 2 younger stages stay in flight) and
-//         one s_barrier.  The fragment reads are inline ds_read_b128 with a
-//         tied s_waitcnt lgkmcnt(0) before their MFMAs: the compiler sees no LDS
-//         read of the ring, so it adds no vmcnt(0) for the DMA it cannot track
-//         through the ring's dynamic stage index.
-// Tile order: XCD x owns the contiguous logical range of k_h1_gemm (query tiles
-// fastest); its wx workgroups take every wx-th tile of it, so at any time the
-// XCD's CUs work on wx consecutive tiles (wx / nqt row tiles, each read from
-// HBM once into that XCD's L2).  DIAG as k_h1_gemm's (exact_tile 15-17).
-// ---------------------------------------------------------------------------
-constexpr int S_NB = 4, S_SK = 32;
-constexpr int S_BUF = (G_BM + G_BN) * S_SK * 2;  // 32 KiB per stage
-
-#define MH_DSR(dst, addr, off) asm volatile("ds_read_b128 %0, %1 offset:" #off : "=v"(dst) : "v"(addr))
-#define MH_LGKM0(f0, f1, f2, f3, f4, f5) \
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3), "+v"(f4), "+v"(f5))
-
-template <int EPI, int DIAG = 0>
-__global__ __launch_bounds__(512) void k_h1_stream(ExactArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring[S_NB * S_BUF];
-    __shared__ int tile_ctr;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 2, wn = wave & 3;
-    const int wv = __builtin_amdgcn_readfirstlane(wave);
-    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
-    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
-    const int64_t nblk = nqt * nnt;
-    const int W = gridDim.x, xcd = blockIdx.x % 8, jx = blockIdx.x / 8;
-    const int wx = W / 8 + (xcd < W % 8 ? 1 : 0);
-    const int64_t per = nblk / 8, rem = nblk % 8;
-    const int64_t lo = xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per;
-    const int64_t hi = lo + per + (xcd < rem ? 1 : 0);
-    const int64_t first = lo + jx;
-    const int64_t ntile = first < hi ? (hi - first + wx - 1) / wx : 0;
-    const int nkt = a.pitch / S_SK;
-    const int64_t S = ntile * nkt;
-    if (EPI == 1 && tid == 0) tile_ctr = 0;
-
-    // per-lane DMA constants: piece i (0, 1) of this wave = image rows
-    // 16 (2 wv + i) + lane / 4; chunk kc of the stage's 32 halves = K-block kc / 2
-    // (16-deep planes, 32 B per row), half kc % 2
-    const int kc = (lane & 3) ^ ((lane >> 4) & 3);
-    const uint32_t pkA = (uint32_t)((kc >> 1) * a.ldQs * 32 + (kc & 1) * 16);
-    const uint32_t pkB = (uint32_t)((kc >> 1) * a.ldXs * 32 + (kc & 1) * 16);
-    const int rr0 = wv * 32 + (lane >> 2);  // piece 1: + 16
-    const int64_t astep = a.ldQs * 64, bstep = a.ldXs * 64;  // bytes per stage (2 K-blocks)
-    auto sbase = [](const char* p) {
-        const uint64_t u = reinterpret_cast<uint64_t>(p);
-        return reinterpret_cast<const char*>((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u) |
-                                             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32))
-                                              << 32));
-    };
-    // producer: the stage being streamed in (tile p_tile of this workgroup, K-stage p_kt)
-    int64_t p_tile = 0;
-    int p_kt = 0;
-    const char *p_a = nullptr, *p_b = nullptr;
-    int p_la = 0, p_lb = 0;  // last valid image row of the tile (rows past B / N clamp to it)
-    auto p_set = [&]() {
-        const int64_t L = first + p_tile * wx;
-        const int64_t qt = L % nqt, nt = L / nqt;
-        const int64_t q0 = qt * G_BM;
-        const int64_t n0 = (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
-        p_a = reinterpret_cast<const char*>(a.Qh + q0 * X3K);
-        p_b = reinterpret_cast<const char*>(a.Xh + n0 * X3K);
-        p_la = (int)min<int64_t>(G_BM - 1, a.B - 1 - q0);
-        p_lb = (int)min<int64_t>(G_BN - 1, a.N - 1 - n0);
-    };
-    // piece i of the producer stage into ring stage slot `st`: 0, 1 A; 2, 3 B
-    auto piece = [&](int st, int i) {
-        const bool isA = i < 2;
-        const int rr = rr0 + (i & 1) * 16;
-        const char* base = sbase((isA ? p_a + (int64_t)p_kt * astep : p_b + (int64_t)p_kt * bstep));
-        const uint32_t off = (isA ? pkA : pkB) + (uint32_t)min(rr, isA ? p_la : p_lb) * 32;
-        uint8_t* dst = ring + st * S_BUF + (isA ? 0 : G_BM * 64) + (wv * 2 + (i & 1)) * 1024;
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + off),
-                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-    };
-    auto p_next = [&]() {
-        if (++p_kt == nkt) {
-            p_kt = 0;
-            if (++p_tile < ntile) p_set();
-        }
-    };
-
-    f32x16 acc[4][2];
-    auto zero = [&]() {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    };
-    zero();
-    // fragment addresses: row lane & 31 of a 32-row block, chunk 2 ks + lane / 32
-    // at slot chunk ^ (((lane & 31) >> 2) & 3); blocks at +2048 B
-    const uint32_t ring_lds = (uint32_t)reinterpret_cast<uintptr_t>(ring);
-    const int sw = ((lane & 31) >> 2) & 3;
-    const uint32_t lo0 = (lane & 31) * 64 + (((lane >> 5) ^ sw) << 4);
-    const uint32_t lo1 = (lane & 31) * 64 + (((2 + (lane >> 5)) ^ sw) << 4);
-    const uint32_t offA = wm * 128 * 64, offB = G_BM * 64 + wn * 64 * 64;
-    auto mma4 = [&](const f16x8* fa, const f16x8* fb, int m0) {
-#pragma unroll
-        for (int m = m0; m < m0 + 2; ++m)
-#pragma unroll
-            for (int n = 0; n < 2; ++n)
-                acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[m], fb[n], acc[m][n], 0, 0, 0);
-    };
-    // one stage: 2 k-steps of 8 MFMAs; the producer's 4 pieces go out 2 per k-step
-    auto compute = [&](int st, bool issue, int pst) {
-        const uint32_t rb = ring_lds + st * S_BUF;
-        const uint32_t va0 = rb + offA + lo0, vb0 = rb + offB + lo0, va1 = rb + offA + lo1, vb1 = rb + offB + lo1;
-        f16x8 fa0[4], fb0[2], fa1[4], fb1[2];
-        MH_DSR(fa0[0], va0, 0);
-        MH_DSR(fa0[1], va0, 2048);
-        MH_DSR(fa0[2], va0, 4096);
-        MH_DSR(fa0[3], va0, 6144);
-        MH_DSR(fb0[0], vb0, 0);
-        MH_DSR(fb0[1], vb0, 2048);
-        MH_LGKM0(fa0[0], fa0[1], fa0[2], fa0[3], fb0[0], fb0[1]);
-        MH_DSR(fa1[0], va1, 0);
-        MH_DSR(fa1[1], va1, 2048);
-        MH_DSR(fa1[2], va1, 4096);
-        MH_DSR(fa1[3], va1, 6144);
-        MH_DSR(fb1[0], vb1, 0);
-        MH_DSR(fb1[1], vb1, 2048);
-        __builtin_amdgcn_sched_barrier(0);
-        mma4(fa0, fb0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (DIAG < 3 && issue) {
-            piece(pst, 0);
-            piece(pst, 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        mma4(fa0, fb0, 2);
-        __builtin_amdgcn_sched_barrier(0);
-        MH_LGKM0(fa1[0], fa1[1], fa1[2], fa1[3], fb1[0], fb1[1]);
-        mma4(fa1, fb1, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (DIAG < 3 && issue) {
-            piece(pst, 2);
-            piece(pst, 3);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        mma4(fa1, fb1, 2);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    const int li = lane & 31, lh = lane >> 5;
-    float keep = 0.f;  // DIAG: keeps the MFMAs live
-    // the epilogue of the consumer's tile L (accumulator acc[mb][nb]: column =
-    // lane & 31 (base row), row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) (query))
-    auto epilogue = [&](int64_t L) {
-        const int64_t qt = L % nqt, nt = L / nqt;
-        const int64_t q0 = qt * G_BM;
-        const int64_t n0 = (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
-        if constexpr (DIAG > 0) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) keep += acc[i][j][r];
-        } else if constexpr (EPI == 0) {
-            const int64_t col0 = a.nsample_tiles > 0 ? nt * G_BN : n0;  // sample: compact columns
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                const int ro = wn * 64 + nb * 32 + li;
-                const int64_t xr = n0 + ro;
-                if (xr >= a.N) continue;
-                const bool xok = !(a.dead && a.dead[xr]);
-                const float xn = a.xnorm[xr], xi = a.xinv[xr];
-#pragma unroll
-                for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int64_t qr = q0 + wm * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                        if (qr >= a.B) continue;
-                        float sc = split_score(RING_H1, a.metric, acc[mb][nb][r], xi, a.qinv[qr], a.qnorm[qr], xn);
-                        if (!xok) sc = __int_as_float(0x7f800000);
-                        a.scores[(size_t)qr * a.ldS + col0 + ro] = sc;
-                    }
-            }
-        } else {
-            // the fused filter of k_scores_ring (same constants, same test, same entries)
-            bool rok[2];
-            float w0[2], w1[2];
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                const int64_t xr = n0 + wn * 64 + nb * 32 + li;
-                rok[nb] = xr < a.N && !(a.dead && a.dead[xr]);
-                const int64_t xc = xr < a.N ? xr : a.N - 1;
-                const float xi = a.xinv[xc], xn = a.xnorm[xc];
-                if (a.metric == COSINE) {
-                    w0[nb] = xn / xi;
-                    w1[nb] = 0.f;
-                } else {
-                    w0[nb] = 1.f / xi;
-                    w1[nb] = xn * xn * 0.5f * (1.0f - 0x1p-20f) / xi;
-                }
-            }
-            uint2* reg = a.region + L * (int64_t)a.rcap;
-            // the entry keys below are loop-invariant: laundering the lane id keeps
-            // the compiler from hoisting all 128 of them out of the stream (spills)
-            int lid = lane;
-            asm volatile("" : "+v"(lid));
-            const int eli = lid & 31, elh = lid >> 5;
-            unsigned long long rokm[2];
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) rokm[nb] = __builtin_amdgcn_ballot_w64(rok[nb]);
-            auto epi = [&](auto cos_tag) {
-                constexpr bool COS = decltype(cos_tag)::value;
-#pragma unroll
-                for (int mb = 0; mb < 4; ++mb) {
-#pragma unroll
-                    for (int r4 = 0; r4 < 4; ++r4) {
-                        const int64_t qb = q0 + wm * 128 + mb * 32 + 8 * r4 + 4 * lh;  // 4 consecutive queries
-                        const float4 c4 = *reinterpret_cast<const float4*>(a.ring_c + qb);
-                        const float cq[4] = {c4.x, c4.y, c4.z, c4.w};
-                        float sq[4] = {0.f, 0.f, 0.f, 0.f};
-                        if constexpr (!COS) {
-                            const float4 s4 = *reinterpret_cast<const float4*>(a.ring_s + qb);
-                            sq[0] = s4.x, sq[1] = s4.y, sq[2] = s4.z, sq[3] = s4.w;
-                        }
-#pragma unroll
-                        for (int r1 = 0; r1 < 4; ++r1) {
-#pragma unroll
-                            for (int nb = 0; nb < 2; ++nb) {
-                                const int r = r4 * 4 + r1;
-                                const float v = acc[mb][nb][r];
-                                float t;
-                                if constexpr (COS)
-                                    t = fmaf(-cq[r1], w0[nb], v);
-                                else
-                                    t = v - fmaf(cq[r1], w0[nb], w1[nb] * sq[r1]);
-                                const unsigned long long m = __builtin_amdgcn_ballot_w64(!(t < 0.f)) & rokm[nb];
-                                if (m) {
-                                    const bool pass = (m >> lane) & 1ull;
-                                    const int fl = __ffsll((long long)m) - 1;
-                                    int base = 0;
-                                    if (lane == fl) base = atomicAdd(&tile_ctr, __popcll(m));
-                                    base = __shfl(base, fl, 64);
-                                    if (pass) {
-                                        const int e = base + __builtin_amdgcn_mbcnt_hi(
-                                                                 (uint32_t)(m >> 32),
-                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                                        const int qo = wm * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * elh;
-                                        const int ro = wn * 64 + nb * 32 + eli;
-                                        if (e < a.rcap)
-                                            reg[e] = make_uint2((uint32_t)ro | ((uint32_t)qo << 16), __float_as_uint(v));
-                                    }
-                                }
-                            }
-                        }
-                    }
-                }
-            };
-            if (a.metric == COSINE)
-                epi(std::true_type{});
-            else
-                epi(std::false_type{});
-            __syncthreads();
-            if (tid == 0) {
-                a.region_cnt[L] = tile_ctr;
-                tile_ctr = 0;  // the next tile's atomics come after at least one more barrier
-            }
-        }
-    };
-
-    constexpr int VMCNT0 = 0x0F70, VMCNT8 = 0x0F78;  // s_waitcnt vmcnt(0) / vmcnt(8) = 2 stages x 4 pieces
-    static_assert(S_NB == 4, "VMCNT8 is 4 x (S_NB - 2)");
-    if (ntile > 0) p_set();
-    int64_t ps = 0;  // stages issued
-    for (; ps < S_NB - 1 && ps < S; ++ps) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (DIAG < 3) piece((int)ps, i);
-        p_next();
-    }
-    int64_t c_tile = 0;
-    int c_kt = 0;
-    for (int64_t s = 0; s < S; ++s) {
-        if (DIAG < 2) {
-            if (s + S_NB - 2 < S)
-                __builtin_amdgcn_s_waitcnt(VMCNT8);
-            else
-                __builtin_amdgcn_s_waitcnt(VMCNT0);
-            __builtin_amdgcn_s_barrier();
-        }
-        const bool issue = ps < S;
-        __builtin_amdgcn_s_setprio(1);
-        compute((int)(s & (S_NB - 1)), issue, (int)(ps & (S_NB - 1)));
-        __builtin_amdgcn_s_setprio(0);
-        if (issue) {
-            p_next();
-            ++ps;
-        }
-        if (++c_kt == nkt) {
-            epilogue(first + c_tile * wx);
-            zero();
-            c_kt = 0;
-            ++c_tile;
-        }
-    }
-    __builtin_amdgcn_s_waitcnt(VMCNT0);  // no DMA may land after the workgroup ends
-    if constexpr (DIAG > 0) {
-        __syncthreads();
-        if (tid == 0 && blockIdx.x < nblk) a.region_cnt[blockIdx.x] = keep == -1.0e38f ? 1 : 0;
-    }
-}
-#undef MH_DSR
-#undef MH_LGKM0
+constexpr int G_BM = 256, G_BN = 256;  // k_h1_pp16 tile: queries x rows
 
 static int device_cus() {
     static int cus = 0;
@@ -1308,45 +679,6 @@ static int device_cus() {
     return cus;
 }
 
-template <int EPI, int DIAG = 0>
-static int launch_h1_stream_t(const ExactArgs& a, hipStream_t s) {
-    if (a.pitch % S_SK) return -5;
-    if ((a.ldQs + G_BM) * 32 >= ((int64_t)1 << 32) || (a.ldXs + G_BN) * 32 >= ((int64_t)1 << 32))
-        return -5;  // per-lane 32-bit DMA offsets
-    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
-    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
-    const int64_t nblk = nqt * nnt;
-    const int64_t W = std::min<int64_t>(nblk, std::max(8, device_cus() / 8 * 8));
-    hipLaunchKernelGGL((k_h1_stream<EPI, DIAG>), dim3((unsigned)W), dim3(512), 0, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// ---------------------------------------------------------------------------
-// k_h1_pp: the 256 x 256 fp16 1-product tile as a persistent, two-group
-// ping-pong stream.  Waves 0-3 (group 0, query rows 0-127) and 4-7 (group 1,
-// rows 128-255) each hold one wave on every SIMD; group 1 runs one barrier
-// behind group 0, so in every barrier interval one wave of a SIMD multiplies
-// (8 x v_mfma_f32_32x32x16_f16, s_setprio 1) while the other reads its next
-// fragments and issues its share of the LDS-DMA, and the roles swap at the
-// barrier.  Per wave and K-slice (16 deep):
-//   R: 6 ds_read_b128 (4 A, 2 B fragments) from the slice's ring slot, 2 DMA
-//      pieces of slice x + D (group 0 the A image, group 1 the B image), barrier
-//   M: lgkmcnt(0), 8 MFMAs, the tile's epilogue after its last slice, barrier
-// The counted vmcnt(2 (D - 1)) before the barrier that precedes group 0's R
-// phase (group 0: end of M, group 1: end of R) retires slice x + 1 for every
-// wave while D - 1 younger slices stay in flight across the barriers.
-//   ring: NS slots of one K-slice (16 KiB: A 256 rows x 32 B, then B); chunk c
-//         of image row r at slot c ^ ((r >> 3) & 1): the four 16-lane groups of
-//         a fragment read (rows {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31})
-//         hit 16 distinct 16-B slots of the bank row.
-//   DMA:  a piece = 32 image rows x 32 B = one contiguous 1 KiB run of the
-//         16-blocked plane (lane l: row 32 P + l / 2, chunk (l & 1) ^ ((l >> 4) & 1)).
-//   WAR:  slice x + D overwrites the slot of slice x + D - NS, whose last reads
-//         (group 1) retired two barrier intervals earlier: NS >= D + 2.
-// The EPI 1 filter has no barrier of its own (the groups are out of step): each
-// wave appends to its own eighth of the tile's region, region_cnt[8 L + wave].
-// Tile order as k_h1_stream.  DIAG: 1 no epilogue, 3 no DMA.
-// ---------------------------------------------------------------------------
 // s_waitcnt vmcnt(v) (6-bit count: bits 3:0 and 15:14; lgkm / exp untouched)
 constexpr int vmcnt_imm(int v) { return 0x0F70 | (v & 15) | (((v >> 4) & 3) << 14); }
 // s_waitcnt vmcnt(BASE + extra) for a wave-uniform extra in [0, sizeof...(I)); a
@@ -1358,388 +690,43 @@ __device__ __forceinline__ void wait_vm_plus(int extra, std::integer_sequence<in
 }
 
 #define MH_DSR(dst, addr, off) asm volatile("ds_read_b128 %0, %1 offset:" #off : "=v"(dst) : "v"(addr))
-#define MH_LGKM0(f0, f1, f2, f3, f4, f5) \
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3), "+v"(f4), "+v"(f5))
 
-template <int EPI, int DIAG, int NS, int D, int PS, int ER>
-__global__ __launch_bounds__(512) void k_h1_pp(ExactArgs a) {
-    static_assert(NS >= D + 2 && D >= 1, "ring depth");
-    static_assert(PS == 1 || PS == 2, "slice depth 16 or 32");
-    constexpr int RB = 32 * PS;                // image row bytes (16 PS halves of K)
-    constexpr int SL = (G_BM + G_BN) * RB;     // one slice: A then B image
-    constexpr int CPR = 2 * PS, RPP = 32 / PS;  // 16-B chunks per row, rows per 1-KiB piece
-    // EPI 1: per tile (double-buffered by tile parity) the filter constants, by
-    // LDS-DMA: 256 rows x {w0, w1, dead, -} (4 KiB), then c and s of 256 queries
-    constexpr int CST = 6144, CSTB = NS * SL;
-    __shared__ __attribute__((aligned(16))) uint8_t ring[NS * SL + (EPI == 1 ? 2 * CST : 0)];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int wr = wave >> 2, wc = wave & 3;
-    const int g = __builtin_amdgcn_readfirstlane(wr);
-    const int wcs = __builtin_amdgcn_readfirstlane(wc);
-    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
-    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
-    const int64_t nblk = nqt * nnt;
-    const int W = gridDim.x, xcd = blockIdx.x % 8, jx = blockIdx.x / 8;
-    const int wx = W / 8 + (xcd < W % 8 ? 1 : 0);
-    const int64_t per = nblk / 8, rem = nblk % 8;
-    const int64_t lo = xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per;
-    const int64_t hi = lo + per + (xcd < rem ? 1 : 0);
-    const int64_t first = lo + jx;
-    const int64_t ntile = first < hi ? (hi - first + wx - 1) / wx : 0;
-    const int nkt = a.pitch / (X3K * PS);  // K-slices per tile
-    const int64_t S = ntile * nkt;
-    if (S == 0) return;  // uniform over the workgroup
-
-    // DMA: this wave's 2 PS pieces of a slice's A (group 0) or B (group 1) image;
-    // lane l: row RPP P + l / CPR, chunk (l % CPR) ^ swizzle(row) = K-block c / 2, half c % 2
-    const int rr0 = wcs * 2 * PS * RPP + lane / CPR;  // piece i: + RPP i
-    const int64_t ld = g == 0 ? a.ldQs : a.ldXs;
-    const int dc = (lane % CPR) ^ (PS == 1 ? (lane >> 4) & 1 : (lane >> 4) & 3);
-    const uint32_t pk = (uint32_t)((dc >> 1) * ld * 32 + (dc & 1) * 16);
-    const char* const plane = reinterpret_cast<const char*>(g == 0 ? a.Qh : a.Xh);
-    auto sbase = [](const char* p) {
-        const uint64_t u = reinterpret_cast<uint64_t>(p);
-        return reinterpret_cast<const char*>((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u) |
-                                             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32))
-                                              << 32));
-    };
-    int64_t p_tile = 0;
-    int p_kt = 0, p_slot = 0;
-    const char* p_base = nullptr;  // the producer tile's first row in K-block 0
-    int p_lim = 0;                 // its last valid image row (rows past B / N clamp to it)
-    auto p_set = [&]() {
-        const int64_t L = first + p_tile * wx;
-        const int64_t qt = L % nqt, nt = L / nqt;
-        const int64_t r0 = g == 0 ? qt * G_BM : (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
-        p_base = plane + r0 * 32;
-        p_lim = (int)min<int64_t>(255, (g == 0 ? a.B : a.N) - 1 - r0);
-    };
-    auto produce = [&]() {  // this wave's pieces of the producer slice, then advance it
-        if (DIAG < 3) {
-            const char* base = sbase(p_base + (int64_t)p_kt * PS * ld * 32);
-#pragma unroll
-            for (int i = 0; i < 2 * PS; ++i) {
-                const uint32_t off = (uint32_t)min(rr0 + RPP * i, p_lim) * 32 + pk;
-                uint8_t* dst = ring + p_slot * SL + g * (G_BM * RB) + (wcs * 2 * PS + i) * 1024;
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + off),
-                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-            }
-        }
-        if (++p_slot == NS) p_slot = 0;
-        if (++p_kt == nkt) {
-            p_kt = 0;
-            if (++p_tile < ntile) p_set();
-        }
-    };
-
-    f32x16 acc[4][2];
-    const f32x16 zacc = {};  // a tile's first MFMAs accumulate onto zero (no clearing pass)
-    const uint32_t ring_lds = (uint32_t)reinterpret_cast<uintptr_t>(ring);
-    // fragment of k-step j: row lane & 31 of a 32-row block, chunk 2 j + lane / 32
-    const int fsw = PS == 1 ? ((lane & 31) >> 3) & 1 : ((lane & 31) >> 2) & 3;
-    const uint32_t lfix0 = (lane & 31) * RB + (((lane >> 5) ^ fsw) << 4);
-    const uint32_t lfix1 = (lane & 31) * RB + (((2 + (lane >> 5)) ^ fsw) << 4);
-    const uint32_t offA = wr * 128 * RB, offB = G_BM * RB + wc * 64 * RB;
-    const int li = lane & 31, lh = lane >> 5;
-    float keep = 0.f;
-    // vector-memory ops this wave issued since its last counted wait besides the
-    // slice pieces (filter-constant DMA, region stores): with D = 2 they are all
-    // younger than the slice the next wait retires, so that wait adds them to its
-    // count instead of draining them
-    int nst = 0;
-
-    auto epilogue = [&](int64_t L, int64_t ctile) {
-        const int64_t qt = L % nqt, nt = L / nqt;
-        const int64_t q0 = qt * G_BM;
-        const int64_t n0 = (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
-        if constexpr (DIAG == 1) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) keep += acc[i][j][r];
-        } else if constexpr (EPI == 0) {
-            const int64_t col0 = a.nsample_tiles > 0 ? nt * G_BN : n0;  // sample: compact columns
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                const int ro = wc * 64 + nb * 32 + li;
-                const int64_t xr = n0 + ro;
-                if (xr >= a.N) continue;
-                const bool xok = !(a.dead && a.dead[xr]);
-                const float xn = a.xnorm[xr], xi = a.xinv[xr];
-#pragma unroll
-                for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int64_t qr = q0 + wr * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                        if (qr >= a.B) continue;
-                        float sc = split_score(RING_H1, a.metric, acc[mb][nb][r], xi, a.qinv[qr], a.qnorm[qr], xn);
-                        if (!xok) sc = __int_as_float(0x7f800000);
-                        a.scores[(size_t)qr * a.ldS + col0 + ro] = sc;
-                    }
-            }
-        } else {
-            // the fused filter of k_scores_ring (same constants, same test, same
-            // entries).  Constants from LDS (staged by DMA at the tile's first
-            // slice); per 32 x 32 block the 16 tests OR their ballots, and only a
-            // block with a passing pair takes the append path.
-            const uint32_t cb = ring_lds + CSTB + (uint32_t)(ctile & 1) * CST;
-            f32x4 xw[2];
-            asm volatile("ds_read_b128 %0, %1" : "=v"(xw[0]) : "v"(cb + (uint32_t)(wc * 64 + li) * 16));
-            asm volatile("ds_read_b128 %0, %1" : "=v"(xw[1]) : "v"(cb + (uint32_t)(wc * 64 + 32 + li) * 16));
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xw[0]), "+v"(xw[1]));
-            __builtin_amdgcn_sched_barrier(0);
-            bool rok[2];
-            unsigned long long rokm[2], rspm[2];
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                rok[nb] = n0 + wc * 64 + nb * 32 + li < a.N && xw[nb][2] == 0.f;
-                rokm[nb] = __builtin_amdgcn_ballot_w64(rok[nb]);
-                rspm[nb] = __builtin_amdgcn_ballot_w64(!(fabsf(xw[nb][0]) < __builtin_inff()) || xw[nb][0] == 0.f);
-            }
-            // this wave's eighth of the region: cap entries, then one trash slot that
-            // the lanes without an entry store to (every append is one store
-            // instruction with all lanes on: the count of them is exact)
-            const int cap = a.rcap / 8 - 1;
-            uint2* reg = a.region + (L * 8 + wave) * (int64_t)(cap + 1);
-            int cnt = 0;  // wave-uniform
-            // the entry keys below are loop-invariant: laundering the lane id keeps
-            // the compiler from hoisting all 128 of them out of the stream (spills)
-            int lid = lane;
-            asm volatile("" : "+v"(lid));
-            const int eli = lid & 31, elh = lid >> 5;
-            auto filt = [&](auto cos_tag) {
-                constexpr bool COS = decltype(cos_tag)::value;
-                auto test = [&](int mb, int nb, int r, const f32x4* c4, const f32x4* s4) {
-                    const float v = acc[mb][nb][r];
-                    const float cq = c4[r >> 2][r & 3];
-                    float t;
-                    if constexpr (COS)
-                        t = fmaf(-cq, xw[nb][0], v);
-                    else
-                        t = v - fmaf(cq, xw[nb][0], xw[nb][1] * s4[r >> 2][r & 3]);
-                    return !(t < 0.f);
-                };
-#pragma unroll
-                for (int mb = 0; mb < 4; ++mb) {
-                    __builtin_amdgcn_sched_barrier(0);  // one block's constants live at a time
-                    // queries wr 128 + mb 32 + 8 r4 + 4 lh + 0..3 (accumulator rows r = 4 r4 + 0..3)
-                    f32x4 c4[4], s4[4];
-                    const uint32_t qa = cb + 4096 + (uint32_t)(wr * 128 + mb * 32 + 4 * lh) * 4;
-                    asm volatile("ds_read_b128 %0, %1" : "=v"(c4[0]) : "v"(qa));
-                    asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(c4[1]) : "v"(qa));
-                    asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(c4[2]) : "v"(qa));
-                    asm volatile("ds_read_b128 %0, %1 offset:96" : "=v"(c4[3]) : "v"(qa));
-                    if constexpr (!COS) {
-                        asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(s4[0]) : "v"(qa));
-                        asm volatile("ds_read_b128 %0, %1 offset:1056" : "=v"(s4[1]) : "v"(qa));
-                        asm volatile("ds_read_b128 %0, %1 offset:1088" : "=v"(s4[2]) : "v"(qa));
-                        asm volatile("ds_read_b128 %0, %1 offset:1120" : "=v"(s4[3]) : "v"(qa));
-                        asm volatile("s_waitcnt lgkmcnt(0)"
-                                     : "+v"(c4[0]), "+v"(c4[1]), "+v"(c4[2]), "+v"(c4[3]), "+v"(s4[0]), "+v"(s4[1]),
-                                       "+v"(s4[2]), "+v"(s4[3]));
-                    } else {
-                        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c4[0]), "+v"(c4[1]), "+v"(c4[2]), "+v"(c4[3]));
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int nb = 0; nb < 2; ++nb) {
-                        unsigned long long any = 0;
-                        if constexpr ((ER & 1) && COS) {
-                            // one ballot per block: the largest test value (a NaN test
-                            // comes only from a row whose w0 is not finite, in rspm)
-                            float mx = -__builtin_inff();
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaf(-c4[r >> 2][r & 3], xw[nb][0], acc[mb][nb][r]));
-                            any = __builtin_amdgcn_ballot_w64(!(mx < 0.f)) | rspm[nb];
-                        } else {
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) any |= __builtin_amdgcn_ballot_w64(test(mb, nb, r, c4, s4));
-                        }
-                        if (DIAG == 4) keep += (float)(any & rokm[nb]);  // diagnostic: the tests without the appends
-                        if (DIAG != 4 && (any & rokm[nb])) {
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) {
-                                const bool pass = test(mb, nb, r, c4, s4) && rok[nb];
-                                const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
-                                if (m) {
-                                    const int e = cnt + (int)__builtin_amdgcn_mbcnt_hi(
-                                                            (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                                    const int qo = wr * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * elh;
-                                    const int ro = wc * 64 + nb * 32 + eli;
-                                    if (pass)  // (m != 0: the store runs for >= 1 lane, so nst counts it exactly)
-                                        reg[e < cap ? e : cap] = make_uint2((uint32_t)ro | ((uint32_t)qo << 16),
-                                                                                __float_as_uint(acc[mb][nb][r]));
-                                    ++nst;
-                                    cnt += __popcll(m);
-                                }
-                            }
-                        }
-                    }
-                }
-            };
-            if (a.metric == COSINE)
-                filt(std::true_type{});
-            else
-                filt(std::false_type{});
-            if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;
-            ++nst;
-            if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;
-        }
-    };
-
-    constexpr int VMC = vmcnt_imm(2 * PS * (D - 1));  // D - 1 slices (2 PS pieces each) stay in flight
-    static_assert(2 * PS * (D - 1) < 64, "vmcnt range");
-    constexpr int VMCNT0 = 0x0F70;
-    auto wait_vmc = [&]() {  // the counted wait: D - 1 slices (+ the extra ops, D = 2) stay in flight
-        if (D == 2 && nst > 0)
-            wait_vm_plus<2 * PS * (D - 1)>(nst, std::make_integer_sequence<int, 40>{});
-        else
-            __builtin_amdgcn_s_waitcnt(VMC);
-    };
-    // prologue: slices 0 .. D-1 (each wave its pieces), slice 0 landed everywhere
-    p_set();
-    int64_t ps = 0;
-    for (; ps < D && ps < S; ++ps) produce();
-    if (D <= S)
-        __builtin_amdgcn_s_waitcnt(VMC);
-    else
-        __builtin_amdgcn_s_waitcnt(VMCNT0);
-    __builtin_amdgcn_s_barrier();
-    if (g == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
-
-    int64_t c_tile = 0;
-    int c_kt = 0, c_slot = 0;
-    for (int64_t x = 0;; ++x) {
-        // R: fragments of slice x, DMA of slice x + D
-        if ((ER & 2) && c_kt == 0 && c_tile > 0) {  // the previous tile's epilogue, beside the partner's MFMAs
-            epilogue(first + (c_tile - 1) * wx, c_tile - 1);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (x == S) break;  // (after the last tile's epilogue: one call site keeps its loops unrolled)
-        const uint32_t sb = ring_lds + (uint32_t)c_slot * SL;
-        if (++c_slot == NS) c_slot = 0;
-        f16x8 fa[PS][4], fb[PS][2];
-        {
-            const uint32_t va = sb + offA + lfix0, vb = sb + offB + lfix0;
-            if constexpr (PS == 1) {
-                MH_DSR(fa[0][0], va, 0);
-                MH_DSR(fa[0][1], va, 1024);
-                MH_DSR(fa[0][2], va, 2048);
-                MH_DSR(fa[0][3], va, 3072);
-                MH_DSR(fb[0][0], vb, 0);
-                MH_DSR(fb[0][1], vb, 1024);
-            } else {
-                const uint32_t va1 = sb + offA + lfix1, vb1 = sb + offB + lfix1;
-                MH_DSR(fa[0][0], va, 0);
-                MH_DSR(fa[0][1], va, 2048);
-                MH_DSR(fa[0][2], va, 4096);
-                MH_DSR(fa[0][3], va, 6144);
-                MH_DSR(fb[0][0], vb, 0);
-                MH_DSR(fb[0][1], vb, 2048);
-                MH_DSR(fa[PS - 1][0], va1, 0);
-                MH_DSR(fa[PS - 1][1], va1, 2048);
-                MH_DSR(fa[PS - 1][2], va1, 4096);
-                MH_DSR(fa[PS - 1][3], va1, 6144);
-                MH_DSR(fb[PS - 1][0], vb1, 0);
-                MH_DSR(fb[PS - 1][1], vb1, 2048);
-            }
-        }
-        if (EPI == 1 && DIAG < 3 && c_kt == 0) {
-            // the filter constants of this tile (read by its epilogue, nkt - 1 >= D
-            // slices later: retired by the counted waits in between)
-            const int64_t L = first + c_tile * wx;
-            const int64_t q0 = (L % nqt) * G_BM, n0 = (L / nqt) * G_BN;
-            uint8_t* cd = ring + CSTB + (int)(c_tile & 1) * CST;
-            const float* src;
-            uint8_t* dst;
-            if (g == 0) {
-                src = (wcs & 1 ? a.ring_s : a.ring_c) + q0 + lane * 4;
-                dst = cd + 4096 + (wcs & 1) * 1024;
-            } else {
-                src = reinterpret_cast<const float*>(a.xw + min<int64_t>(n0 + wcs * 64 + lane, a.N - 1));
-                dst = cd + wcs * 1024;
-            }
-            if (g == 1 || wcs < 2) {
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
-                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-                ++nst;
-            }
-        }
-        if (ps < S) {
-            produce();
-            ++ps;
-        }
-        const bool tail = x + 1 + D > S;  // fewer than D slices left in flight: retire them all
-        if (g == 1) {
-            if (tail)
-                __builtin_amdgcn_s_waitcnt(VMCNT0);
-            else
-                wait_vmc();
-            nst = 0;
-        }
-        __builtin_amdgcn_s_barrier();
-        // M: 8 PS MFMAs (+ the epilogue after a tile's last slice)
-#pragma unroll
-        for (int j = 0; j < PS; ++j) MH_LGKM0(fa[j][0], fa[j][1], fa[j][2], fa[j][3], fb[j][0], fb[j][1]);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-        if (c_kt == 0) {
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-#pragma unroll
-                for (int n = 0; n < 2; ++n)
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0][m], fb[0][n], zacc, 0, 0, 0);
-        } else {
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-#pragma unroll
-                for (int n = 0; n < 2; ++n)
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0][m], fb[0][n], acc[m][n], 0, 0, 0);
-        }
-#pragma unroll
-        for (int j = 1; j < PS; ++j)
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-#pragma unroll
-                for (int n = 0; n < 2; ++n)
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[j][m], fb[j][n], acc[m][n], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (++c_kt == nkt) {
-            if (!(ER & 2)) epilogue(first + c_tile * wx, c_tile);  // (ER & 2: in the next R phase)
-            c_kt = 0;
-            ++c_tile;
-        }
-        if (g == 0) {
-            if (tail)
-                __builtin_amdgcn_s_waitcnt(VMCNT0);
-            else
-                wait_vmc();
-            nst = 0;
-        }
-        __builtin_amdgcn_s_barrier();
-    }
-    if (g == 0) __builtin_amdgcn_s_barrier();  // evens the barrier count
-    __builtin_amdgcn_s_waitcnt(VMCNT0);
-    if constexpr (DIAG == 1 || DIAG == 4) {
-        if (lane == 0 && keep == -1.0e38f) a.region_cnt[0] = 1;
-    }
-}
 // ---------------------------------------------------------------------------
-// k_h1_pp16: k_h1_pp (PS 2, NS 4, D 2) on v_mfma_f32_16x16x32_f16 -- the same ring,
-// DMA image and ping-pong; each wave's 128 x 64 tile is 8 x 4 blocks of 16 x 16,
-// 32 MFMAs per 32-deep slice from 8 A + 4 B fragment reads (the 16 x 16 shape
-// holds a higher clock than 32 x 32 on random operands: MI355X_MICROARCH.md DVFS (7)).
-// The fused filter tests a block's largest value first (one ballot per 16 queries).
+// k_h1_pp16: the fp16 1-product scores (exact_precision 3) as a persistent,
+// two-group ping-pong stream of 256 x 256 tiles (queries x rows) on
+// v_mfma_f32_16x16x32_f16.  Waves 0-3 (group 0, query rows 0-127) and 4-7
+// (group 1, rows 128-255) hold one wave on every SIMD; group 1 runs one
+// barrier behind group 0, so in every barrier interval one wave of a SIMD
+// multiplies (32 MFMAs, s_setprio 1) while the other reads its next fragments
+// and issues its share of the LDS-DMA, and the roles swap at the barrier.  Per
+// wave (a 128 x 64 tile: 8 x 4 blocks of 16 x 16) and 32-deep K-slice:
+//   R: 12 ds_read_b128 (8 A, 4 B fragments) from the slice's ring slot, the
+//      wave's 4 DMA pieces of slice x + D (group 0 the A image, group 1 the B
+//      image), barrier
+//   M: lgkmcnt(0), 32 MFMAs, the tile's epilogue after its last slice, barrier
+// The counted vmcnt(4 (D - 1)) before the barrier that precedes group 0's R
+// phase (group 0: end of M, group 1: end of R) retires slice x + 1 for every
+// wave while D - 1 younger slices stay in flight across the barriers.
+//   ring: NS = 4 slots of one K-slice (32 KiB: A 256 rows x 64 B, then B);
+//         16-B chunk c of image row r at slot c ^ ((r >> 2) & 3): the four
+//         16-lane groups of a fragment read hit 16 distinct 16-B slots.
+//   DMA:  a piece = 16 image rows x 64 B = one contiguous 1 KiB run of the
+//         16-blocked plane (lane l: row 16 P + l / 4, chunk (l & 3) ^ swizzle).
+//   WAR:  slice x + D overwrites the slot of slice x + D - NS, whose last reads
+//         (group 1) retired two barrier intervals earlier: NS >= D + 2.
+// Tile order: each XCD walks a contiguous run of logical tiles, query tiles
+// fastest, so a row tile enters that XCD's L2 once (blockIdx.x % 8 = XCD).
+// EPI 0 writes every score of the (sampled) row tiles; EPI 1 is the fused
+// filter (records, below): the per-tile filter constants arrive by LDS-DMA at
+// the tile's first slice, double-buffered by tile parity.
+// DIAG (timing diagnostics, tools build only -- MH_EXACT_DIAG): 1 no epilogue,
+// 4 the filter's tests without the record stores (no pair passes: every query
+// takes the canonical fallback, results stay exact).
 // ---------------------------------------------------------------------------
-template <int EPI, int DIAG, int REC = 0>
+template <int EPI, int DIAG = 0>
 __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     constexpr int NS = 4, D = 2, PS = 2;
     static_assert(NS >= D + 2 && D >= 1, "ring depth");
-    static_assert(PS == 1 || PS == 2, "slice depth 16 or 32");
     constexpr int RB = 32 * PS;                // image row bytes (16 PS halves of K)
     constexpr int SL = (G_BM + G_BN) * RB;     // one slice: A then B image
     constexpr int CPR = 2 * PS, RPP = 32 / PS;  // 16-B chunks per row, rows per 1-KiB piece
@@ -1747,21 +734,6 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     // LDS-DMA: 256 rows x {w0, w1, dead, -} (4 KiB), then c and s of 256 queries
     constexpr int CST = 6144, CSTB = NS * SL;
     __shared__ __attribute__((aligned(16))) uint8_t ring[NS * SL + (EPI == 1 ? 2 * CST : 0)];
-    // REC 3: per wave an LDS buffer of H1_LRC records (80 B each), written out in
-    // coalesced 16-B chunks (the ring and constants leave exactly 20 KiB of the 160)
-    constexpr int H1_LRC = 32;
-    __shared__ __attribute__((aligned(16))) uint8_t lrec[REC == 3 && EPI == 1 ? 8 * H1_LRC * 80 : 16];
-    // REC 5 (split roles): group 0 issues every LDS-DMA piece and never a global
-    // store on the fast path; its records go to an LDS buffer that its group-1
-    // partner (same wc) writes out, and group 1, which then waits on no DMA,
-    // stores its own records directly.  vmcnt retires in issue order
-    // (MI355X_MICROARCH.md), so a store issued by a wave that later waits for its
-    // own DMA stalls that wait until the store is acknowledged (~3k cycles under
-    // load); here no waiting wave has a store in flight.  SPC records per group-0
-    // wave (the ring and constants leave 20 KiB); more spill to direct stores.
-    constexpr bool SPL = REC == 5;
-    constexpr int SPC = 63;
-    __shared__ __attribute__((aligned(16))) uint8_t srec[SPL && EPI == 1 ? 4 * SPC * 80 + 16 : 16];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 2, wc = wave & 3;
@@ -1798,52 +770,21 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     int p_kt = 0, p_slot = 0;
     const char* p_base = nullptr;  // the producer tile's first row in K-block 0
     int p_lim = 0;                 // its last valid image row (rows past B / N clamp to it)
-    // SPL: group 0 loads both images (its wave wcs the pieces group 1's wave wcs
-    // loads otherwise); the B image's base and limit
-    const int64_t ldB = a.ldXs;
-    const uint32_t pkB = (uint32_t)((dc >> 1) * ldB * 32 + (dc & 1) * 16);
-    const char* const planeB = reinterpret_cast<const char*>(a.Xh);
-    const char* pB_base = nullptr;
-    int pB_lim = 0;
     auto p_set = [&]() {
         const int64_t L = first + p_tile * wx;
         const int64_t qt = L % nqt, nt = L / nqt;
         const int64_t r0 = g == 0 ? qt * G_BM : (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
         p_base = plane + r0 * 32;
         p_lim = (int)min<int64_t>(255, (g == 0 ? a.B : a.N) - 1 - r0);
-        if constexpr (SPL) {
-            const int64_t rB = (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
-            pB_base = planeB + rB * 32;
-            pB_lim = (int)min<int64_t>(255, a.N - 1 - rB);
-        }
     };
     auto produce = [&]() {  // this wave's pieces of the producer slice, then advance it
-        if (SPL && DIAG < 3 && g == 0) {
-            const char* base = sbase(p_base + (int64_t)p_kt * PS * ld * 32);
-            const char* baseB = sbase(pB_base + (int64_t)p_kt * PS * ldB * 32);
+        const char* base = sbase(p_base + (int64_t)p_kt * PS * ld * 32);
 #pragma unroll
-            for (int i = 0; i < 2 * PS; ++i) {
-                const uint32_t off = (uint32_t)min(rr0 + RPP * i, p_lim) * 32 + pk;
-                uint8_t* dst = ring + p_slot * SL + (wcs * 2 * PS + i) * 1024;
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + off),
-                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-            }
-#pragma unroll
-            for (int i = 0; i < 2 * PS; ++i) {
-                const uint32_t off = (uint32_t)min(rr0 + RPP * i, pB_lim) * 32 + pkB;
-                uint8_t* dst = ring + p_slot * SL + G_BM * RB + (wcs * 2 * PS + i) * 1024;
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(baseB + off),
-                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-            }
-        } else if (!SPL && DIAG < 3) {
-            const char* base = sbase(p_base + (int64_t)p_kt * PS * ld * 32);
-#pragma unroll
-            for (int i = 0; i < 2 * PS; ++i) {
-                const uint32_t off = (uint32_t)min(rr0 + RPP * i, p_lim) * 32 + pk;
-                uint8_t* dst = ring + p_slot * SL + g * (G_BM * RB) + (wcs * 2 * PS + i) * 1024;
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + off),
-                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-            }
+        for (int i = 0; i < 2 * PS; ++i) {
+            const uint32_t off = (uint32_t)min(rr0 + RPP * i, p_lim) * 32 + pk;
+            uint8_t* dst = ring + p_slot * SL + g * (G_BM * RB) + (wcs * 2 * PS + i) * 1024;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + off),
+                                             (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
         }
         if (++p_slot == NS) p_slot = 0;
         if (++p_kt == nkt) {
@@ -1861,15 +802,17 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     const uint32_t lfix = (lane & 15) * RB + ((((lane >> 4) ^ ((lane >> 2) & 3)) & 3) << 4);
     const uint32_t offA = wr * 128 * RB, offB = G_BM * RB + wc * 64 * RB;
     const int fr = lane & 15, fq = lane >> 4;  // accumulator: column (row) fr, queries 4 fq + j
-    float keep = 0.f;
-    int nst = 0;  // vector-memory ops besides the slice pieces since the last counted wait (as k_h1_pp)
+    float keep = 0.f;  // DIAG: keeps the MFMAs / tests live
+    int nst = 0;  // vector-memory ops besides the slice pieces since the last counted wait
 
-    // REC 4: the epilogue only tests; per lane a mask of the block rows with a
-    // passing pair (hm), and the tile's record stores are issued in the next R phase
-    // (while the partner group multiplies; acc holds the tile until the next M phase)
-    uint32_t hm = 0;
-    int pend = 0;  // wave-uniform: a tested tile's records are pending
-    int64_t pend_L = 0;
+    // The fused filter, in records: per lane four rows (nb) and, per 16-query
+    // block row mb, four queries; a pair passes unless acc - c_q w_x < 0 (cosine;
+    // L2 acc - (c_q w0_x + w1_x s_q) < 0), every constant from the tile's LDS copy.
+    // A lane with a passing pair in block row mb stores that row's 16 accumulators
+    // as one record ({mb | lane << 8, 0}, pad, 4 x float4 = H1_REC uint2) in its
+    // wave's eighth of the tile's region; k_bucket_rec re-applies the identical
+    // test to each.  A block's largest value is tested first (one ballot per 16
+    // queries).
     auto epilogue = [&](int64_t L, int64_t ctile) {
         const int64_t qt = L % nqt, nt = L / nqt;
         const int64_t q0 = qt * G_BM;
@@ -1902,8 +845,6 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                     }
             }
         } else {
-            // the fused filter of k_h1_pp on the 16 x 16 accumulator layout: per lane
-            // four rows (nb) and, per block, four queries; constants from LDS
             const uint32_t cb = ring_lds + CSTB + (uint32_t)(ctile & 1) * CST;
             f32x4 xw[4];
 #pragma unroll
@@ -1918,31 +859,11 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                 // a row whose w0 is not finite (or 0) always takes the exact per-pair tests
                 rsp[nb] = rok[nb] && (!(fabsf(xw[nb][0]) < __builtin_inff()) || xw[nb][0] == 0.f);
             }
-            const int cap = a.rcap / 8 - 1;
-            uint2* reg = a.region + (L * 8 + wave) * (int64_t)(cap + 1);
             int cnt = 0;  // wave-uniform
-            uint32_t bx = 0, by = 0;  // buffered entries of the current chunk (lane j: entry 64 (cnt / 64) + j)
-            const int rcw = a.rcap / (8 * H1_REC);  // REC: records per wave region
+            const int rcw = a.rcap / (8 * H1_REC);  // records per wave region
             uint2* regr = a.region + (L * 8 + wave) * (int64_t)(rcw * H1_REC);
             int lid = lane;
             asm volatile("" : "+v"(lid));
-            const int efr = lid & 15, efq = lid >> 4;
-            int lcnt = 0;  // REC 3: records buffered in LDS (wave-uniform; they are cnt - lcnt ..)
-            // the buffered records to their slots, 64 chunks per store; returns the
-            // store instructions issued (values in: no captured counters)
-            auto flush_rec = [lid, wave, rcw, regr](int base, int n) -> int {
-                const int nch = n * 5;
-                const uint4* src = reinterpret_cast<const uint4*>(lrec + wave * H1_LRC * 80);
-                int st = 0;
-                for (int c0 = 0; c0 < nch; c0 += 64, ++st) {
-                    const int c = c0 + lid;
-                    if (c < nch) {
-                        const int i = c / 5, j = c - 5 * i;
-                        reinterpret_cast<uint4*>(regr + (int64_t)min(base + i, rcw - 1) * H1_REC)[j] = src[c];
-                    }
-                }
-                return st;
-            };
             auto filt = [&](auto cos_tag) {
                 constexpr bool COS = decltype(cos_tag)::value;
                 auto tval = [&](int mb, int nb, int r, const f32x4& c4, const f32x4& s4) {
@@ -1974,154 +895,24 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, tval(mb, nb, r, c4, s4));
                         hit |= (rok[nb] && !(mx < 0.f)) || rsp[nb];
                     }
-                    if (DIAG == 4) keep += (float)__builtin_amdgcn_ballot_w64(hit);
-                    if constexpr (REC == 4) {
-                        hm |= hit ? 1u << mb : 0u;
-                    } else if constexpr (REC == 3) {
-                        // record mode through the wave's LDS buffer: the block row's
-                        // records are staged at lcnt + rank; a full buffer is written
-                        // out first; a block row larger than the buffer stores directly
+                    if constexpr (DIAG == 4) {
+                        keep += (float)__builtin_amdgcn_ballot_w64(hit);
+                    } else {
                         const unsigned long long m = __builtin_amdgcn_ballot_w64(hit);
                         if (m) {
                             const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                            const int pc = __popcll(m);
-                            if (lcnt + pc > H1_LRC) {
-                                nst += flush_rec(cnt - lcnt, lcnt);
-                                lcnt = 0;
-                            }
-                            if (pc <= H1_LRC) {
-                                if (hit) {
-                                    uint4* d = reinterpret_cast<uint4*>(lrec + (wave * H1_LRC + lcnt + rk) * 80);
-                                    d[0] = make_uint4((uint32_t)mb | ((uint32_t)lid << 8), 0u, 0u, 0u);
-#pragma unroll
-                                    for (int nb = 0; nb < 4; ++nb)
-                                        d[1 + nb] = make_uint4(__float_as_uint(acc[mb][nb][0]), __float_as_uint(acc[mb][nb][1]),
-                                                               __float_as_uint(acc[mb][nb][2]), __float_as_uint(acc[mb][nb][3]));
-                                }
-                                lcnt += pc;
-                            } else {
-                                if (hit) {
-                                    uint2* rec = regr + (int64_t)min(cnt + rk, rcw - 1) * H1_REC;
-                                    rec[0] = make_uint2((uint32_t)mb | ((uint32_t)lid << 8), 0u);
-                                    float4* ra = reinterpret_cast<float4*>(rec + 2);
-#pragma unroll
-                                    for (int nb = 0; nb < 4; ++nb)
-                                        ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
-                                }
-                                nst += 5;
-                            }
-                            cnt += pc;
-                        }
-                    } else if constexpr (REC) {
-                        // record mode: a lane with a passing pair in this block row
-                        // stores its 16 accumulators (k_bucket applies the same tests)
-                        const unsigned long long m = __builtin_amdgcn_ballot_w64(hit);
-                        if (m) {
-                            const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                            if (SPL && g == 0) {
-                                // to the LDS buffer; past it (rare), stored directly
-                                if (hit) {
-                                    const int slot = cnt + rk;
-                                    if (slot < SPC) {
-                                        uint4* d = reinterpret_cast<uint4*>(srec + (wcs * SPC + slot) * 80);
-                                        d[0] = make_uint4((uint32_t)mb | ((uint32_t)lid << 8), 0u, 0u, 0u);
-#pragma unroll
-                                        for (int nb = 0; nb < 4; ++nb)
-                                            d[1 + nb] = make_uint4(__float_as_uint(acc[mb][nb][0]), __float_as_uint(acc[mb][nb][1]),
-                                                                   __float_as_uint(acc[mb][nb][2]), __float_as_uint(acc[mb][nb][3]));
-                                    } else {
-                                        uint2* rec = regr + (int64_t)min(slot, rcw - 1) * H1_REC;
-                                        rec[0] = make_uint2((uint32_t)mb | ((uint32_t)lid << 8), 0u);
-                                        float4* ra = reinterpret_cast<float4*>(rec + 2);
-#pragma unroll
-                                        for (int nb = 0; nb < 4; ++nb)
-                                            ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
-                                    }
-                                }
-                                if (cnt + __popcll(m) > SPC) nst += 5;
-                            } else if (hit) {
+                            if (hit) {
                                 const int slot = min(cnt + rk, rcw - 1);  // past the capacity: the last record (flagged)
                                 uint2* rec = regr + (int64_t)slot * H1_REC;
+                                rec[0] = make_uint2((uint32_t)mb | ((uint32_t)lid << 8), 0u);
                                 float4* ra = reinterpret_cast<float4*>(rec + 2);
-                                if constexpr (REC == 2) {  // non-temporal record stores
-                                    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-                                    const u32x2 hd = {(uint32_t)mb | ((uint32_t)lid << 8), 0u};
-                                    __builtin_nontemporal_store(hd, reinterpret_cast<u32x2*>(rec));
 #pragma unroll
-                                    for (int nb = 0; nb < 4; ++nb)
-                                        __builtin_nontemporal_store(acc[mb][nb], reinterpret_cast<f32x4*>(ra + nb));
-                                } else {
-                                    rec[0] = make_uint2((uint32_t)mb | ((uint32_t)lid << 8), 0u);
-#pragma unroll
-                                    for (int nb = 0; nb < 4; ++nb)
-                                        ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
-                                }
+                                for (int nb = 0; nb < 4; ++nb)
+                                    ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
                             }
-                            if (!SPL) nst += 5;  // (at least 5 store instructions: never an over-count)
+                            nst += 5;  // (at least 5 store instructions: never an over-count)
                             cnt += __popcll(m);
-                        }
-                    } else if (DIAG != 4 && __builtin_amdgcn_ballot_w64(hit)) {
-                        // the passing pairs of this block row, per lane a 16-bit mask
-                        // (bit 4 nb + r); each round appends every lane's lowest
-                        // pair, so the rounds are the largest count of one lane
-                        uint32_t pm = 0;
-#pragma unroll
-                        for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-                            for (int r = 0; r < 4; ++r)
-                                pm |= (!(tval(mb, nb, r, c4, s4) < 0.f) && rok[nb]) ? 1u << (nb * 4 + r) : 0u;
-                        for (;;) {
-                            const bool pass = pm != 0;
-                            const unsigned long long m = __builtin_amdgcn_ballot_w64(pass);
-                            if (!m) break;
-                            const int b = pass ? __builtin_ctz(pm) : 0;
-                            pm &= pm - 1u;
-                            // acc[mb][b >> 2][b & 3] by a select tree (no dynamic register index)
-                            float v4[4];
-#pragma unroll
-                            for (int nb = 0; nb < 4; ++nb) {
-                                const float lo = (b & 1) ? acc[mb][nb][1] : acc[mb][nb][0];
-                                const float hi = (b & 1) ? acc[mb][nb][3] : acc[mb][nb][2];
-                                v4[nb] = (b & 2) ? hi : lo;
-                            }
-                            const float v01 = (b & 4) ? v4[1] : v4[0], v23 = (b & 4) ? v4[3] : v4[2];
-                            const float v = (b & 8) ? v23 : v01;
-                            const int pc = __popcll(m);
-                            const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                            // entry e goes to buffer lane e & 63 (one permutation of all lanes:
-                            // passing lanes to cnt + rank, the others behind them); each full
-                            // chunk of 64 is one coalesced store
-                            const int dst = (pass ? cnt + rk : cnt + pc + (lid - rk)) & 63;
-                            const int qo = wr * 128 + mb * 16 + 4 * efq + (b & 3);
-                            const int ro = wc * 64 + (b >> 2) * 16 + efr;
-                            uint32_t nx, ny;
-                            if constexpr (DIAG == 6) {  // diagnostic: no permutes
-                                nx = (uint32_t)ro | ((uint32_t)qo << 16);
-                                ny = __float_as_uint(v);
-                            } else {
-                                nx = push_to((uint32_t)ro | ((uint32_t)qo << 16), dst);
-                                ny = push_to(__float_as_uint(v), dst);
-                            }
-                            const int c0 = cnt & 63;
-                            const bool fresh = ((lid - c0) & 63) < pc;  // lanes receiving an entry
-                            if (c0 + pc >= 64) {  // chunk cnt / 64 complete: lanes >= c0 new, the rest buffered
-                                const int e = (cnt & ~63) + lid;
-                                const uint32_t sx = lid >= c0 ? nx : bx, sy = lid >= c0 ? ny : by;
-                                if constexpr (DIAG == 5) {  // diagnostic: no stores
-                                    keep += __uint_as_float(sx ^ sy);
-                                } else {
-                                    reg[e < cap ? e : cap] = make_uint2(sx, sy);  // (past cap: the trash slot; every lane stores, so nst is exact)
-                                    ++nst;
-                                }
-                            }
-                            if (fresh) {
-                                bx = nx;
-                                by = ny;
-                            }
-                            cnt += pc;
                         }
                     }
                 }
@@ -2130,83 +921,16 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                 filt(std::true_type{});
             else
                 filt(std::false_type{});
-            if constexpr (REC == 3) {
-                if (lcnt) nst += flush_rec(cnt - lcnt, lcnt);
-            }
-            if (!REC && (cnt & 63)) {  // the partial last chunk
-                const int e = (cnt & ~63) + lane;
-                if constexpr (DIAG == 5) {
-                    keep += __uint_as_float(bx ^ by);
-                } else {
-                    if (lane < (cnt & 63)) reg[e < cap ? e : cap] = make_uint2(bx, by);  // (lane 0 always stores)
-                    ++nst;
-                }
-            }
-            if constexpr (REC == 4) {
-                pend = 1;
-                pend_L = L;
-            } else if constexpr (SPL) {
-                uint8_t* const cnts = srec + 4 * SPC * 80;
-                if (g == 0) {
-                    // the count beside the records; both visible to group 1 after the barrier
-                    if (lane == 0) *reinterpret_cast<int*>(cnts + wcs * 4) = cnt;
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                } else {
-                    if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;
-                    // the partner's records (group 0, wave wcs) of this tile, 64 chunks per store
-                    const int pc = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(cnts + wcs * 4));
-                    const int nch = min(pc, SPC) * 5;
-                    const uint4* src = reinterpret_cast<const uint4*>(srec + wcs * SPC * 80);
-                    uint2* regp = a.region + (L * 8 + wcs) * (int64_t)(rcw * H1_REC);
-                    for (int c0 = 0; c0 < nch; c0 += 64) {
-                        const int c = c0 + lid;
-                        if (c < nch) {
-                            const int i = c / 5, j = c - 5 * i;
-                            reinterpret_cast<uint4*>(regp + (int64_t)i * H1_REC)[j] = src[c];
-                        }
-                    }
-                    if (lane == 0) a.region_cnt[L * 8 + wcs] = pc;
-                }
-            } else {
-                if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;
-                ++nst;
-            }
+            if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;  // (DIAG 4: 0)
+            ++nst;
         }
-    };
-    auto store_pending = [&]() {  // REC 4: the pending tile's records (as REC 1 stores them)
-        const int rcw = a.rcap / (8 * H1_REC);
-        uint2* regr = a.region + (pend_L * 8 + wave) * (int64_t)(rcw * H1_REC);
-        int cnt = 0;
-#pragma unroll
-        for (int mb = 0; mb < 8; ++mb) {
-            const bool hit = (hm >> mb) & 1u;
-            const unsigned long long m = __builtin_amdgcn_ballot_w64(hit);
-            if (m) {
-                const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                if (hit) {
-                    uint2* rec = regr + (int64_t)min(cnt + rk, rcw - 1) * H1_REC;
-                    rec[0] = make_uint2((uint32_t)mb | ((uint32_t)lane << 8), 0u);
-                    float4* ra = reinterpret_cast<float4*>(rec + 2);
-#pragma unroll
-                    for (int nb = 0; nb < 4; ++nb)
-                        ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
-                }
-                nst += 5;
-                cnt += __popcll(m);
-            }
-        }
-        if (lane == 0) a.region_cnt[pend_L * 8 + wave] = cnt;
-        ++nst;
-        hm = 0;
-        pend = 0;
     };
 
-    constexpr int PIECES = (SPL ? 2 : 1) * 2 * PS;  // DMA pieces per slice of a loading wave
-    constexpr int VMC = vmcnt_imm(PIECES * (D - 1));
+    constexpr int VMC = vmcnt_imm(2 * PS * (D - 1));
     constexpr int VMCNT0 = 0x0F70;
     auto wait_vmc = [&]() {
         if (nst > 0)
-            wait_vm_plus<PIECES * (D - 1)>(nst, std::make_integer_sequence<int, 52>{});  // (vmcnt <= 63)
+            wait_vm_plus<2 * PS * (D - 1)>(nst, std::make_integer_sequence<int, 59>{});  // (vmcnt <= 63)
         else
             __builtin_amdgcn_s_waitcnt(VMC);
     };
@@ -2257,19 +981,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                 src = reinterpret_cast<const float*>(a.xw + min<int64_t>(n0 + wcs * 64 + lane, a.N - 1));
                 dst = cd + wcs * 1024;
             }
-            if (SPL) {  // group 0 loads the row constants too
-                if (g == 0) {
-                    if (wcs < 2) {
-                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
-                                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-                        ++nst;
-                    }
-                    const float* srcx = reinterpret_cast<const float*>(a.xw + min<int64_t>(n0 + wcs * 64 + lane, a.N - 1));
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(srcx),
-                                                     (__attribute__((address_space(3))) void*)(cd + wcs * 1024), 16, 0, 0);
-                    ++nst;
-                }
-            } else if (g == 1 || wcs < 2) {
+            if (g == 1 || wcs < 2) {
                 __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
                                                  (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
                 ++nst;
@@ -2279,11 +991,8 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
             produce();
             ++ps;
         }
-        if constexpr (EPI == 1 && REC == 4) {
-            if (pend) store_pending();
-        }
         const bool tail = x + 1 + D > S;  // fewer than D slices left in flight: retire them all
-        if (g == 1 && !SPL) {  // (SPL: group 1 loads nothing)
+        if (g == 1) {
             if (tail)
                 __builtin_amdgcn_s_waitcnt(VMCNT0);
             else
@@ -2325,17 +1034,14 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
         }
         __builtin_amdgcn_s_barrier();
     }
-    if constexpr (EPI == 1 && REC == 4) {
-        if (pend) store_pending();  // the last tile's records
-    }
     if (g == 0) __builtin_amdgcn_s_barrier();  // evens the barrier count
     __builtin_amdgcn_s_waitcnt(VMCNT0);
-    if constexpr (DIAG == 1 || DIAG >= 4) {
+    if constexpr (DIAG > 0) {
         if (lane == 0 && keep == -1.0e38f) a.region_cnt[0] = 1;
     }
 }
 
-template <int EPI, int DIAG = 0, int REC = 0>
+template <int EPI, int DIAG = 0>
 static int launch_h1_pp16_t(const ExactArgs& a, hipStream_t s) {
     if (a.pitch % (X3K * 2)) return -5;
     if (std::max(a.ldQs, a.ldXs) * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return -5;  // 32-bit DMA offsets
@@ -2343,91 +1049,45 @@ static int launch_h1_pp16_t(const ExactArgs& a, hipStream_t s) {
     const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
     const int64_t nblk = nqt * nnt;
     const int64_t W = std::min<int64_t>(nblk, std::max(8, device_cus() / 8 * 8));
-    hipLaunchKernelGGL((k_h1_pp16<EPI, DIAG, REC>), dim3((unsigned)W), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((k_h1_pp16<EPI, DIAG>), dim3((unsigned)W), dim3(512), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 #undef MH_DSR
-#undef MH_LGKM0
-
-template <int EPI, int DIAG = 0, int NS = 8, int D = 6, int PS = 1, int ER = 0>
-static int launch_h1_pp_t(const ExactArgs& a, hipStream_t s) {
-    if (a.pitch % (X3K * PS)) return -5;
-    if ((PS - 1) * std::max(a.ldQs, a.ldXs) * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return -5;  // 32-bit DMA offsets
-    const int64_t nqt = (a.B + G_BM - 1) / G_BM;
-    const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
-    const int64_t nblk = nqt * nnt;
-    const int64_t W = std::min<int64_t>(nblk, std::max(8, device_cus() / 8 * 8));
-    hipLaunchKernelGGL((k_h1_pp<EPI, DIAG, NS, D, PS, ER>), dim3((unsigned)W), dim3(512), 0, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
 
 // ---------------------------------------------------------------------------
 // fp16 1-product path with the fused preselection (exact_precision 3)
 // ---------------------------------------------------------------------------
-// ring variants (exact_tile for precision 3; 0 = 5): 1 = 256 x 256, 32-deep stages,
-// 4 buffers; 2 = 256 x 256, 64-deep stages, 2 buffers; 3 = 256 x 256, 16-deep
-// stages, 4 buffers; 4 = 128 x 256, 32-deep, 4 buffers; 5 = 128 x 256, 32-deep, 3 buffers
-// (two workgroups per CU); 6 = 128 x 256 on 4 waves of 128 x 64, 32-deep, 3 buffers
+// exact_tile for precision 3: 0 / 34 = k_h1_pp16 (the default); 5 = the ring
+// kernel's fused filter (k_scores_ring, 128 x 256 tiles, 32-deep stages, 3
+// buffers, two workgroups per CU), which also runs every shape k_h1_pp16 does
+// not admit (fewer than 3 K-slices per tile, DMA offsets past 32 bits).  The
+// tools build (MH_EXACT_DIAG) adds 30 / 31: k_h1_pp16 with no epilogue / the
+// filter's tests without the record stores.
 template <int EPI>
 static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
     if (a.B <= 0 || a.N <= 0) return 0;
-    if (variant == 0) variant = 34;
     switch (variant) {
-        case 10: return launch_h1_gemm_t<EPI>(a, s);
-        case 11: return launch_h1_gemm_t<EPI, EPI ? 1 : 0>(a, s);
-        case 12: return launch_h1_gemm_t<EPI, EPI ? 2 : 0>(a, s);
-        case 13: return launch_h1_gemm_t<EPI, EPI ? 3 : 0>(a, s);
-        case 14: return launch_h1_stream_t<EPI>(a, s);
-        case 15: return launch_h1_stream_t<EPI, EPI ? 1 : 0>(a, s);
-        case 16: return launch_h1_stream_t<EPI, EPI ? 2 : 0>(a, s);
-        case 17: return launch_h1_stream_t<EPI, EPI ? 3 : 0>(a, s);
-        case 18: return launch_h1_pp_t<EPI>(a, s);
-        case 19: return launch_h1_pp_t<EPI, EPI ? 1 : 0>(a, s);
-        case 20: return launch_h1_pp_t<EPI, EPI ? 3 : 0>(a, s);
-        case 21: return launch_h1_pp_t<EPI, 0, 8, 4>(a, s);
-        case 22: return launch_h1_pp_t<EPI, 0, 9, 7>(a, s);
-        case 23: return launch_h1_pp_t<EPI, 0, 4, 2, 2>(a, s);
-        case 24: return launch_h1_pp_t<EPI, EPI ? 1 : 0, 4, 2, 2>(a, s);
-        case 25: return launch_h1_pp_t<EPI, EPI ? 3 : 0, 4, 2, 2>(a, s);
-        case 26: return launch_h1_pp_t<EPI, EPI ? 4 : 0, 4, 2, 2>(a, s);
-        case 27: return launch_h1_pp_t<EPI, 0, 4, 2, 2, 3>(a, s);
-        case 28: return launch_h1_pp_t<EPI, 0, 4, 2, 2, 1>(a, s);
-        case 29: return launch_h1_pp16_t<EPI>(a, s);
+        case 5: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 3, EPI>(a, s);
+#ifdef MH_EXACT_DIAG
         case 30: return launch_h1_pp16_t<EPI, EPI ? 1 : 0>(a, s);
         case 31: return launch_h1_pp16_t<EPI, EPI ? 4 : 0>(a, s);
-        case 32: return launch_h1_pp16_t<EPI, EPI ? 5 : 0>(a, s);
-        case 33: return launch_h1_pp16_t<EPI, EPI ? 6 : 0>(a, s);
-        case 34: return launch_h1_pp16_t<EPI, 0, EPI>(a, s);
-        case 35: return launch_h1_pp16_t<EPI, 0, EPI ? 2 : 0>(a, s);
-        case 36: return launch_h1_pp16_t<EPI, 0, EPI ? 3 : 0>(a, s);
-        case 37: return launch_h1_pp16_t<EPI, 0, EPI ? 4 : 0>(a, s);
-        case 38: return launch_h1_pp16_t<EPI, 0, EPI ? 5 : 0>(a, s);
-        case 2: return launch_ring_t<2, 4, 4, 2, RING_H1, 4, 2, EPI>(a, s);
-        case 3: return launch_ring_t<2, 4, 4, 2, RING_H1, 1, 4, EPI>(a, s);
-        case 4: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 4, EPI>(a, s);
-        case 5: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 3, EPI>(a, s);
-        case 6: return launch_ring_t<1, 4, 4, 2, RING_H1, 2, 3, EPI>(a, s);
-        case 7: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 3, EPI, EPI ? 1 : 0>(a, s);
-        case 8: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 3, EPI, EPI ? 2 : 0>(a, s);
-        case 9: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 3, EPI, EPI ? 3 : 0>(a, s);
-        default: return launch_ring_t<2, 4, 4, 2, RING_H1, 2, 4, EPI>(a, s);
+#endif
+        default: return launch_h1_pp16_t<EPI>(a, s);
     }
 }
-int h1_tile_bm(int variant) { return variant >= 4 && variant <= 9 ? 128 : 256; }
-// The variant a search runs: 0 = the default (23); the k_h1_pp family needs K-slices
-// of its depth, at least D + 1 of them per tile (the filter constants staged at a
-// tile's first slice must have landed by its epilogue), and 32-bit DMA offsets --
-// otherwise k_h1_gemm (10).
+int h1_tile_bm(int variant) { return variant == 5 ? 128 : 256; }
+// The variant a search runs: k_h1_pp16 (34) needs at least D + 1 = 3 K-slices per
+// tile (the filter constants staged at a tile's first slice must have landed by
+// its epilogue) and 32-bit DMA offsets -- otherwise the ring (5).
 int h1_effective_variant(int variant, int pitch, int64_t ld) {
     const int v = variant == 0 ? 34 : variant;
-    if (v < 18) return v;
-    const int ps = v >= 23 ? 2 : 1, d = v == 21 ? 4 : v == 22 ? 7 : v >= 23 ? 2 : 6;
-    if (pitch % (X3K * ps) || pitch / (X3K * ps) < d + 1 || (ps - 1) * ld * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return 10;
+    if (v == 5) return 5;
+    if (pitch % (X3K * 2) || pitch / (X3K * 2) < 3 || ld * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return 5;
     return v;
 }
 
-// Per row the fused filter's constants {w0, w1, dead, 0} (k_h1_pp stages them per
+// Per row the fused filter's constants {w0, w1, dead, 0} (k_h1_pp16 stages them per
 // tile by DMA): cosine w0 = |x| / xi; L2 w0 = 1 / xi, w1 = |x|^2 (1 - 2^-20) / (2 xi)
 __global__ void k_h1_rowconst(const float* xinv, const float* xnorm, const uint8_t* dead, int64_t n, int metric,
                               float4* xw) {
@@ -2451,15 +1111,13 @@ int launch_h1_rowconst(const float* xinv, const float* xnorm, const uint8_t* dea
                        xw);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-bool h1_timing_diag(int variant) {
-    return (variant >= 7 && variant <= 9) || (variant >= 11 && variant <= 13) || (variant >= 15 && variant <= 17) ||
-           variant == 19 || variant == 20 || (variant >= 24 && variant <= 26) || (variant >= 30 && variant <= 33);
-}
-// regions per tile of a variant's fused filter (k_h1_pp: one per wave)
-int h1_region_split(int variant) { return variant >= 18 ? 8 : 1; }  // (an effective variant)
+// tools build (MH_EXACT_DIAG): the timing diagnostics, which let no pair pass
+bool h1_timing_diag(int variant) { return variant == 30 || variant == 31; }
+// regions per tile of a variant's fused filter (k_h1_pp16: one per wave)
+int h1_region_split(int variant) { return variant == 5 ? 1 : 8; }  // (an effective variant)
 // the variant's regions hold records (H1_REC uint2 each: a lane's 16 accumulators of one
-// block row, tested by k_bucket) instead of passing pairs
-bool h1_records(int variant) { return variant >= 34 && variant <= 38; }
+// block row, tested by k_bucket_rec) instead of passing pairs
+bool h1_records(int variant) { return variant != 5; }
 int launch_h1_sample(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<0>(a, variant, s); }
 int launch_h1_filter(const ExactArgs& a, int variant, hipStream_t s) { return launch_h1<1>(a, variant, s); }
 

@@ -85,24 +85,12 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * 2 fp16 2-product split MFMA, 3 (default) fp16 1-product MFMA with the top-kk
  * preselection fused into the GEMM epilogue; all preselect, re-rank canonically
  * and certify, so results are identical),
- * "exact_tile" (GEMM tile, 0 = the measured best per precision; precisions 1/2:
- * 1 128x256, 2 128x128, 3-6 256x256; precision 3: 1 256x256 S2 R4, 2 256x256
- * S4 R2, 3 256x256 S1 R4, 4 128x256 S2 R4, 5 128x256 S2 R3,
- * 6 128x256 on 4 waves S2 R3 -- S = 16-deep K-blocks per stage, R = ring
- * buffers; 10 256x256 64-deep K-tiles, 2 buffers, 32x32 MFMAs; 14 the same as
- * a persistent stream of 32-deep stages; 18, 21, 22 and 23 the
- * persistent two-group ping-pong stream with 16-deep (18, 21, 22) or 32-deep
- * (23) K-slices on 32x32x16 MFMAs, 27/28 23 with a max-first filter test (27
- * also runs the epilogue in the next R phase), 29 the same stream on 16x16x32
- * MFMAs appending passing pairs, 34 (the default) 29 storing per-lane
- * records of a block row's accumulators that k_bucket tests, 35 34 with
- * non-temporal record stores -- a shape the
- * stream does not admit (fewer than 3 slices per tile) runs 10; 7-9 / 11-13 /
- * 15-17 / 19-20, 24-26, 30-33 timing diagnostics of 5 / 10 / 14 / 18, 23, 29
- * that let no pair pass, so every query takes the canonical
- * fallback: 7/11/15/19/24/30 no epilogue, 8/12/16 also no waits/barriers,
- * 9/13/17/20/25 no DMA, 26/31 the filter tests without the appends, 32 no
- * stores, 33 no permutes), "compat_waves" (1 or 8 waves scoring the compat insert's
+ * "exact_tile" (GEMM variant, 0 = the measured best per precision; precisions 1/2:
+ * 1 128x256, 2 128x128, 3 256x256 ring tiles; precision 3: 34 (the default)
+ * the persistent two-group ping-pong stream k_h1_pp16 on 16x16x32 MFMAs with
+ * the fused filter storing per-lane records of a block row's accumulators,
+ * 5 the ring kernel's fused filter (128x256), which also runs every shape
+ * k_h1_pp16 does not admit), "compat_waves" (1 or 8 waves scoring the compat insert's
  * distance batches), "upper_ef" (beam mode: upper-layer descent width, 1 =
  * greedy), "screen" (beam mode and batched insert, default 1: keep an fp16
  * copy of the rows; a candidate is skipped only when the copy proves the f32

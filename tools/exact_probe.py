@@ -36,8 +36,8 @@ S = Searcher(g, B, 10, d, dev)
 def run():
     try:
         S.run(Q, H.MODE_EXACT, 0)
-    except H.HnswError as e:  # exact_tile 7-9: timing diagnostics return no results
-        if tile < 7:
+    except H.HnswError as e:  # exact_tile 30 / 31 (MHNSW_LIB=tools/libmhnsw_diag.so): no results
+        if tile not in (30, 31):
             raise
         assert "timing diagnostic" in str(e)
 
