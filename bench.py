@@ -44,7 +44,7 @@ import hnsw_amd as H  # noqa: E402
 # revision of the search/build kernels the recorded PMC passes (profiles/*_pmc_*.json)
 # were taken on; a pass recorded on another revision is not attached as `traffic`
 KERNEL_REV = "r03"
-from hnsw_amd.shard import engine_local_search, shard_range, sharded_search  # noqa: E402
+from hnsw_amd.shard import engine_local_search, gather_topk, merge_topk, shard_range, sharded_search  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -79,6 +79,8 @@ def parse():
                    help="1: fp16 screening copy, 0: plain f32 evaluation of every candidate; same results")
     p.add_argument("--ef-sweep", default="32,48,64,72,80,96,128,256",
                    help="extra operating points (ef values) reported at N=1; '' disables")
+    p.add_argument("--shard-ef-sweep", default="64,96,128,192,256",
+                   help="operating points of the shard layout (ef values; recall vs the sharded exact path); '' disables")
     p.add_argument("--batch-sweep", default="1,1024,10000",
                    help="query batch sizes re-measured at ef --ef on the same graph at N=1 (SURVEY 8(d) C2); '' disables")
     p.add_argument("--seed", type=int, default=1234)
@@ -512,6 +514,49 @@ def main():
         srecall = mean_over_ranks(recall_at_k(sk[:ngt], sn[:ngt], ek, en, a.k))
         s_el, s_kms, s_st = timed_steps(sstep, gs)
         skms = float(np.mean(s_kms))
+        # the step's phases (HIP events on torch's stream): local search, the packed
+        # all-gather (RCCL), the GPU merge -- 0 at one rank (nothing is exchanged)
+        ph = {"search": [], "all_gather": [], "merge": []}
+        for _ in range(3):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            ev[0].record()
+            lk, ld, ln = engine_local_search(gs, a.k, H.MODE_BEAM, a.ef)(Qs)
+            ev[1].record()
+            if world > 1:
+                gk, gd, gn = gather_topk(lk, ld, ln)
+                ev[2].record()
+                merge_topk(gk, gd, gn, a.k)
+            else:
+                ev[2].record()
+            ev[3].record()
+            torch.cuda.synchronize()
+            for name, i in (("search", 0), ("all_gather", 1), ("merge", 2)):
+                ph[name].append(ev[i].elapsed_time(ev[i + 1]))
+        phases = {f"{k_}_ms": round(float(np.mean(v)), 4) for k_, v in ph.items()}
+        # operating points of the shard layout (recall vs the sharded exact top-k, QPS of
+        # the whole step: search + exchange + merge, max over ranks), so that one 10M
+        # index (N = 1) and 8 shards of 1.25M (N = 8) compare at equal recall
+        spoints = []
+        for ef in ([int(x) for x in a.shard_ef_sweep.split(",") if x] if a.shard_ef_sweep else []):
+            step_ef = lambda: sharded_search(engine_local_search(gs, a.k, H.MODE_BEAM, ef), Qs, a.k)  # noqa: E731
+            kk_, _, nn_ = (x.clone() for x in step_ef())
+            r_ = mean_over_ranks(recall_at_k(kk_[:ngt], nn_[:ngt], ek, en, a.k))
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(3):
+                step_ef()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            tt_ = torch.tensor([(time.perf_counter() - t1) / 3], dtype=torch.float64, device=device)
+            if world > 1:
+                dist.all_reduce(tt_, op=dist.ReduceOp.MAX)
+            spoints.append({"ef": ef, "recall_at_10": round(r_, 4), "qps": round(a.batch / tt_.item(), 1),
+                            "ms_per_step": round(tt_.item() * 1e3, 3)})
+        gs.device_status()
+        sat99 = next((p_ for p_ in spoints if p_["recall_at_10"] >= 0.99), None)
         shard_out = {
             "value": round(a.batch * a.steps / s_el, 1), "unit": "queries/s",
             "ms_per_step": round(s_el / a.steps * 1e3, 3), "recall_at_10": round(srecall, 4),
@@ -521,6 +566,9 @@ def main():
                          f"one all-gather of {a.batch * (12 * a.k + 4)} B per rank ({a.backend}), k_merge on the GPU"),
             "recall_reference": "sharded exact search (per-shard MFMA exact + the same gather + merge)",
             "build_inserts_per_s_per_rank": round((hi - lo) / sbuild_s, 1),
+            "phases": phases,
+            "operating_points": spoints,
+            "at_recall_0.99": sat99,
             "scaling": "strong (fixed total rows; BASELINE configs[3] at 8 ranks)",
             "layout_ceiling": ("node-ID range shards: every query runs on every shard and a shard's search cost "
                                "falls only ~log(rows per shard), so N ranks serve about the queries/s of one GPU "

@@ -102,7 +102,8 @@ struct mhnsw_index {
     bool any_dead = false;
     // key identity (compat; GraphDev::kid): allocated at the first replaced or re-added key
     int32_t* kid = nullptr;      // [capn] first row that held the row's key
-    int32_t* kidlive = nullptr;  // [capn] by kid: the key's live row (-1 none)
+    int32_t* kidlive = nullptr;  // [capn] by kid: the key's newest live row (-1 none)
+    int32_t* kprev = nullptr;    // [capn] the next older live row of the same key (-1 none; GraphDev::kprev)
     bool aliased = false;
     uint32_t* cur_entry = nullptr;
     int32_t* inc_cnt = nullptr;
@@ -180,6 +181,7 @@ struct mhnsw_index {
     std::vector<uint32_t> hmask;  // bit l: row is in layer l (compat may promote into emptied layers)
     std::vector<uint8_t> hdead;
     std::vector<int32_t> hkid;                       // kid mirror (aliased only)
+    std::vector<int32_t> hprev;                      // kprev mirror (aliased only)
     std::unordered_map<int64_t, int32_t> dead_kid;   // deleted keys -> kid, for a later re-add
     int64_t stats_host[8] = {0};
     std::string err;
@@ -348,7 +350,9 @@ int ensure_capacity(mhnsw_index* h, int64_t need) {
     if ((r = grow(h, h->keys, oc, nc, 0))) return r;
     if ((r = grow(h, h->levels, oc, nc, 0))) return r;
     if ((r = grow(h, h->dead, oc, nc, 0))) return r;
-    if (h->aliased && ((r = grow(h, h->kid, oc, nc, 0xFF)) || (r = grow(h, h->kidlive, oc, nc, 0xFF)))) return r;
+    if (h->aliased && ((r = grow(h, h->kid, oc, nc, 0xFF)) || (r = grow(h, h->kidlive, oc, nc, 0xFF)) ||
+                       (r = grow(h, h->kprev, oc, nc, 0xFF))))
+        return r;
     if ((r = grow(h, h->cur_entry, 0, nc, 0))) return r;
     if ((r = grow(h, h->inc_cnt, 0, nc, 0))) return r;
     if (h->build_mode == MHNSW_BUILD_BATCH || h->inc_src) {
@@ -401,6 +405,7 @@ GraphDev graph_view(const mhnsw_index* h) {
     if (h->h16_metric != h->metric) g.h16 = nullptr;  // stale format: no screening
     g.kid = h->aliased ? h->kid : nullptr;
     g.kidlive = h->aliased ? h->kidlive : nullptr;
+    g.kprev = h->aliased ? h->kprev : nullptr;
     return g;
 }
 
@@ -693,8 +698,10 @@ int start_alias(mhnsw_index* h) {
     if (h->aliased) return 0;
     const int64_t c = std::max<int64_t>(h->capn, 1);
     int r;
-    if ((r = grow(h, h->kid, 0, c, 0xFF)) || (r = grow(h, h->kidlive, 0, c, 0xFF))) return r;
+    if ((r = grow(h, h->kid, 0, c, 0xFF)) || (r = grow(h, h->kidlive, 0, c, 0xFF)) || (r = grow(h, h->kprev, 0, c, 0xFF)))
+        return r;
     h->hkid.resize((size_t)h->n);
+    h->hprev.assign((size_t)h->n, -1);
     std::vector<int32_t> live((size_t)std::max<int64_t>(h->n, 1));
     for (int64_t i = 0; i < h->n; ++i) {
         h->hkid[i] = (int32_t)i;
@@ -711,6 +718,24 @@ int start_alias(mhnsw_index* h) {
 
 // a row leaves the key map (Delete): remember its kid for a later re-add
 void forget_key(mhnsw_index* h, int64_t key, int32_t row) { h->dead_kid[key] = kid_of_row(h, row); }
+
+// every live row of the key, newest first (the key's nodes in disjoint layers: a
+// failed insert leaves its node in the layers above the failing one, graph.go:1009,
+// and a later insert of the key below them adds another)
+std::vector<int32_t> key_rows(const mhnsw_index* h, int64_t key) {
+    std::vector<int32_t> out;
+    auto it = h->key2id.find(key);
+    if (it == h->key2id.end()) return out;
+    for (int32_t r = it->second; r >= 0 && (int)out.size() < MH_MAXL; r = h->aliased ? h->hprev[r] : -1)
+        if (!h->hdead[r]) out.push_back(r);
+    return out;
+}
+// layers[l].nodes[key]: the key's live row that is a member of layer l, -1 none
+int32_t key_row_in(const mhnsw_index* h, int64_t key, int l) {
+    for (int32_t r : key_rows(h, key))
+        if (in_layer(h, r, l)) return r;
+    return -1;
+}
 
 int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_on_device, int64_t n, int dim,
              const int32_t* levels) {
@@ -779,6 +804,7 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
         snap_key2id.emplace(keys[i], it == h->key2id.end() ? -1 : it->second);
     }
     const size_t hm0 = h->hmask.size(), hd0 = h->hdead.size(), hl0 = h->hlevels.size(), hk0 = h->hkid.size();
+    const size_t hp0 = h->hprev.size();
     const size_t nlay0 = h->layers.size();
     h->hmask.resize(n0 + n + 1, 0u);
     h->hdead.resize(n0 + n + 1, 0);
@@ -801,6 +827,7 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
                 h->dead_kid.erase(dk);
             }
             h->hkid.push_back(kid);
+            h->hprev.push_back(-1);
             kidset.push_back(kid);
             kidset.push_back(id);
         } else {
@@ -818,6 +845,11 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
         }
         h->hmask[id] = mask;
         if (mask) {
+            // the key's newest live row; older ones (in higher layers) stay reachable per layer
+            if (h->aliased) {
+                auto kp = h->key2id.find(keys[i]);
+                h->hprev[id] = kp != h->key2id.end() ? kp->second : -1;
+            }
             h->key2id[keys[i]] = id;
         } else if (snap_dead_kid.count(keys[i])) {  // failed before touching a layer: still a deleted key
             h->dead_kid[keys[i]] = snap_dead_kid[keys[i]];
@@ -828,9 +860,11 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     // never reached).  A present key whose node holds a layer at or below the
     // new level is replaced there and ends the walk; one whose node sits only in
     // higher layers (left by a failed insert) is inserted like a new key.
-    int64_t rep = -1, nfresh = 0;
+    int64_t rep = -1, nfresh = 0, cont = -1;
     int rep_i0 = -1;
-    int32_t old = -1;
+    int32_t old = -1;               // the key's newest live row
+    std::vector<int32_t> old_rows;  // all its live rows (the sweep deletes every one)
+    bool rep_in0 = false;           // one of them in layer 0: Len() stays put, "node not added"
     // A host-detected failure after the bookkeeping began (a drawn level past
     // MH_MAXL, a layer, capacity or staging allocation) leaves the index as it
     // was: records, key maps, layers created by this call and the Rng back to
@@ -859,10 +893,12 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
         } else {
             for (int64_t i = 0; i < nfresh; ++i) h->key2id.erase(keys[i]);  // all new (duplicates rejected above)
         }
-        if (old >= 0 && (size_t)old < hd0) h->hdead[old] = 0;  // live until the sweep
+        for (int32_t r : old_rows)
+            if ((size_t)r < hd0) h->hdead[r] = 0;  // live until the sweep
         for (auto& kv : snap_dead_kid) h->dead_kid[kv.first] = kv.second;
         h->hlevels.resize(hl0);
         h->hkid.resize(hk0);
+        h->hprev.resize(hp0);
         h->hmask.resize(hm0);
         h->hdead.resize(hd0);
         h->rng = rng0;
@@ -888,10 +924,12 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
                 auto it = h->key2id.find(keys[i]);
                 if (it != h->key2id.end()) {
                     for (int l = l_i; l >= 0 && rep_i0 < 0; --l)
-                        if (in_layer(h, it->second, l)) rep_i0 = l;
+                        if (key_row_in(h, keys[i], l) >= 0) rep_i0 = l;
                     if (rep_i0 >= 0) {
                         rep = i;
                         old = it->second;
+                        old_rows = key_rows(h, keys[i]);
+                        rep_in0 = key_row_in(h, keys[i], 0) >= 0;
                         break;
                     }
                 }
@@ -917,6 +955,7 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
             rowkey.push_back(keys[rep]);
             h->hlevels.push_back(rep_level);
             h->hkid.push_back(kid);
+            h->hprev.push_back(-1);
         }
         // graph.go:980-1032 top-down, as the walk sees the layers
         for (int l = nl - 1; l > floor; --l) {
@@ -924,12 +963,16 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
             const int32_t id = l > rep_i0 && ida >= 0 ? ida : idb;
             if (l == rep_i0) {  // the sweep, after this layer's search
                 rep_entry[l] = L.entry;
+                // layers[l2].nodes[key] of every layer: one of the key's old rows, or A
                 for (int l2 = 0; l2 < (int)h->layers.size(); ++l2) {
-                    const int32_t x = in_layer(h, old, l2) ? old : (ida >= 0 && ((amask >> l2) & 1u)) ? ida : -1;
+                    int32_t x = -1;
+                    for (int32_t o : old_rows)
+                        if (in_layer(h, o, l2)) x = o;
+                    if (x < 0 && ida >= 0 && ((amask >> l2) & 1u)) x = ida;
                     rep_sweep[l2] = x;
                     if (x >= 0) h->layers[l2].count--;
                 }
-                h->hdead[old] = 1;
+                for (int32_t o : old_rows) h->hdead[o] = 1;
                 if (ida >= 0) h->hdead[ida] = 1;
                 h->any_dead = true;
                 h->key2id[keys[rep]] = idb;
@@ -975,7 +1018,7 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
             else
                 h->key2id[kv.first] = kv.second;
         }
-        if (rep >= 0) h->hdead[old] = 0;  // live until the sweep
+        for (int32_t o : old_rows) h->hdead[o] = 0;  // live until the sweep
         for (auto& kv : snap_dead_kid) h->dead_kid[kv.first] = kv.second;
         for (size_t t = 0; t + 1 < kidset.size() && h->aliased; t += 2)  // unpublish; the replay republishes
             HIPCHK(h, hipMemcpyAsync(h->kidlive + kidset[t], &kNoRow, 4, hipMemcpyHostToDevice, h->stream));
@@ -984,7 +1027,10 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
         kidset.clear();
         snap_dead_kid.clear();
         h->hlevels.resize(n0);
-        if (h->aliased) h->hkid.resize(n0);
+        if (h->aliased) {
+            h->hkid.resize(n0);
+            h->hprev.resize(n0);
+        }
         std::fill(h->hmask.begin() + n0, h->hmask.end(), 0u);
         std::fill(h->hdead.begin() + n0, h->hdead.end(), (uint8_t)0);
         nl = top0 + 1;
@@ -996,11 +1042,17 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
             nl = std::max(nl, rep_level + 1);
             book_rep(fail_layer);
             rows = nfresh + (ida >= 0 ? 2 : 1);
-            if (fail_layer >= rep_i0) {  // failed before the sweep: the old node stays
+            if (fail_layer >= rep_i0) {  // failed before the sweep: the old nodes stay ...
                 h->key2id[keys[rep]] = old;
-                h->hdead[old] = 0;
+                for (int32_t o : old_rows) h->hdead[o] = 0;
                 if (ida >= 0) h->hdead[ida] = 0;
                 h->any_dead = snap_any_dead;
+                // ... and the new node, in the layers above the failing one, is the key's node there
+                const int32_t placed = ida >= 0 && h->hmask[ida] ? ida : h->hmask[idb] ? idb : -1;
+                if (placed >= 0) {
+                    h->hprev[placed] = old;
+                    h->key2id[keys[rep]] = placed;
+                }
             }
         }
         std::vector<int32_t> live;  // (kid, row): the batch's keys' live rows after the replay
@@ -1012,6 +1064,9 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
         }
         for (size_t t = 0; t + 1 < live.size() && h->aliased; t += 2)
             HIPCHK(h, hipMemcpyAsync(h->kidlive + live[t], &live[t + 1], 4, hipMemcpyHostToDevice, h->stream));
+        if (h->aliased)
+            HIPCHK(h, hipMemcpyAsync(h->kprev + n0, h->hprev.data() + n0, (size_t)rows * 4, hipMemcpyHostToDevice,
+                                     h->stream));
         HIPCHK(h, hipMemcpyAsync(h->dead, h->hdead.data(), (size_t)(n0 + rows), hipMemcpyHostToDevice, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
         h->n = n0 + rows;
@@ -1041,6 +1096,8 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
                              h->stream));
     if (h->aliased) {
         HIPCHK(h, hipMemcpyAsync(h->kid + n0, h->hkid.data() + n0, nrows * sizeof(int32_t), hipMemcpyHostToDevice,
+                                 h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->kprev + n0, h->hprev.data() + n0, nrows * sizeof(int32_t), hipMemcpyHostToDevice,
                                  h->stream));
         for (size_t t = 0; t + 1 < kidset.size(); t += 2)
             HIPCHK(h, hipMemcpyAsync(h->kidlive + kidset[t], &kidset[t + 1], 4, hipMemcpyHostToDevice, h->stream));
@@ -1075,8 +1132,13 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
         } else if (r == 0 && rep >= 0) {
             HIPCHK(h, hipMemcpyAsync(h->dead, h->hdead.data(), (size_t)h->n, hipMemcpyHostToDevice, h->stream));
             fix_entries(h);
-            // graph.go:1035-1037: a replacement leaves Len() unchanged
-            if (rep_i0 >= 0) r = fail(h, MHNSW_EINTERNAL, "node not added");
+            // graph.go:1035-1037: a replacement of a key that layer 0 held leaves Len()
+            // unchanged -- "node not added" ends the walk; one whose nodes sat only in
+            // upper layers (left by a failed insert) grows it, and the walk goes on
+            if (rep_in0)
+                r = fail(h, MHNSW_EINTERNAL, "node not added");
+            else
+                cont = rep + 1;
         }
     } else {
         r = run_build_batch(h, n0, n1, top_live, entry_live);
@@ -1088,6 +1150,9 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
         h->build_search_us += ms * 1e3;
     }
     h->tev_used = 0;
+    if (r == 0 && cont > 0 && cont < n)  // the rest of the walk (graph.go:950: the next node)
+        return add_impl(h, keys + cont, vecs + (size_t)cont * dim, vecs_on_device, n - cont, dim,
+                        levels ? levels + cont : nullptr);
     return r;
 }
 
@@ -1161,10 +1226,9 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
     const int top = top_live_layer(h);
     uint32_t entry = (uint32_t)h->layers[top].entry;
     if (entry_key) {
-        auto it = h->key2id.find(*entry_key);
-        if (it == h->key2id.end() || !in_layer(h, it->second, top))
-            return fail(h, MHNSW_EINVAL, "entry key %lld not in top layer", (long long)*entry_key);
-        entry = (uint32_t)it->second;
+        const int32_t e = key_row_in(h, *entry_key, top);
+        if (e < 0) return fail(h, MHNSW_EINVAL, "entry key %lld not in top layer", (long long)*entry_key);
+        entry = (uint32_t)e;
     }
     if ((r = ensure_buf(h, h->qpad, (size_t)B * h->pitch))) return r;
     const float* qsrc = queries;
@@ -1201,7 +1265,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         const int64_t budget = (int64_t)4 << 30;  // score workspace bytes
         int64_t qc = std::max<int64_t>(1, std::min<int64_t>(B, budget / (ldS * 4)));
         qc = std::min<int64_t>(qc, 4096);
-        if ((r = ensure_buf(h, h->scores, (size_t)qc * ldS)) || (r = ensure_buf(h, h->qnorm, (size_t)B)) ||
+        if ((r = ensure_buf(h, h->qnorm, (size_t)B)) ||
             (r = ensure_buf(h, h->cand, (size_t)qc * kk)) || (r = ensure_buf(h, h->xbound, (size_t)qc)) ||
             (r = ensure_buf(h, h->xflag, (size_t)qc)) || (r = ensure_buf(h, h->xflagged, (size_t)qc)) ||
             (r = ensure_buf(h, h->xnflag, 1)) || (r = ensure_buf(h, h->xmaxn, 1)))
@@ -1229,6 +1293,11 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         const int stride = (int)std::max<int64_t>(1, std::min<int64_t>(128, (nnt + h->exact_sample - 1) / h->exact_sample));
         const int64_t nsamp = h1 ? ((h->n / H1_BN) - 1) / stride + 1 : 0;  // sampled full tiles
         const int J = stride < 8 ? kk : h->exact_thr_rank > 0 ? std::min(kk, std::max(k, h->exact_thr_rank)) : std::max(k, kk / 8);
+        // the score workspace: every (query, row) score (precisions 0-2, and their
+        // fallback), or only the sample's (fused path: its fallback streams distances
+        // into per-segment lists, k_fallback_select)
+        if ((r = ensure_buf(h, h->scores, (size_t)qc * (h1 ? (size_t)std::max<int64_t>(nsamp, 1) * H1_BN : (size_t)ldS))))
+            return r;
         int sseg = 1;
         int64_t sseglen = 0;
         if (h1) {
@@ -1429,11 +1498,16 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
             c1.qnorm = h->qnorm.p + q0;
             LCHK(h, launch_rerank(a.Q, g, h->cand.p, kk, nb, h->lpr, h->vpl, k, ok_, od_, on_, oi_, c1, s));
             // uncertified queries: canonical distances of every row, then select + re-rank again
-            LCHK(h, launch_exact_fallback(a.Q, g, h->n, h->xflagged.p, h->xnflag.p, h->scores.p, ldS, h->lpr, h->vpl, s));
             ExactArgs a2 = a;
             a2.only = h->xflag.p;
             a2.bound = nullptr;
-            LCHK(h, launch_exact_select(a2, s));
+            if (h1) {
+                LCHK(h, launch_fallback_select(a.Q, g, a2, h->lpr, h->vpl, s));
+            } else {
+                LCHK(h, launch_exact_fallback(a.Q, g, h->n, h->xflagged.p, h->xnflag.p, h->scores.p, ldS, h->lpr,
+                                              h->vpl, s));
+                LCHK(h, launch_exact_select(a2, s));
+            }
             CertArgs c2{};
             c2.only = h->xflag.p;
             LCHK(h, launch_rerank(a.Q, g, h->cand.p, kk, nb, h->lpr, h->vpl, k, ok_, od_, on_, oi_, c2, s));
@@ -1550,6 +1624,7 @@ void mhnsw_destroy(mhnsw_index* h) {
     F(h->dead);
     F(h->kid);
     F(h->kidlive);
+    F(h->kprev);
     F(h->cur_entry);
     F(h->inc_cnt);
     F(h->inc_src);
@@ -1701,7 +1776,7 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "exact_tile") {
         // precisions 1 / 2: 0-3 (the split GEMM's tiles); precision 3: 0, 5 or 34 (the
         // tools build, MH_EXACT_DIAG, also 30 / 31: timing diagnostics)
-        bool ok = (v >= 0 && v <= 3) || v == 5 || v == 34;
+        bool ok = (v >= 0 && v <= 3) || v == 5 || v == 34 || v == 35;
 #ifdef MH_EXACT_DIAG
         ok = ok || v == 30 || v == 31;
 #endif
@@ -1906,9 +1981,9 @@ int mhnsw_add_plan(mhnsw_index* h, const int64_t* keys, int64_t n, int64_t* nwal
 
 int mhnsw_lookup(mhnsw_index* h, int64_t key, float* out) {
     std::shared_lock<std::shared_mutex> lk(h->mu);
-    auto it = h->key2id.find(key);
-    if (it == h->key2id.end() || !in_layer(h, it->second, 0)) return 0;  // graph.go:906 layers[0].nodes[key]
-    HIPCHK(h, hipMemcpy(out, h->vecs + (size_t)it->second * h->pitch, (size_t)h->dim * 4, hipMemcpyDeviceToHost));
+    const int32_t r0 = key_row_in(h, key, 0);  // graph.go:906 layers[0].nodes[key]
+    if (r0 < 0) return 0;
+    HIPCHK(h, hipMemcpy(out, h->vecs + (size_t)r0 * h->pitch, (size_t)h->dim * 4, hipMemcpyDeviceToHost));
     return 1;
 }
 
@@ -2014,8 +2089,10 @@ void reset_graph(mhnsw_index* h) {
     h->layers_exist = h->any_dead = false;
     F(h->kid);
     F(h->kidlive);
+    F(h->kprev);
     h->aliased = false;
     h->hkid.clear();
+    h->hprev.clear();
     h->dead_kid.clear();
     h->key2id.clear();
     h->hlevels.clear();
@@ -2084,9 +2161,15 @@ int import_csr(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t
         Ly.entry = entry[l];
     }
     HIPCHK(h, hipMemcpy(h->levels, h->hlevels.data(), N * 4, hipMemcpyHostToDevice));
+    // a key's live rows (disjoint layers): the newest heads its chain (key_rows)
     h->key2id.clear();
-    for (int64_t i = 0; i < N; ++i)
-        if (!h->hdead[i] && !h->key2id.count(keys[i])) h->key2id[keys[i]] = (int32_t)i;
+    std::vector<int32_t> prevl((size_t)N, -1);
+    for (int64_t i = 0; i < N; ++i) {
+        if (h->hdead[i]) continue;
+        auto it = h->key2id.find(keys[i]);
+        if (it != h->key2id.end()) prevl[i] = it->second;
+        h->key2id[keys[i]] = (int32_t)i;
+    }
     h->n = N;
     h->layers_exist = L > 0;
     // key identity: several rows of one key (a replaced or re-added key) -> kids
@@ -2101,8 +2184,10 @@ int import_csr(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t
         std::vector<int32_t> live((size_t)N, -1);
         for (int64_t i = 0; i < N; ++i) h->hkid[i] = first[keys[i]];
         for (auto& kv : h->key2id) live[first[kv.first]] = kv.second;
+        h->hprev = prevl;
         HIPCHK(h, hipMemcpy(h->kid, h->hkid.data(), (size_t)N * 4, hipMemcpyHostToDevice));
         HIPCHK(h, hipMemcpy(h->kidlive, live.data(), (size_t)N * 4, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(h->kprev, h->hprev.data(), (size_t)N * 4, hipMemcpyHostToDevice));
     }
     // live rows outside layer 0 (an exported graph keeps a failed insert's upper rows):
     // the brute force skips them as the reference's Search cannot reach them
@@ -2586,20 +2671,27 @@ int mhnsw_delete(mhnsw_index* h, const int64_t* keys, int64_t n, uint8_t* out) {
     for (int64_t i = 0; i < n; ++i) out[i] = 0;
     if (n <= 0 || h->layers.empty()) return 0;
     ++h->mut_epoch;
-    std::vector<uint32_t> ids;
+    std::vector<uint32_t> ids, lay;  // (row, layer) in the reference's order: per key, its layers ascending
     for (int64_t i = 0; i < n; ++i) {
         auto it = h->key2id.find(keys[i]);
         if (it == h->key2id.end()) continue;  // not found (or deleted earlier in this batch)
+        // graph.go:852-861: layers[l].nodes[key] of every layer -- the key's live rows
+        // (usually one; more after a failed insert) hold disjoint layers
+        const std::vector<int32_t> rows = key_rows(h, keys[i]);
+        for (int l = 0; l < (int)h->layers.size(); ++l)
+            for (int32_t id : rows)
+                if (in_layer(h, id, l)) {
+                    h->layers[l].count--;
+                    ids.push_back((uint32_t)id);
+                    lay.push_back((uint32_t)l);
+                }
         const int32_t id = it->second;
         h->key2id.erase(it);
         forget_key(h, keys[i], id);
         if (h->aliased)
             HIPCHK(h, hipMemcpyAsync(h->kidlive + h->hkid[id], &kNoRow, 4, hipMemcpyHostToDevice, h->stream));
-        h->hdead[id] = 1;
-        for (int l = 0; l < (int)h->layers.size(); ++l)
-            if (in_layer(h, id, l)) h->layers[l].count--;
+        for (int32_t r : rows) h->hdead[r] = 1;
         out[i] = 1;
-        ids.push_back((uint32_t)id);
     }
     if (ids.empty()) return 0;
     h->any_dead = true;
@@ -2615,9 +2707,12 @@ int mhnsw_delete(mhnsw_index* h, const int64_t* keys, int64_t n, uint8_t* out) {
     if (h->build_mode == MHNSW_BUILD_FLAT) {
         // no links to repair: the dead flag removes the row from exact search
     } else if (h->build_mode == MHNSW_BUILD_COMPAT) {
-        if ((r = ensure_buf(h, h->cand, ids.size()))) return r;
+        if ((r = ensure_buf(h, h->cand, 2 * ids.size()))) return r;
         HIPCHK(h, hipMemcpyAsync(h->cand.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->cand.p + ids.size(), lay.data(), lay.size() * 4, hipMemcpyHostToDevice,
+                                 h->stream));
         a.ids = h->cand.p;
+        a.lay = h->cand.p + ids.size();
         a.nids = (int64_t)ids.size();
         a.M = h->M;
         const int lr = launch_delete_compat(a, h->lpr, h->vpl, h->stream);

@@ -1047,10 +1047,9 @@ __global__ __launch_bounds__(64) void k_delete_compat(DeleteArgs a) {
     int err = 0;
     for (int64_t i = 0; i < a.nids; ++i) {
         const uint32_t id = a.ids[i];
-        for (int l = 0; l < a.g.nlayers; ++l) {
-            if (ld_i32<true>(a.g.layers[l].deg + id) == -2) continue;
-            isolate<C, G>(a.g, l, id, a.M, S, st, err, ev);
-        }
+        const int l = (int)a.lay[i];
+        if (ld_i32<true>(a.g.layers[l].deg + id) == -2) continue;
+        isolate<C, G>(a.g, l, id, a.M, S, st, err, ev);
     }
     if (lane == 0) {
         atomicAdd(&a.stats[0], st.E);
@@ -1277,14 +1276,20 @@ int MH_PARTFN(launch_build_batch_descend)(const BatchBuildArgs& a, int lpr, int 
     return -3;
 }
 
+// MH_BUILD_GMAX (a build flag, default 8): cap on the rows in flight per wave
+// step of the batched insert's search kernel
+#ifndef MH_BUILD_GMAX
+#define MH_BUILD_GMAX 8
+#endif
 int MH_PARTFN(launch_build_batch_search)(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s) {
-#define X_(L, V, G)                                                          \
-    if (lpr == L && vpl == V) {                                              \
-        if (a.ef <= 64) return launch_batch_search_t<Cfg<L, V>, 1, G>(a, s); \
-        if (a.ef <= 128) return launch_batch_search_t<Cfg<L, V>, 2, G>(a, s); \
-        if (a.ef <= 256) return launch_batch_search_t<Cfg<L, V>, 4, G>(a, s); \
-        if (a.ef <= 512) return launch_batch_search_t<Cfg<L, V>, 8, G>(a, s); \
-        return -4;                                                           \
+#define X_(L, V, G)                                                                                    \
+    if (lpr == L && vpl == V) {                                                                        \
+        constexpr int GB = G < MH_BUILD_GMAX ? G : MH_BUILD_GMAX;                                      \
+        if (a.ef <= 64) return launch_batch_search_t<Cfg<L, V>, 1, GB>(a, s);                          \
+        if (a.ef <= 128) return launch_batch_search_t<Cfg<L, V>, 2, GB>(a, s);                         \
+        if (a.ef <= 256) return launch_batch_search_t<Cfg<L, V>, 4, GB>(a, s);                         \
+        if (a.ef <= 512) return launch_batch_search_t<Cfg<L, V>, 8, GB>(a, s);                         \
+        return -4;                                                                                     \
     }
     MH_FOR_EACH_CFG(X_)
 #undef X_

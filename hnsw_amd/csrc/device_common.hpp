@@ -65,7 +65,12 @@ struct GraphDev {
     // replaced or re-added key leaves several rows with one key; every map
     // operation compares kids).  nullptr until the first such row: kid == row.
     const int32_t* kid;   // [cap_nodes] the first row that ever held this row's key
-    int32_t* kidlive;     // [cap_nodes] by kid: the key's live row (-1 none)
+    int32_t* kidlive;     // [cap_nodes] by kid: the key's newest live row (-1 none)
+    // [cap_nodes] the next older live row of the same key (-1 none): a key can
+    // hold live nodes in several layers at once (a failed insert leaves its node
+    // in the layers above the failing one, graph.go:1009; a later insert of the
+    // key below them adds another), one per layer map, in disjoint layers
+    const int32_t* kprev;
 };
 
 __device__ __forceinline__ bool is_dead(const GraphDev& g, uint32_t id) { return g.dead && g.dead[id]; }

@@ -32,15 +32,18 @@ __device__ __forceinline__ void st_i32(int32_t* p, int32_t v) {
 }
 
 // `layers[l].nodes[*elevator]` (graph.go:497, 574): the layer's node of the
-// elevator row's KEY -- the key's live row if it is a member of layer l, else
-// nil (EMPTY_ID).  The elevator itself may be a replaced or deleted node that
-// a dangling edge led to.
+// elevator row's KEY -- the key's live row that is a member of layer l (its
+// newest, then the older ones through kprev), else nil (EMPTY_ID).  The
+// elevator itself may be a replaced or deleted node that a dangling edge led to.
 template <bool COH>
 __device__ __forceinline__ uint32_t resolve_member(const GraphDev& g, int l, uint32_t e) {
     if (g.kidlive) {
-        const int32_t r = ld_i32<COH>(g.kidlive + kid_of(g, e));
-        if (r < 0 || (uint32_t)r >= g.capn) return EMPTY_ID;
-        e = (uint32_t)r;
+        int32_t r = ld_i32<COH>(g.kidlive + kid_of(g, e));
+        for (int hop = 0; hop < MH_MAXL && r >= 0 && (uint32_t)r < g.capn; ++hop) {  // (rows hold disjoint layers)
+            if (ld_i32<COH>(g.layers[l].deg + r) != -2 && !is_dead(g, (uint32_t)r)) return (uint32_t)r;
+            r = g.kprev ? ld_i32<COH>(g.kprev + r) : -1;
+        }
+        return EMPTY_ID;
     }
     if (e >= g.capn || ld_i32<COH>(g.layers[l].deg + e) == -2 || is_dead(g, e)) return EMPTY_ID;
     return e;

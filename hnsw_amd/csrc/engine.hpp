@@ -101,7 +101,9 @@ int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, int waves, h
 // ---- delete (graph.go:843-895) ----
 struct DeleteArgs {
     GraphDev g;
-    const uint32_t* ids;          // compat: internal ids in BatchDelete order
+    const uint32_t* ids;          // compat: internal ids in BatchDelete order ...
+    const uint32_t* lay;          // ... each isolated in layer lay[i] only (graph.go:852-861 walks a key's
+                                  //     layers; a key's nodes can be several rows in disjoint layers)
     int64_t nids;
     int64_t n;                    // repair: rows [0, n)
     int layer;                    // repair: layer being repaired
@@ -242,6 +244,10 @@ int launch_rerank(const float* Q, const GraphDev& g, const uint32_t* cand, int k
 int launch_exact_fallback(const float* Q, const GraphDev& g, int64_t N, const int32_t* flagged, const int32_t* nflag,
                           float* scores, int64_t ldS, int lpr, int vpl, hipStream_t s);
 
+// the fused path's fallback: canonical distances of every row streamed into per-segment
+// top-kk lists (a.seg_d / a.seg_i, k_select's layout) for the queries a.only flags, then
+// k_select_merge -> a.cand, a.bound (no score matrix)
+int launch_fallback_select(const float* Q, const GraphDev& g, const ExactArgs& a, int lpr, int vpl, hipStream_t s);
 int launch_merge_topk(const int64_t* keys_in, const float* dist_in, const int32_t* n_in, int shards, int64_t B,
                       int k, int64_t* out_keys, float* out_dist, int32_t* out_n, hipStream_t s);
 

@@ -689,6 +689,20 @@ __device__ __forceinline__ void wait_vm_plus(int extra, std::integer_sequence<in
     if (!done) __builtin_amdgcn_s_waitcnt(vmcnt_imm(BASE));
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform n in [LO, HI] (a binary tree of scalar branches)
+template <int LO, int HI>
+__device__ __forceinline__ void wait_vm_range(int n) {
+    if constexpr (LO == HI) {
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(LO));
+    } else {
+        constexpr int MID = (LO + HI) / 2;
+        if (n <= MID)
+            wait_vm_range<LO, MID>(n);
+        else
+            wait_vm_range<MID + 1, HI>(n);
+    }
+}
+
 #define MH_DSR(dst, addr, off) asm volatile("ds_read_b128 %0, %1 offset:" #off : "=v"(dst) : "v"(addr))
 
 // ---------------------------------------------------------------------------
@@ -723,7 +737,7 @@ __device__ __forceinline__ void wait_vm_plus(int extra, std::integer_sequence<in
 // 4 the filter's tests without the record stores (no pair passes: every query
 // takes the canonical fallback, results stay exact).
 // ---------------------------------------------------------------------------
-template <int EPI, int DIAG = 0>
+template <int EPI, int DIAG = 0, int EXW = 0>
 __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     constexpr int NS = 4, D = 2, PS = 2;
     static_assert(NS >= D + 2 && D >= 1, "ring depth");
@@ -777,6 +791,14 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
         p_base = plane + r0 * 32;
         p_lim = (int)min<int64_t>(255, (g == 0 ? a.B : a.N) - 1 - r0);
     };
+    // EXW: exact in-order accounting of this wave's vector-memory operations
+    // (vmcnt retires them in issue order, MI355X_MICROARCH.md): opc counts every
+    // one issued, mk_last / mk_prev the count right after the newest / the
+    // previous slice's pieces, so the wait for a slice allows exactly the
+    // operations issued after it -- an epilogue's record stores then stay in
+    // flight until a slice issued after them is waited for, instead of the
+    // next wait (the count only under-counts, which waits for more: safe).
+    int opc = 0, mk_last = 0, mk_prev = 0;
     auto produce = [&]() {  // this wave's pieces of the producer slice, then advance it
         const char* base = sbase(p_base + (int64_t)p_kt * PS * ld * 32);
 #pragma unroll
@@ -786,6 +808,9 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + off),
                                              (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
         }
+        opc += 2 * PS;
+        mk_prev = mk_last;
+        mk_last = opc;
         if (++p_slot == NS) p_slot = 0;
         if (++p_kt == nkt) {
             p_kt = 0;
@@ -912,6 +937,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                                     ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
                             }
                             nst += 5;  // (at least 5 store instructions: never an over-count)
+                            opc += 5;
                             cnt += __popcll(m);
                         }
                     }
@@ -923,16 +949,21 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                 filt(std::false_type{});
             if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;  // (DIAG 4: 0)
             ++nst;
+            ++opc;
         }
     };
 
     constexpr int VMC = vmcnt_imm(2 * PS * (D - 1));
     constexpr int VMCNT0 = 0x0F70;
     auto wait_vmc = [&]() {
-        if (nst > 0)
+        if constexpr (EXW) {  // the operations issued after the awaited slice (D = 2: the previous one)
+            const int y = __builtin_amdgcn_readfirstlane(opc - mk_prev);
+            wait_vm_range<2 * PS * (D - 1), 63>(min(y, 63));
+        } else if (nst > 0) {
             wait_vm_plus<2 * PS * (D - 1)>(nst, std::make_integer_sequence<int, 59>{});  // (vmcnt <= 63)
-        else
+        } else {
             __builtin_amdgcn_s_waitcnt(VMC);
+        }
     };
     p_set();
     int64_t ps = 0;
@@ -985,6 +1016,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                 __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
                                                  (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
                 ++nst;
+                ++opc;
             }
         }
         if (ps < S) {
@@ -1041,7 +1073,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     }
 }
 
-template <int EPI, int DIAG = 0>
+template <int EPI, int DIAG = 0, int EXW = 0>
 static int launch_h1_pp16_t(const ExactArgs& a, hipStream_t s) {
     if (a.pitch % (X3K * 2)) return -5;
     if (std::max(a.ldQs, a.ldXs) * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return -5;  // 32-bit DMA offsets
@@ -1049,7 +1081,7 @@ static int launch_h1_pp16_t(const ExactArgs& a, hipStream_t s) {
     const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
     const int64_t nblk = nqt * nnt;
     const int64_t W = std::min<int64_t>(nblk, std::max(8, device_cus() / 8 * 8));
-    hipLaunchKernelGGL((k_h1_pp16<EPI, DIAG>), dim3((unsigned)W), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((k_h1_pp16<EPI, DIAG, EXW>), dim3((unsigned)W), dim3(512), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1069,6 +1101,7 @@ static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
     if (a.B <= 0 || a.N <= 0) return 0;
     switch (variant) {
         case 5: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 3, EPI>(a, s);
+        case 35: return launch_h1_pp16_t<EPI, 0, EPI>(a, s);
 #ifdef MH_EXACT_DIAG
         case 30: return launch_h1_pp16_t<EPI, EPI ? 1 : 0>(a, s);
         case 31: return launch_h1_pp16_t<EPI, EPI ? 4 : 0>(a, s);
@@ -1652,6 +1685,91 @@ __global__ __launch_bounds__(256) void k_exact_fallback(const float* __restrict_
     }
 }
 
+// The fused path's fallback (precision 3): for each uncertified query, the
+// canonical distance of every row (k_exact_fallback's arithmetic) streamed
+// straight into a top-kk per row segment -- no score matrix.  Block (b, s):
+// query b (flag[b] set, else it exits at once), segment s of nseg; its 4 waves
+// take a quarter of the segment each, keep the best kk by (distance, id), and
+// wave 0 merges the four lists (LDS) into the segment's list, in k_select's
+// layout for k_select_merge.  Deleted rows and NaN distances never enter.
+template <class C, int G, int R>
+__global__ __launch_bounds__(256) void k_fallback_select(const float* __restrict__ Q, GraphDev g, int64_t N,
+                                                         const uint8_t* __restrict__ flag, int kk, int nseg,
+                                                         int64_t seglen, float* seg_d, uint32_t* seg_i) {
+    using RM = RowMap<C, G>;
+    constexpr int GROUP = C::LPR >> RM::LG;
+    __shared__ float md[4 * 64 * R];
+    __shared__ uint32_t mi[4 * 64 * R];
+    const int64_t b = blockIdx.x / nseg;
+    const int sg = (int)(blockIdx.x % nseg);
+    if (!flag[b]) return;
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const float inf = __int_as_float(0x7f800000);
+    QReg<C> q;
+    load_query(q, Q + (size_t)b * C::PITCH);
+    const float qn = query_norm(q);
+    const int64_t lo = (int64_t)sg * seglen, hi = min(lo + seglen, N);
+    const int64_t sub = (max<int64_t>(hi - lo, 0) + 3) / 4;
+    const int64_t wlo = lo + w * sub, whi = min(wlo + sub, hi);
+    BList<R> L;
+    bl_init(L);
+    float worst = inf;
+    for (int64_t base = wlo; base < whi; base += RM::T) {
+        uint32_t ids[G];
+        bool valid[G];
+#pragma unroll
+        for (int gg = 0; gg < G; ++gg) {
+            const int64_t r = base + RM::reg_row(gg, lane);
+            valid[gg] = r < whi;
+            ids[gg] = valid[gg] ? (uint32_t)r : 0u;
+        }
+        const float sacc = g.metric == EUCLIDEAN ? eval_rows<C, G, true>(q, g.vecs, g.pitch, ids, valid)
+                                                 : eval_rows<C, G, false>(q, g.vecs, g.pitch, ids, valid);
+        const int64_t rown = base + RM::owned_row(lane);
+        const bool own = rown < whi && (lane & (GROUP - 1)) == 0;
+        float d = inf;
+        if (own) {
+            const float xn = g.metric == COSINE ? g.norms[rown] : 1.f;
+            d = finalize(g.metric, sacc, xn, qn);
+            if (g.dead && g.dead[rown]) d = inf;
+        }
+        // <=: a row tying the kk-th distance may still win on its id
+        unsigned long long m = __ballot(own && d <= worst && d < inf);
+        while (m) {
+            const int src = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            if (bl_insert(L, kk, rl_f(d, src), (uint32_t)rl_u((uint32_t)rown, src))) {
+                float wd;
+                uint32_t wi;
+                bl_at(L, kk - 1, wd, wi);
+                worst = wi == EMPTY_ID ? inf : wd;
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        md[(w * R + r) * 64 + lane] = L.d[r];
+        mi[(w * R + r) * 64 + lane] = L.i[r];
+    }
+    __syncthreads();
+    if (w != 0) return;
+    for (int ow = 1; ow < 4; ++ow)
+        for (int e = 0; e < kk; ++e) {
+            const uint32_t id = mi[(ow * R + (e >> 6)) * 64 + (e & 63)];  // (uniform reads: every lane the same entry)
+            if (id == EMPTY_ID) break;
+            bl_insert(L, kk, md[(ow * R + (e >> 6)) * 64 + (e & 63)], id & ID_MASK);
+        }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int idx = r * 64 + lane;
+        if (idx < kk) {
+            const size_t o = ((size_t)b * nseg + sg) * kk + idx;
+            seg_d[o] = L.d[r];
+            seg_i[o] = L.i[r] == EMPTY_ID ? EMPTY_ID : (L.i[r] & ID_MASK);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // merge S shard lists (each sorted, n_in valid) -> best k by (distance, key)
 // ---------------------------------------------------------------------------
@@ -1774,6 +1892,30 @@ int launch_exact_fallback(const float* Q, const GraphDev& g, int64_t N, const in
         hipLaunchKernelGGL((k_exact_fallback<Cfg<L, V>, (G < 4 ? G : 4)>), dim3(1024), dim3(256), 0, s, Q, g, N, \
                            flagged, nflag, scores, ldS);                                                     \
         return hipGetLastError() == hipSuccess ? 0 : -1;                                                     \
+    }
+    MH_FOR_EACH_CFG(X_)
+#undef X_
+    return -3;
+}
+
+int launch_fallback_select(const float* Q, const GraphDev& g, const ExactArgs& a, int lpr, int vpl, hipStream_t s) {
+    if (a.B <= 0 || a.N <= 0) return 0;
+    if (a.kk < 1 || a.kk > 256 || a.nseg < 1 || a.nseg * a.kk > SEL_MERGE_MAX || !a.only) return -4;
+    const dim3 grid((unsigned)(a.B * a.nseg));
+#define X_(L, V, G)                                                                                            \
+    if (lpr == L && vpl == V) {                                                                                \
+        constexpr int GF = G < 4 ? G : 4;                                                                      \
+        if (a.kk <= 64)                                                                                        \
+            hipLaunchKernelGGL((k_fallback_select<Cfg<L, V>, GF, 1>), grid, dim3(256), 0, s, Q, g, a.N, a.only, \
+                               a.kk, a.nseg, a.seglen, a.seg_d, a.seg_i);                                       \
+        else if (a.kk <= 128)                                                                                  \
+            hipLaunchKernelGGL((k_fallback_select<Cfg<L, V>, GF, 2>), grid, dim3(256), 0, s, Q, g, a.N, a.only, \
+                               a.kk, a.nseg, a.seglen, a.seg_d, a.seg_i);                                       \
+        else                                                                                                   \
+            hipLaunchKernelGGL((k_fallback_select<Cfg<L, V>, GF, 4>), grid, dim3(256), 0, s, Q, g, a.N, a.only, \
+                               a.kk, a.nseg, a.seglen, a.seg_d, a.seg_i);                                       \
+        hipLaunchKernelGGL(k_select_merge, dim3((unsigned)a.B), dim3(64), 0, s, a);                            \
+        return hipGetLastError() == hipSuccess ? 0 : -1;                                                       \
     }
     MH_FOR_EACH_CFG(X_)
 #undef X_

@@ -261,6 +261,12 @@ struct og_graph {
     int acap;
     int64_t *keys;
     int32_t *kid;  /* [cap_nodes] key identity: the first row that held keys[row] */
+    /* [cap_nodes] the next older live row of the same key (-1 none).  A key can
+     * hold live nodes in several layers at once -- a failed insert leaves its
+     * node in the layers above the failing one (graph.go:1009), a later insert of
+     * the key below them adds another -- each layer's map holding one of them:
+     * hget(key) is the newest, prev_live links the rest (disjoint layers). */
+    int32_t *prev_live;
     float *vecs;
     float *norms;
     uint8_t *dead; /* [cap_nodes] 1 = deleted (graph.go:843-864); rows stay for dangling edges */
@@ -407,6 +413,7 @@ void og_destroy(og_graph *g) {
     free_layers(g);
     free(g->keys);
     free(g->kid);
+    free(g->prev_live);
     free(g->vecs);
     free(g->norms);
     free(g->dead);
@@ -469,6 +476,10 @@ static int ensure_nodes(og_graph *g, int64_t need) {
     if (!dd) return -1;
     for (int64_t i = g->cap_nodes; i < nc; ++i) dd[i] = 0;
     g->dead = dd;
+    int32_t *pl = (int32_t *)realloc(g->prev_live, sizeof(int32_t) * (size_t)nc);
+    if (!pl) return -1;
+    for (int64_t i = g->cap_nodes; i < nc; ++i) pl[i] = -1;
+    g->prev_live = pl;
     uint32_t *vis = (uint32_t *)realloc(g->scr.visited, sizeof(uint32_t) * (size_t)nc);
     if (!vis) return -1;
     for (int64_t i = g->cap_nodes; i < nc; ++i) vis[i] = 0;
@@ -537,10 +548,12 @@ static inline int member(const og_graph *g, int l, int32_t id) {
  * KEY -- the key's live row when it is a member of layer l, else nil.  The
  * elevator row itself may be a replaced or deleted node reached through a
  * dangling edge. */
-static inline int32_t resolve(og_graph *g, int l, int32_t row) {
-    int32_t r = hget(g, g->keys[row]);
-    return member(g, l, r) ? r : -1;
+static inline int32_t key_row_in(og_graph *g, int64_t key, int l) {
+    for (int32_t r = hget(g, key); r >= 0; r = g->prev_live[r])
+        if (member(g, l, r)) return r;
+    return -1;
 }
+static inline int32_t resolve(og_graph *g, int l, int32_t row) { return key_row_in(g, g->keys[row], l); }
 
 /* highest layer with a live node (empty top layers are skipped by Search:
  * entry() == nil -> search() == nil -> continue, graph.go:572-582) */
@@ -835,20 +848,27 @@ int og_preview_levels(og_graph *g, int64_t n, int32_t *out) {
 static void isolate(og_graph *g, int l, int32_t n, int m);
 
 /* graph.go:1015-1024: BatchAdd found the key in layer i0 (after that layer's
- * search): every layer holding the key -- the old node, and the new node's own
- * upper row A in the layers above i0 -- deletes it and isolates it, in layer
- * order.  Both rows stay behind their one-directional edges, like Delete's. */
-static void replace_sweep(og_graph *g, int64_t key, int32_t old, int32_t ida, int32_t idb) {
-    g->dead[old] = 1;
+ * search): every layer holding the key -- the key's old nodes (one per layer,
+ * from one or several rows), and the new node's own upper row A in the layers
+ * above i0 -- deletes it and isolates it, in layer order.  The rows stay behind
+ * their one-directional edges, like Delete's. */
+static void replace_sweep(og_graph *g, int64_t key, int32_t ida, int32_t idb) {
+    int nl = g->nlayers > 0 ? g->nlayers : 1;
+    int32_t *rows = (int32_t *)malloc(sizeof(int32_t) * (size_t)nl);
+    for (int l = 0; l < g->nlayers; ++l) {
+        rows[l] = key_row_in(g, key, l);
+        if (rows[l] < 0 && ida >= 0 && g->layers[l].deg[ida] != -2) rows[l] = ida;
+    }
+    for (int32_t r = hget(g, key); r >= 0; r = g->prev_live[r]) g->dead[r] = 1;
     if (ida >= 0) g->dead[ida] = 1;
     for (int l = 0; l < g->nlayers; ++l) {
-        og_layer *L = &g->layers[l];
-        int32_t r = L->deg[old] != -2 ? old : (ida >= 0 && L->deg[ida] != -2) ? ida : -1;
-        if (r < 0) continue;
-        L->count--; /* delete(l.nodes, key) */
-        isolate(g, l, r, g->M);
+        if (rows[l] < 0) continue;
+        g->layers[l].count--; /* delete(l.nodes, key) */
+        isolate(g, l, rows[l], g->M);
     }
+    free(rows);
     hput(g, key, idb);
+    g->prev_live[idb] = -1;
 }
 
 static void fix_entries(og_graph *g);
@@ -872,14 +892,16 @@ int og_add(og_graph *g, const int64_t *keys, const float *vecs, int64_t n, int d
             if (add_layer(g)) return set_err(g, OG_ENOMEM, "out of memory");
         g->layers_exist = 1;
         /* a present key: the first layer (from the top) at or below the insert
-         * level whose map holds it is where the replacement happens */
-        int32_t old = hget(g, key);
+         * level whose map holds it is where the replacement happens; Len() then
+         * stays put -- "node not added" -- only when layer 0 held it */
+        int32_t head = hget(g, key);
         int i0 = -1;
-        for (int l = level; old >= 0 && l >= 0; --l)
-            if (member(g, l, old)) {
+        for (int l = level; head >= 0 && l >= 0; --l)
+            if (key_row_in(g, key, l) >= 0) {
                 i0 = l;
                 break;
             }
+        const int in0 = head >= 0 && key_row_in(g, key, 0) >= 0;
         /* rows: the new node's layers above i0 (deleted again by the sweep) get a
          * row of their own, A; B holds it from i0 down */
         int need_a = 0;
@@ -895,7 +917,10 @@ int og_add(og_graph *g, const int64_t *keys, const float *vecs, int64_t n, int d
             memcpy(g->vecs + (size_t)id * dim, vec, sizeof(float) * (size_t)dim);
             g->norms[id] = og_dev_norm(vec, dim);
         }
-        if (i0 < 0 && hput(g, key, idb)) return set_err(g, OG_ENOMEM, "out of memory");
+        if (i0 < 0) { /* a fresh node: the key's newest live row (older ones stay in their layers) */
+            if (hput(g, key, idb)) return set_err(g, OG_ENOMEM, "out of memory");
+            g->prev_live[idb] = head;
+        }
         float qn = g->norms[idb];
         int32_t elevator = -1;
         int32_t *nbh = (int32_t *)malloc(sizeof(int32_t) * (size_t)(g->M + 2));
@@ -917,17 +942,30 @@ int og_add(og_graph *g, const int64_t *keys, const float *vecs, int64_t n, int d
             if (cnt == 0) {
                 free(nbh);
                 free(nbd);
-                /* graph.go:1009 returns here: the node keeps the layers above;
-                 * in none of them, its key is not present */
-                int any = 0;
-                for (int l2 = 0; l2 < g->nlayers; ++l2) any |= g->layers[l2].deg[idb] != -2;
-                if (i0 < 0 && !any) hdel(g, key);
+                /* graph.go:1009 returns here: the node keeps the layers above */
+                int any_b = 0, any_a = 0;
+                for (int l2 = 0; l2 < g->nlayers; ++l2) {
+                    any_b |= g->layers[l2].deg[idb] != -2;
+                    any_a |= ida >= 0 && g->layers[l2].deg[ida] != -2;
+                }
+                if (i0 < 0 && !any_b) { /* in none of them: the key is as before */
+                    if (head >= 0)
+                        hput(g, key, head);
+                    else
+                        hdel(g, key);
+                } else if (i0 >= 0 && l >= i0) { /* before the sweep: the new node joins the key's rows */
+                    const int32_t placed = any_a ? ida : any_b ? idb : -1;
+                    if (placed >= 0) {
+                        hput(g, key, placed);
+                        g->prev_live[placed] = head;
+                    }
+                }
                 fix_entries(g);
                 return set_err(g, OG_EINTERNAL, "no nodes found in neighborhood search");
             }
             elevator = nbh[0]; /* graph.go:1013 */
             if (level >= l) {  /* graph.go:1015-1032 */
-                if (l == i0) replace_sweep(g, key, old, ida, idb);
+                if (l == i0) replace_sweep(g, key, ida, idb);
                 L->deg[id] = -1;
                 L->count++;
                 for (int j = 0; j < cnt; ++j) {
@@ -938,10 +976,11 @@ int og_add(og_graph *g, const int64_t *keys, const float *vecs, int64_t n, int d
         }
         free(nbh);
         free(nbd);
-        if (i0 >= 0) { /* graph.go:1035-1037: Len() did not grow -> the batch stops here */
+        if (i0 >= 0 && in0) { /* graph.go:1035-1037: Len() did not grow -> the batch stops here */
             fix_entries(g);
             return set_err(g, OG_EINTERNAL, "node not added");
         }
+        if (i0 >= 0) fix_entries(g); /* the sweep may have emptied an entry; the walk goes on */
     }
     return OG_OK;
 }
@@ -1053,20 +1092,24 @@ static void fix_entries(og_graph *g) {
 
 int og_delete(og_graph *g, const int64_t *keys, int64_t n, int mode, int heuristic, int keep_pruned, uint8_t *out) {
     int any = 0;
+    int32_t *rows = (int32_t *)malloc(sizeof(int32_t) * (size_t)(g->nlayers > 0 ? g->nlayers : 1));
     for (int64_t i = 0; i < n; ++i) {
-        int32_t id = hget(g, keys[i]);
+        int32_t head = hget(g, keys[i]);
         out[i] = 0;
-        if (id < 0 || g->nlayers == 0) continue;
+        if (head < 0 || g->nlayers == 0) continue;
+        /* layers[l].nodes[key] of every layer (the key's rows hold disjoint layers) */
+        for (int l = 0; l < g->nlayers; ++l) rows[l] = key_row_in(g, keys[i], l);
+        for (int32_t r = head; r >= 0; r = g->prev_live[r]) g->dead[r] = 1;
         hdel(g, keys[i]);
-        g->dead[id] = 1;
         any = 1;
         for (int l = 0; l < g->nlayers; ++l) { /* graph.go:852-861 */
-            if (g->layers[l].deg[id] == -2) continue;
+            if (rows[l] < 0) continue;
             g->layers[l].count--;
             out[i] = 1;
-            if (mode == 0) isolate(g, l, id, g->M); /* cap M on every layer (Q13) */
+            if (mode == 0) isolate(g, l, rows[l], g->M); /* cap M on every layer (Q13) */
         }
     }
+    free(rows);
     if (any && mode == 1)
         for (int l = 0; l < g->nlayers; ++l) repair_layer(g, l, l == 0 ? g->M0 : g->M, heuristic, keep_pruned);
     if (any) fix_entries(g);
@@ -1160,8 +1203,8 @@ static int search_prologue(og_graph *g, int64_t B, int dim, int k, const int64_t
     int top = top_live_layer(g);
     *entry = g->layers[top].entry;
     if (entry_key) {
-        int32_t e = hget(g, *entry_key);
-        if (e < 0 || !member(g, top, e))
+        int32_t e = key_row_in(g, *entry_key, top);
+        if (e < 0)
             return set_err(g, OG_EINVAL, "entry key %lld not in top layer", (long long)*entry_key);
         *entry = e;
     }
@@ -1431,7 +1474,11 @@ int og_import(og_graph *g, int64_t N, int dim, int L, int cap, const int64_t *ke
         g->norms[i] = og_dev_norm(vecs + (size_t)i * dim, dim);
         g->dead[i] = dead ? dead[i] : 0;
         g->kid[i] = kid_get(g, keys[i], (int32_t)i);
-        if (!g->dead[i] && hget(g, keys[i]) < 0) hput(g, keys[i], (int32_t)i);
+        g->prev_live[i] = -1;
+        if (!g->dead[i]) { /* the newest live row heads the key's chain */
+            g->prev_live[i] = hget(g, keys[i]);
+            hput(g, keys[i], (int32_t)i);
+        }
     }
     for (int l = 0; l < L; ++l) {
         og_layer *Ly = &g->layers[l];

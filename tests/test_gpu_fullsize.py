@@ -192,7 +192,7 @@ def test_fullsize_c5_exact(H, O):
     g.close()
 
 
-@pytest.mark.parametrize("tile", [34, 5])
+@pytest.mark.parametrize("tile", [34, 35, 5])
 @pytest.mark.parametrize("metric,k", [("cosine", 10), ("cosine", 256), ("l2", 64)])
 def test_exact_record_variants(H, O, tile, metric, k):
     """Both precision-3 GEMM variants -- k_h1_pp16 with the record-mode fused
@@ -237,4 +237,32 @@ def test_exact_threshold_rank(H, O, metric, k, rank):
     got = _search(g, Q, k, H.MODE_EXACT, 0)
     for a, b in zip(ref, got):
         assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8)), rank
+    g.close()
+
+
+@pytest.mark.parametrize("metric", ["cosine", "l2"])
+def test_exact_fused_fallback_segments(H, O, metric):
+    """kk = k leaves the certificate no margin, so (nearly) every query takes the
+    fallback.  On the fused fp16 path it streams canonical distances into
+    per-segment lists (k_fallback_select: 16 segments x 4 waves per query, no
+    score matrix); the results equal the f32-input path's (whose fallback writes
+    a score row per query), bitwise, with deleted rows and a ragged row count."""
+    n, d, B, k = 200_003, 768, 96, 10
+    X = _gen(n, d, 63, metric)
+    Q = _gen(B, d, 64, metric)
+    dist = H.CosineDistance if metric == "cosine" else H.EuclideanDistance
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=dist, Rng=5, build_mode=H.BUILD_FLAT)
+    g.reserve(n, d)
+    g.add_device(np.arange(n), X.data_ptr(), n, d)
+    g.BatchDelete([int(x) for x in np.random.default_rng(3).choice(n, 2000, replace=False)])
+    g.set_option("exact_kk", k)
+    res = {}
+    for prec in (0, 3):
+        g.set_option("exact_precision", prec)
+        g.reset_stats()
+        res[prec] = _search(g, Q, k, H.MODE_EXACT, 0)
+        assert g.stats()["exact_uncertified"] >= B // 2, (prec, g.stats())
+    for a, b in zip(res[0], res[3]):
+        assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+    assert (res[3][2] == k).all()
     g.close()

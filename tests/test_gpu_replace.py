@@ -90,13 +90,11 @@ def test_readd_live_keys(H, O, metric, M, ml, d, seeded):
             lv = np.concatenate([lv, np.zeros(len(ks) - w, np.int32)])
         err = _both_add(H, O, g, o, ks, V, lv)
         errors[err] = errors.get(err, 0) + 1
-        if err is None or err == "node not added":
-            for k, v in zip(ks[:w], vs[:w]):
-                vec[k] = v
-        else:  # the walk failed part way: re-sync the model of live keys from the oracle
-            ex = o.export()
-            live = ex["dead"] == 0
-            vec = {int(k): ex["vecs"][i] for i, k in enumerate(ex["keys"]) if live[i] and ex["deg"][0, i] != -2}
+        # the model of live keys (layer 0) from the oracle: a walk goes on past a key
+        # whose nodes sat only in upper layers, and stops part way on a failure
+        ex = o.export()
+        live = ex["dead"] == 0
+        vec = {int(k): ex["vecs"][i] for i, k in enumerate(ex["keys"]) if live[i] and ex["deg"][0, i] != -2}
         _agree(H, O, g, o, Q)
         if seeded:
             assert np.array_equal(g.preview_levels(8), o.preview_levels(8))
@@ -265,3 +263,79 @@ def test_add_capacity_failure_leaves_index_unchanged(H, O, compat, dup):
         _search_parity(H, O, b, o, Q)
     a.close()
     b.close()
+
+
+def _partial_keys(o):
+    """keys with a live node outside layer 0 (left by a failed insert), and their layers"""
+    ex = o.export()
+    out = {}
+    for i, k in enumerate(ex["keys"]):
+        if ex["dead"][i] == 0 and ex["deg"][0, i] == -2:
+            layers = [l for l in range(ex["deg"].shape[0]) if ex["deg"][l, i] != -2]
+            if layers:  # (a failed insert's row that reached no layer is no node)
+                out[int(k)] = layers
+    return out
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_partial_nodes_resolved_per_layer(H, O, metric):
+    """A failed insert (graph.go:1009) leaves its node in the layers above the
+    failing one.  The reference's layer maps are keyed by K, so:
+      * a later insert of that key at or above one of those layers sweeps the
+        old node (graph.go:1015-1024) and -- layer 0 never held it -- Len()
+        grows: no "node not added", BatchAdd goes on with the next nodes;
+      * an insert of that key below all of them adds a second live node; each
+        layer's map resolves the key to the node it holds (the elevator,
+        graph.go:997-1003, 574), Lookup to the layer-0 one, Delete removes both.
+    Ops are driven identically on the engine and the oracle; every step agrees
+    (rows, adjacency, errors, compat / beam / exact results)."""
+    rng = np.random.default_rng(900 + metric)
+    n, d, M = 600, 8, 6
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    keys = np.arange(n, dtype=np.int64) * 3 + 1
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=0.5, EfSearch=16, seed=55)
+    g = H.Graph(M=M, Ml=0.5, EfSearch=16, Distance=_metric_fn(H, metric), Rng=55)
+    assert _both_add(H, O, g, o, keys, X) is None
+    Q = rng.uniform(-1, 1, (24, d)).astype(np.float32)
+    # delete most of the graph, then add keys back at high levels: elevators through
+    # deleted nodes fail inserts part way
+    gone = [int(k) for k in rng.choice(keys, int(0.7 * n), replace=False)]
+    assert o.delete(gone) == g.BatchDelete(gone)
+    _agree(H, O, g, o, Q)
+    fresh = 10**6
+    seen = {"continue": 0, "second": 0}
+    for step in range(60):
+        part = _partial_keys(o)
+        ks, lv = [], []
+        if part and step % 2 == 0:
+            k = int(rng.choice(list(part)))
+            top = max(part[k])
+            if rng.random() < 0.5:  # at or above one of its layers: swept, the walk goes on
+                ks.append(k)
+                lv.append(int(rng.integers(min(part[k]), top + 2)))
+                seen["continue"] += 1
+            elif min(part[k]) > 0:  # below all of them: a second live node
+                ks.append(k)
+                lv.append(int(rng.integers(0, min(part[k]))))
+                seen["second"] += 1
+        for _ in range(int(rng.integers(1, 5))):
+            r = rng.random()
+            ks.append(int(rng.choice(gone)) if r < 0.5 else fresh)
+            fresh += r >= 0.5
+            lv.append(int(rng.integers(0, 5)))
+        V = rng.uniform(-1, 1, (len(ks), d)).astype(np.float32)
+        err = _both_add(H, O, g, o, ks, V, np.array(lv, np.int32))
+        assert err in (None, "no nodes found in neighborhood search", "node not added"), err
+        _agree(H, O, g, o, Q, efs=(16, 40))
+        for k in ks:  # Lookup = layers[0].nodes[key]
+            gv, gok = g.Lookup(k)
+            ex = o.export()
+            rows = [i for i, kk in enumerate(ex["keys"]) if kk == k and ex["dead"][i] == 0 and ex["deg"][0, i] != -2]
+            assert gok == bool(rows), k
+            if rows:
+                assert np.array_equal(gv, ex["vecs"][rows[0]]), k
+        if step % 10 == 9:  # Delete removes every node of a key
+            dk = list(_partial_keys(o))[:3] + [int(rng.choice(keys))]
+            assert o.delete(dk) == g.BatchDelete(dk)
+            _agree(H, O, g, o, Q)
+    assert seen["continue"] + seen["second"] > 0, seen
