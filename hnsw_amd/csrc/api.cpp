@@ -1776,7 +1776,7 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "exact_tile") {
         // precisions 1 / 2: 0-3 (the split GEMM's tiles); precision 3: 0, 5 or 34 (the
         // tools build, MH_EXACT_DIAG, also 30 / 31: timing diagnostics)
-        bool ok = (v >= 0 && v <= 3) || v == 5 || v == 34 || v == 35;
+        bool ok = (v >= 0 && v <= 3) || v == 5 || v == 34;
 #ifdef MH_EXACT_DIAG
         ok = ok || v == 30 || v == 31;
 #endif

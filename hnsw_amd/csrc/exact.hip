@@ -689,20 +689,6 @@ __device__ __forceinline__ void wait_vm_plus(int extra, std::integer_sequence<in
     if (!done) __builtin_amdgcn_s_waitcnt(vmcnt_imm(BASE));
 }
 
-// s_waitcnt vmcnt(n) for a wave-uniform n in [LO, HI] (a binary tree of scalar branches)
-template <int LO, int HI>
-__device__ __forceinline__ void wait_vm_range(int n) {
-    if constexpr (LO == HI) {
-        __builtin_amdgcn_s_waitcnt(vmcnt_imm(LO));
-    } else {
-        constexpr int MID = (LO + HI) / 2;
-        if (n <= MID)
-            wait_vm_range<LO, MID>(n);
-        else
-            wait_vm_range<MID + 1, HI>(n);
-    }
-}
-
 #define MH_DSR(dst, addr, off) asm volatile("ds_read_b128 %0, %1 offset:" #off : "=v"(dst) : "v"(addr))
 
 // ---------------------------------------------------------------------------
@@ -737,7 +723,7 @@ __device__ __forceinline__ void wait_vm_range(int n) {
 // 4 the filter's tests without the record stores (no pair passes: every query
 // takes the canonical fallback, results stay exact).
 // ---------------------------------------------------------------------------
-template <int EPI, int DIAG = 0, int EXW = 0>
+template <int EPI, int DIAG = 0>
 __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     constexpr int NS = 4, D = 2, PS = 2;
     static_assert(NS >= D + 2 && D >= 1, "ring depth");
@@ -791,14 +777,6 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
         p_base = plane + r0 * 32;
         p_lim = (int)min<int64_t>(255, (g == 0 ? a.B : a.N) - 1 - r0);
     };
-    // EXW: exact in-order accounting of this wave's vector-memory operations
-    // (vmcnt retires them in issue order, MI355X_MICROARCH.md): opc counts every
-    // one issued, mk_last / mk_prev the count right after the newest / the
-    // previous slice's pieces, so the wait for a slice allows exactly the
-    // operations issued after it -- an epilogue's record stores then stay in
-    // flight until a slice issued after them is waited for, instead of the
-    // next wait (the count only under-counts, which waits for more: safe).
-    int opc = 0, mk_last = 0, mk_prev = 0;
     auto produce = [&]() {  // this wave's pieces of the producer slice, then advance it
         const char* base = sbase(p_base + (int64_t)p_kt * PS * ld * 32);
 #pragma unroll
@@ -808,9 +786,6 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + off),
                                              (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
         }
-        opc += 2 * PS;
-        mk_prev = mk_last;
-        mk_last = opc;
         if (++p_slot == NS) p_slot = 0;
         if (++p_kt == nkt) {
             p_kt = 0;
@@ -937,7 +912,6 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                                     ra[nb] = make_float4(acc[mb][nb][0], acc[mb][nb][1], acc[mb][nb][2], acc[mb][nb][3]);
                             }
                             nst += 5;  // (at least 5 store instructions: never an over-count)
-                            opc += 5;
                             cnt += __popcll(m);
                         }
                     }
@@ -949,17 +923,13 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                 filt(std::false_type{});
             if (lane == 0) a.region_cnt[L * 8 + wave] = cnt;  // (DIAG 4: 0)
             ++nst;
-            ++opc;
         }
     };
 
     constexpr int VMC = vmcnt_imm(2 * PS * (D - 1));
     constexpr int VMCNT0 = 0x0F70;
     auto wait_vmc = [&]() {
-        if constexpr (EXW) {  // the operations issued after the awaited slice (D = 2: the previous one)
-            const int y = __builtin_amdgcn_readfirstlane(opc - mk_prev);
-            wait_vm_range<2 * PS * (D - 1), 63>(min(y, 63));
-        } else if (nst > 0) {
+        if (nst > 0) {
             wait_vm_plus<2 * PS * (D - 1)>(nst, std::make_integer_sequence<int, 59>{});  // (vmcnt <= 63)
         } else {
             __builtin_amdgcn_s_waitcnt(VMC);
@@ -1016,7 +986,6 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                 __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
                                                  (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
                 ++nst;
-                ++opc;
             }
         }
         if (ps < S) {
@@ -1073,7 +1042,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     }
 }
 
-template <int EPI, int DIAG = 0, int EXW = 0>
+template <int EPI, int DIAG = 0>
 static int launch_h1_pp16_t(const ExactArgs& a, hipStream_t s) {
     if (a.pitch % (X3K * 2)) return -5;
     if (std::max(a.ldQs, a.ldXs) * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return -5;  // 32-bit DMA offsets
@@ -1081,7 +1050,7 @@ static int launch_h1_pp16_t(const ExactArgs& a, hipStream_t s) {
     const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
     const int64_t nblk = nqt * nnt;
     const int64_t W = std::min<int64_t>(nblk, std::max(8, device_cus() / 8 * 8));
-    hipLaunchKernelGGL((k_h1_pp16<EPI, DIAG, EXW>), dim3((unsigned)W), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((k_h1_pp16<EPI, DIAG>), dim3((unsigned)W), dim3(512), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1101,7 +1070,6 @@ static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
     if (a.B <= 0 || a.N <= 0) return 0;
     switch (variant) {
         case 5: return launch_ring_t<2, 4, 2, 2, RING_H1, 2, 3, EPI>(a, s);
-        case 35: return launch_h1_pp16_t<EPI, 0, EPI>(a, s);
 #ifdef MH_EXACT_DIAG
         case 30: return launch_h1_pp16_t<EPI, EPI ? 1 : 0>(a, s);
         case 31: return launch_h1_pp16_t<EPI, EPI ? 4 : 0>(a, s);

@@ -113,11 +113,13 @@ int mhnsw_reserve(mhnsw_index *h, int64_t n, int dim);
  * levels: NULL draws each level like randomLevel (graph.go:388-417) from the
  * handle's RNG; non-NULL injects them (a host drawing from its own Rng, or
  * parity testing).  COMPAT build mode follows BatchAdd's walk: the nodes are
- * inserted in order up to the first key already present (in the index or
- * earlier in the batch); that node replaces the key's node -- after its layer
- * search, every layer holding the key deletes and isolates it
- * (graph.go:1015-1024) -- and the walk stops with "node not added" (MHNSW_EINTERNAL;
- * graph.go:1035-1037: Len() did not grow).  A failing insert ("no nodes found in
+ * inserted in order; a node whose key is already present (in the index or
+ * earlier in the batch) replaces the key's nodes -- after its layer search,
+ * every layer holding the key deletes and isolates it (graph.go:1015-1024) --
+ * and when layer 0 held the key the walk stops with "node not added"
+ * (MHNSW_EINTERNAL; graph.go:1035-1037: Len() did not grow); a key whose nodes
+ * sat only in upper layers (left by a failed insert) leaves Len() one higher,
+ * and the walk goes on.  A failing insert ("no nodes found in
  * neighborhood search", graph.go:1009) also ends the walk, leaving the graph as
  * the reference leaves it.  Add of a present key deadlocks in the reference
  * (graph.go:511-513 -> Delete re-locks, :844); here it is BatchAdd's walk.

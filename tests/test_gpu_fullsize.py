@@ -192,7 +192,7 @@ def test_fullsize_c5_exact(H, O):
     g.close()
 
 
-@pytest.mark.parametrize("tile", [34, 35, 5])
+@pytest.mark.parametrize("tile", [34, 5])
 @pytest.mark.parametrize("metric,k", [("cosine", 10), ("cosine", 256), ("l2", 64)])
 def test_exact_record_variants(H, O, tile, metric, k):
     """Both precision-3 GEMM variants -- k_h1_pp16 with the record-mode fused

@@ -153,3 +153,28 @@ def test_screened_batch_build_identical(H, metric, alpha):
         ex2.append(g.export())
         g.close()
     _same_graph(ex2[0], ex2[1])
+
+
+@pytest.mark.parametrize("d", [1024, 1536])
+def test_batch_build_wide_lists(H, O, d):
+    """The batched insert with the widest candidate list (efConstruction 400:
+    8 registers per lane) at the configurations that evaluate 4 rows per wave
+    step (1024-d, 1536-d): the same graph with and without the fp16 screen, and
+    the oracle's beam search on it == the engine's."""
+    rng = np.random.default_rng(700 + d)
+    n = 3000
+    X, Q = _adversarial(rng, n, d, 0)
+    graphs = []
+    for scr in (1, 0):
+        g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_BATCH,
+                    ef_construction=400, heuristic=2, keep_pruned=1, m0=32, screen=scr)
+        g.add_arrays(np.arange(n), X)
+        graphs.append(g)
+    ea, eb = graphs[0].export(), graphs[1].export()
+    for name in ("deg", "adj", "entry"):
+        assert np.array_equal(ea[name], eb[name]), name
+    o = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=16, M0=32, Ml=0.25, EfSearch=64)
+    o.import_graph(**ea)
+    _same_results(*_search(graphs[0], Q, 64, H), *o.search(Q, 10, mode=O.MODE_BEAM, ef=64))
+    for g in graphs:
+        g.close()
