@@ -45,7 +45,7 @@ struct BuildSmem {
 // Rows are loaded together with their degree (one round trip; entries past
 // the degree are ignored): the sequential walk is bound by dependent loads.
 template <class C, int G, class Ev>
-__device__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v, const Ev& ev) {
+__device__ __forceinline__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v, const Ev& ev) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
     int32_t* row = g.layers[l].adj + (size_t)n * capl;
@@ -70,7 +70,7 @@ __device__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v, co
 // may hold another row of that key), else append; returns the new degree and,
 // in *rowout (nullable), the row after the assignment (lane i: entry i)
 template <class Ev>
-__device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw, const Ev& ev,
+__device__ __forceinline__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw, const Ev& ev,
                            int32_t* rowout = nullptr) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
@@ -92,6 +92,108 @@ __device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw, co
     return present ? d : d + 1;
 }
 
+// graph.go:172-219 when the outcome does not depend on the walk order.  With
+// one row per key (no replaced keys: g.kid == nullptr) the candidates are a SET
+// -- neighbours of neighbours, minus n and its neighbours, one per key -- and
+// when the pops it takes are strict minima (no NaN, no tie at any pop) every
+// heap shape pops the same rows in the same order.  So: stage the rows without
+// their keys, collect the set through the visited table in any lane order,
+// score it, and check the pops before making any of them.  Returns false
+// (nothing changed) when a NaN or a tie needs the reference's exact push
+// order; replenish then takes the ordered walk.
+template <class C, int G, class Ev>
+__device__ __forceinline__ bool replenish_set(const GraphDev& g, int l, uint32_t n, int m, int dn, int32_t rv, BuildSmem& S,
+                              WaveStats& st, int& err, const Ev& ev) {
+    const int lane = lane_id();
+    const int capl = g.layers[l].cap;
+    const uint32_t mine = lane < dn ? guard_id(g, (uint32_t)rv) : 0u;
+    const int mydeg = lane < dn ? min(ld_i32<true>(g.layers[l].deg + mine), capl) : -1;
+    const int tot = min(dn * capl, S.hcap);
+    const int vsize = 1 << S.cs.vlog2, vmask = vsize - 1;
+    vis_clear(S.cs.vis, vsize);
+    ev.sync();
+    if (lane == 0) vis_probe(S.cs.vis, vmask, n);     // graph.go:184
+    if (lane < dn) vis_probe(S.cs.vis, vmask, mine);  // graph.go:187-189
+    ev.sync();
+    int ncand = 0;
+    constexpr int U = 4;  // rows' entries in flight per pass
+    for (int e0 = 0; e0 < tot; e0 += 64 * U) {
+        int32_t x[U];
+        int dj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // uniform trip count: the shuffles see every lane
+            const int e = e0 + u * 64 + lane;
+            const int j = min(e / capl, 63), i = e % capl;
+            const uint32_t nb = shfl_u(mine, j);
+            x[u] = e < tot && j < dn ? ld_i32<true>(g.layers[l].adj + (size_t)nb * capl + i) : -1;
+            dj[u] = __shfl(mydeg, j, 64);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = e0 + u * 64 + lane;
+            const int i = e % capl;
+            uint32_t v = EMPTY_ID;
+            if (e < tot && i < dj[u]) v = guard_id(g, (uint32_t)x[u]);
+            int pr = 0;
+            if (v != EMPTY_ID) pr = vis_probe(S.cs.vis, vmask, v);  // graph.go:198-201
+            if (__ballot(pr == 2)) err = 1;
+            int cnt;
+            const uint32_t cid = compact(v, pr == 1, cnt);
+            if (ncand + cnt > S.hcap) {
+                err |= 8;
+                cnt = S.hcap - ncand;
+            }
+            if (lane < cnt) ev.list[ncand + lane] = cid;
+            ncand += cnt;
+        }
+    }
+    ev.sync();
+    st.E += ncand;
+    CPROF_CNT(19, ncand);
+    {
+        QReg<C> q;
+        load_query(q, g.vecs + (size_t)n * g.pitch);
+        ev.template score<C, G>(g, q, g.norms[n], ncand, COSINE, S.hd, S.hi);  // graph.go:204 hard-coded cosine
+    }
+    ev.sync();
+    bool anynan = false;
+    for (int e = lane; e < ncand; e += 64) anynan |= !(S.hd[e] == S.hd[e]);
+    const int need = min(m - dn, ncand);  // each pop adds a new key: deg grows by one
+    if (__ballot(anynan) || need > 64) return false;
+    uint32_t popped = 0xFFFFFFFFu;  // lane p: the candidate index of pop p
+    for (int p = 0; p < need; ++p) {
+        float mv = __int_as_float(0x7f800000);
+        int mi = -1;
+        for (int e = lane; e < ncand; e += 64) {
+            bool gone = false;
+            for (int j = 0; j < p; ++j) gone |= rl_u(popped, j) == (uint32_t)e;
+            const float v = S.hd[e];
+            if (!gone && (mi < 0 || v < mv)) {
+                mv = v;
+                mi = e;
+            }
+        }
+        float wm = mi < 0 ? __int_as_float(0x7f800000) : mv;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) wm = fminf(wm, __shfl_xor(wm, o, 64));
+        int eq = 0;
+        for (int e = lane; e < ncand; e += 64) {
+            bool gone = false;
+            for (int j = 0; j < p; ++j) gone |= rl_u(popped, j) == (uint32_t)e;
+            eq += (!gone && S.hd[e] == wm) ? 1 : 0;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) eq += __shfl_xor(eq, o, 64);
+        if (eq != 1) return false;  // a tie: the heap's shape decides
+        const unsigned long long own = __ballot(mi >= 0 && mv == wm);
+        const int bi = __shfl(mi, __ffsll((long long)own) - 1, 64);
+        if (lane == p) popped = (uint32_t)bi;
+    }
+    CPROF_CNT(15, 1);
+    for (int p = 0; p < need; ++p) list_append(g, l, n, S.hi[rl_u(popped, p)], ev);  // graph.go:213-218
+    return true;
+}
+
 // graph.go:172-219.  The neighbours' rows and keys are staged in LDS in one
 // pass (instead of one dependent load chain per neighbour); the candidates are
 // then collected in the reference's walk order (neighbours, then their
@@ -99,7 +201,7 @@ __device__ int list_append(const GraphDev& g, int l, uint32_t n, uint32_t nw, co
 // rows at once, and ONE distance batch scores them all; the heap sees the
 // pushes in the same order as a per-neighbour loop would produce.
 template <class C, int G, class Ev>
-__device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err,
+__device__ __forceinline__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err,
                           const Ev& ev) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
@@ -107,6 +209,14 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
     int dn = ld_i32<true>(g.layers[l].deg + n);
     if (dn < 0) dn = 0;
     if (dn >= m) return;
+    CPROF_T(tr);
+    CPROF_CNT(18, 1);
+    if (!g.kid) {
+        const bool done = replenish_set<C, G>(g, l, n, m, dn, rv, S, st, err, ev);
+        CPROF_ADD(tr, 14);
+        if (done) return;
+        CPROF_CNT(20, 1);
+    }
     uint32_t mine = 0xFFFFFFFFu;
     int64_t key = INT64_MAX;
     if (lane < dn) {
@@ -136,6 +246,7 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
         }
     }
     ev.sync();
+    CPROF_ADD(tr, 5);
     // The reference's walk (graph.go:184-210): visited = {n} + n's neighbours;
     // then each neighbour j in key order, each of its neighbours in key order,
     // collecting the ones not yet visited.  All rows at once: (1) every entry's
@@ -166,6 +277,7 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
         }
     }
     ev.sync();
+    CPROF_ADD(tr, 6);
     const int vsize = 1 << S.cs.vlog2, vmask = vsize - 1;
     vis_clear(S.cs.vis, vsize);
     ev.sync();
@@ -193,23 +305,18 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
         ncand += cnt;
     }
     ev.sync();
+    CPROF_ADD(tr, 7);
+    CPROF_CNT(19, ncand);
     st.E += ncand;
     // distances in push order (the reference pushes each into its heap)
     {
         QReg<C> q;
         load_query(q, g.vecs + (size_t)n * g.pitch);
         const float qn = g.norms[n];
-        int t = 0;
-        ev.template run_list<C, G>(g, q, qn, ncand, COSINE,  // graph.go:204 hard-coded cosine
-                                   [&](float d, uint32_t u) {
-                                       if (lane == 0) {
-                                           S.hd[t] = d;
-                                           S.hi[t] = u;
-                                       }
-                                       ++t;
-                                   });
+        ev.template score<C, G>(g, q, qn, ncand, COSINE, S.hd, S.hi);  // graph.go:204 hard-coded cosine
     }
     ev.sync();
+    CPROF_ADD(tr, 8);
     // graph.go:213-218 (len < m before every add: addNeighbor cannot evict).
     // Every Pop returns the heap's minimum.  While no distance is NaN and the
     // minimum of what is left is unique, that is the arg-min whatever shape
@@ -281,46 +388,69 @@ __device__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem
         }
         list_append(g, l, n, best, ev);
     }
+    CPROF_ADD(tr, 9);
 }
 
 // graph.go:41-81
 template <class C, int G, class Ev>
-__device__ void add_neighbor(const GraphDev& g, int l, uint32_t n, uint32_t nw, int m, BuildSmem& S, WaveStats& st,
+__device__ __forceinline__ void add_neighbor(const GraphDev& g, int l, uint32_t n, uint32_t nw, int m, BuildSmem& S, WaveStats& st,
                              int& err, const Ev& ev) {
     const int lane = lane_id();
     int32_t rv;
+    CPROF_T(ta);
     const int d = list_append(g, l, n, nw, ev, &rv);
+    CPROF_ADD(ta, 1);
     if (d <= m) return;
-    uint32_t nb = 0xFFFFFFFFu;
-    int64_t key = INT64_MAX;
-    if (lane < d) {
-        nb = guard_id(g, (uint32_t)rv);
-        key = g.keys[nb];
-    }
-    rank_sort(key, nb, d);  // Go map order -> ascending key
+    CPROF_CNT(17, 1);
+    uint32_t nb = lane < d ? guard_id(g, (uint32_t)rv) : 0xFFFFFFFFu;
     QReg<C> q;
     load_query(q, g.vecs + (size_t)n * g.pitch);
     const float qn = g.norms[n];
     float worst_d = -__int_as_float(0x7f800000);
     uint32_t worst = EMPTY_ID;
     st.E += d;
-    ev.template run<C, G>(g, q, qn, nb, d, g.metric, [&](float dd, uint32_t u) {  // graph.go:60-71
+    // graph.go:60-71 takes the first maximum in map order.  A unique maximum and
+    // no NaN make the order irrelevant: score the row as it lies, and rank it
+    // by key (the map-order stand-in) only when a tie or a NaN needs it.
+    int nmax = 0;
+    bool nan = false;
+    ev.template run<C, G>(g, q, qn, nb, d, g.metric, [&](float dd, uint32_t u) {
+        nan |= !(dd == dd);
         if (dd > worst_d || worst == EMPTY_ID) {
             worst_d = dd;
             worst = u;
+            nmax = 1;
+        } else if (dd == worst_d) {
+            ++nmax;
         }
     });
+    if (nan || nmax > 1) {
+        int64_t key = lane < d ? g.keys[nb] : INT64_MAX;
+        rank_sort(key, nb, d);  // Go map order -> ascending key
+        worst_d = -__int_as_float(0x7f800000);
+        worst = EMPTY_ID;
+        st.E += d;
+        ev.template run<C, G>(g, q, qn, nb, d, g.metric, [&](float dd, uint32_t u) {  // graph.go:60-71
+            if (dd > worst_d || worst == EMPTY_ID) {
+                worst_d = dd;
+                worst = u;
+            }
+        });
+    }
+    CPROF_ADD(ta, 2);
     if (worst == EMPTY_ID) return;
     list_remove<C, G>(g, l, n, worst, ev);  // graph.go:74
     if (ld_i32<true>(g.layers[l].deg + worst) >= 0) list_remove<C, G>(g, l, worst, n, ev);  // graph.go:76-78
+    CPROF_ADD(ta, 3);
     replenish<C, G>(g, l, worst, m, S, st, err, ev);  // graph.go:79
+    CPROF_ADD(ta, 4);
 }
 
 // graph.go:221-235 isolate: neighbours in ascending key order (the map-order
 // stand-in) drop their backlink and are replenished; the deleted node's own
 // row stays (the reference keeps the layerNode behind one-directional edges).
 template <class C, int G, class Ev>
-__device__ void isolate(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err,
+__device__ __forceinline__ void isolate(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err,
                         const Ev& ev) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
@@ -393,7 +523,7 @@ struct MwEval {
     int nw;
     template <class C2, int G, class Sink>
     __device__ __forceinline__ void run_list(const GraphDev& g, const QReg<C2>& q, float qn, int cnt, int metric,
-                                             Sink&& sink) const {
+                                             Sink&& sink, bool sinks = true) const {
         if (cnt <= 0) return;
         const int lane = lane_id();
 #pragma unroll
@@ -404,10 +534,19 @@ struct MwEval {
             hdr->metric = metric;
             hdr->qn = qn;
         }
+        CPROF_T(tp);
         mw_barrier();  // post
         mw_share<C2, G>(g, q, qn, list, dist, cnt, metric, 0, nw);
         mw_barrier();  // collect
-        for (int t = 0; t < cnt; ++t) sink(dist[t], list[t]);
+        CPROF_ADD(tp, 11);
+        // the results go through registers: the sink loop reads lanes, not LDS
+        for (int b = 0; sinks && b < cnt; b += 64) {
+            const int c = min(64, cnt - b);
+            const float dv = lane < c ? dist[b + lane] : 0.f;
+            const uint32_t iv = lane < c ? list[b + lane] : 0u;
+            for (int t = 0; t < c; ++t) sink(rl_f(dv, t), rl_u(iv, t));
+        }
+        CPROF_ADD(tp, 12);
     }
     template <class C2, int G, class Sink>
     __device__ __forceinline__ void run(const GraphDev& g, const QReg<C2>& q, float qn, uint32_t cid, int cnt,
@@ -415,6 +554,16 @@ struct MwEval {
         if (cnt <= 0) return;
         if (lane_id() < cnt) list[lane_id()] = cid;
         run_list<C2, G>(g, q, qn, cnt, metric, sink);
+    }
+    // rows list[0, cnt): distance e into outd[e], the row into outi[e]
+    template <class C2, int G>
+    __device__ __forceinline__ void score(const GraphDev& g, const QReg<C2>& q, float qn, int cnt, int metric,
+                                          float* outd, uint32_t* outi) const {
+        run_list<C2, G>(g, q, qn, cnt, metric, [](float, uint32_t) {}, false);
+        for (int e = lane_id(); e < cnt; e += 64) {
+            outd[e] = dist[e];
+            outi[e] = list[e];
+        }
     }
     // the master's own lanes only (workers never touch graph state)
     __device__ __forceinline__ void sync() const {
@@ -424,7 +573,7 @@ struct MwEval {
 };
 
 template <class C, int G>
-__device__ void mw_worker(const GraphDev& g, const MwEval<C>& ev, int w) {
+__device__ __forceinline__ void mw_worker(const GraphDev& g, const MwEval<C>& ev, int w) {
     for (;;) {
         mw_barrier();
         if (ev.hdr->cmd == MW_EXIT) break;
@@ -476,7 +625,7 @@ __host__ __device__ constexpr size_t build_smem_words(int vis_log2, int M, int e
 // live row becomes id_b.  Returns false on the reference's "no nodes found in
 // neighborhood search" (layer in *fail_layer).
 template <class C, int G, class Ev>
-__device__ bool compat_insert(const CompatBuildArgs& a, BuildSmem& S, const Ev& ev, WaveStats& st, int& err,
+__device__ __forceinline__ bool compat_insert(const CompatBuildArgs& a, BuildSmem& S, const Ev& ev, WaveStats& st, int& err,
                               int level, int top, uint32_t id_a, uint32_t id_b, int i0, const int32_t* ent,
                               const int32_t* sweep, int& fail_layer) {
     const int lane = lane_id();
@@ -496,7 +645,9 @@ __device__ bool compat_insert(const CompatBuildArgs& a, BuildSmem& S, const Ev& 
         uint32_t sp = ent[l] < 0 ? EMPTY_ID : (uint32_t)ent[l];
         if (elevator != EMPTY_ID) sp = resolve_member<true>(a.g, l, elevator);
         int cnt = 0;
+        CPROF_T(ts);
         if (sp != EMPTY_ID) cnt = compat_layer<C, G, true>(a.g, l, sp, a.M, a.ef, q, qn, S.cs, st, err, ev);  // :1005
+        CPROF_ADD(ts, 0);
         if (cnt == 0) {  // search(nil) -> "no nodes found in neighborhood search"
             fail_layer = l;
             return false;
@@ -505,19 +656,23 @@ __device__ bool compat_insert(const CompatBuildArgs& a, BuildSmem& S, const Ev& 
         if (level >= l) {       // graph.go:1015-1032
             const uint32_t nbh = lane < cnt ? S.cs.ri[lane] : 0u;
             if (l == i0) {
+                CPROF_T(ti);
                 for (int l2 = 0; l2 < a.g.nlayers; ++l2)  // graph.go:1018-1023
                     if (sweep[l2] >= 0) isolate<C, G>(a.g, l2, (uint32_t)sweep[l2], a.M, S, st, err, ev);
                 ev.sync();
                 if (lane == 0) st_i32(a.g.kidlive + kid_of(a.g, id_b), (int32_t)id_b);
+                CPROF_ADD(ti, 10);
             }
             ev.sync();
             if (lane == 0) st_i32(a.g.layers[l].deg + id, -1);
             ev.sync();
+            CPROF_T(tn);
             for (int j = 0; j < cnt; ++j) {
                 const uint32_t c = rl_u(nbh, j);
                 add_neighbor<C, G>(a.g, l, c, id, a.M, S, st, err, ev);
                 add_neighbor<C, G>(a.g, l, id, c, a.M, S, st, err, ev);
             }
+            CPROF_ADD(tn, 13);
         }
     }
     return true;
@@ -526,7 +681,7 @@ __device__ bool compat_insert(const CompatBuildArgs& a, BuildSmem& S, const Ev& 
 // graph.go:942-1042 for the fresh inserts [n0, n1), then the replacing insert
 // (a.rep_level >= 0), in order; the first failing insert ends the walk
 template <class C, int G, class Ev>
-__device__ void compat_inserts(const CompatBuildArgs& a, BuildSmem& S, const Ev& ev, WaveStats& st, int& err) {
+__device__ __forceinline__ void compat_inserts(const CompatBuildArgs& a, BuildSmem& S, const Ev& ev, WaveStats& st, int& err) {
     int top = a.top0;
     int fail_layer = -1;
     int64_t fail_row = -1;
@@ -597,7 +752,20 @@ __global__ __launch_bounds__(64 * NW) void k_build_compat_mw(CompatBuildArgs a) 
     }
     WaveStats st;
     int err = 0;
+#ifdef MH_COMPAT_PROF
+    if (lane_id() < 24) mh_cprof[lane_id()] = 0;
+    __builtin_amdgcn_wave_barrier();
+    CPROF_T(tk);
+    CPROF_CNT(16, a.n1 - a.n0);
+#endif
     compat_inserts<C, G>(a, S, ev, st, err);
+#ifdef MH_COMPAT_PROF
+    CPROF_ADD(tk, 21);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if (lane_id() == 0) {
+        for (int i = 0; i < 24; ++i) printf("cprof %d %llu\n", i, mh_cprof[i]);
+    }
+#endif
     if (lane_id() == 0) ev.hdr->cmd = MW_EXIT;
     mw_barrier();  // releases the workers
     if (lane_id() == 0) {
@@ -1228,6 +1396,8 @@ static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
 // configurations' kernels compile in parallel; each part instantiates its
 // share of the configurations, and part 0 also holds the dispatchers, which
 // ask each part in turn (-3: configuration not in that part).
+// (MH_NO_PARTS: templates only, for ISA inspection of one instantiation)
+#ifndef MH_NO_PARTS
 #ifndef MH_PART
 #define MH_PART 0
 #endif
@@ -1372,5 +1542,6 @@ int launch_delete_repair(const DeleteArgs& a, int lpr, int vpl, hipStream_t s) {
 }
 #undef MH_ASK_PARTS
 #endif
+#endif  // MH_NO_PARTS
 
 }  // namespace mh

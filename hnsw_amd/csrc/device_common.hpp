@@ -459,7 +459,17 @@ __device__ __forceinline__ void bl_at(const BList<R>& L, int idx, float& d, uint
         }
 }
 
-// insert (d,u) keeping the best `ef` entries; returns true when inserted
+// one-lane shift up across the wave (lane l gets lane l-1, lane 0 gets
+// `in`): DPP wave_shr:1, no LDS permute on the list's insertion path
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t in) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)in, (int)v, 0x138, 0xf, 0xf, false);
+}
+
+// insert (d,u) keeping the best `ef` entries; returns true when inserted.
+// Registers wholly before the insertion point keep their entries and
+// registers past ef stay empty (uniform branches); the ones in between shift
+// by one entry, highest first so that each reads its predecessor's last lane
+// before that register moves.
 template <int R>
 __device__ __forceinline__ bool bl_insert(BList<R>& L, int ef, float d, uint32_t u) {
     if (!(d == d)) return false;  // NaN never enters the list
@@ -475,27 +485,18 @@ __device__ __forceinline__ bool bl_insert(BList<R>& L, int ef, float d, uint32_t
 #pragma unroll
     for (int r = 0; r < R; ++r) pos += __popcll(__ballot(lt_di(L.d[r], L.i[r] & ID_MASK, d, u)));
     const int lane = lane_id();
-    float pd[R];
-    uint32_t pi[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        pd[r] = __shfl_up(L.d[r], 1, 64);
-        pi[r] = (uint32_t)__shfl_up((int)L.i[r], 1, 64);
-        if (r > 0) {
-            float cd = rl_f(L.d[r - 1], 63);
-            uint32_t ci = rl_u(L.i[r - 1], 63);
-            if (lane == 0) {
-                pd[r] = cd;
-                pi[r] = ci;
-            }
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
+    for (int r = R - 1; r >= 0; --r) {
+        if (r * 64 >= ef) continue;   // empty, stays empty
+        if (r * 64 + 63 < pos) break;  // this register and the ones below are unchanged
+        const uint32_t cd = r > 0 ? rl_u(__float_as_uint(L.d[r > 0 ? r - 1 : 0]), 63) : 0u;
+        const uint32_t ci = r > 0 ? rl_u(L.i[r > 0 ? r - 1 : 0], 63) : EMPTY_ID;
+        const float sd = __uint_as_float(wave_shr1(__float_as_uint(L.d[r]), cd));
+        const uint32_t si = wave_shr1(L.i[r], ci);
         const int idx = r * 64 + lane;
         if (idx > pos) {
-            L.d[r] = pd[r];
-            L.i[r] = pi[r];
+            L.d[r] = sd;
+            L.i[r] = si;
         } else if (idx == pos) {
             L.d[r] = d;
             L.i[r] = u;
@@ -592,6 +593,80 @@ __device__ __forceinline__ void gh_pop(GHeap& h, float& d, uint32_t& id) {
 // PopLast == Remove(Len()-1): i == n, no swap (heap/heap.go:73-81)
 __device__ __forceinline__ void gh_poplast(GHeap& h) { h.n--; }
 
+// The same heap with slot i in lane i (capacity 64), for the compat walks'
+// small heaps (ef + 1 and k + 1 entries): the sift loops run on readlane /
+// writelane instead of dependent LDS round trips.  Sifts move a hole instead
+// of swapping; the slots end up exactly where Go's swap loops put them.
+struct RHeap {
+    float d = 0.f;
+    uint32_t id = 0u;
+    int n = 0;
+};
+__device__ __forceinline__ void rh_set(RHeap& h, int j, float d, uint32_t id) {
+    const bool me = lane_id() == j;  // (no writelane builtin in this compiler: compare + select)
+    h.d = me ? d : h.d;
+    h.id = me ? id : h.id;
+}
+// element (xd, xi) entering at slot j, moved up (heap.go up: Less(j, parent))
+__device__ __forceinline__ void rh_up(RHeap& h, int j, float xd, uint32_t xi) {
+    while (j > 0) {
+        const int p = (j - 1) / 2;
+        const float pd = rl_f(h.d, p);
+        if (!(xd < pd)) break;
+        rh_set(h, j, pd, rl_u(h.id, p));
+        j = p;
+    }
+    rh_set(h, j, xd, xi);
+}
+// element (xd, xi) at slot i, moved down within [0, n) (heap.go down)
+__device__ __forceinline__ void rh_down(RHeap& h, int i, int n, float xd, uint32_t xi) {
+    for (;;) {
+        const int j1 = 2 * i + 1;
+        if (j1 >= n) break;
+        int j = j1;
+        float jd = rl_f(h.d, j1);
+        if (j1 + 1 < n) {
+            const float d2 = rl_f(h.d, j1 + 1);
+            if (d2 < jd) {
+                j = j1 + 1;
+                jd = d2;
+            }
+        }
+        if (!(jd < xd)) break;
+        rh_set(h, i, jd, rl_u(h.id, j));
+        i = j;
+    }
+    rh_set(h, i, xd, xi);
+}
+
+// one interface over both heaps (compat_layer is written against it)
+__device__ __forceinline__ void hp_push(GHeap& h, float d, uint32_t id) { gh_push(h, d, id); }
+__device__ __forceinline__ void hp_pop(GHeap& h, float& d, uint32_t& id) { gh_pop(h, d, id); }
+__device__ __forceinline__ void hp_poplast(GHeap& h) { h.n--; }
+__device__ __forceinline__ float hp_d(const GHeap& h, int i) { return h.d[i]; }
+__device__ __forceinline__ uint32_t hp_id(const GHeap& h, int i) { return h.id[i]; }
+__device__ __forceinline__ void hp_store(const GHeap&, float*, uint32_t*) {}  // already in place
+__device__ __forceinline__ void hp_push(RHeap& h, float d, uint32_t id) {
+    rh_up(h, h.n, d, id);
+    h.n++;
+}
+__device__ __forceinline__ void hp_pop(RHeap& h, float& d, uint32_t& id) {
+    const int n1 = h.n - 1;
+    d = rl_f(h.d, 0);
+    id = rl_u(h.id, 0);
+    if (n1 > 0) rh_down(h, 0, n1, rl_f(h.d, n1), rl_u(h.id, n1));
+    h.n = n1;
+}
+__device__ __forceinline__ void hp_poplast(RHeap& h) { h.n--; }
+__device__ __forceinline__ float hp_d(const RHeap& h, int i) { return rl_f(h.d, i); }
+__device__ __forceinline__ uint32_t hp_id(const RHeap& h, int i) { return rl_u(h.id, i); }
+__device__ __forceinline__ void hp_store(const RHeap& h, float* d, uint32_t* id) {
+    if (lane_id() < h.n) {
+        d[lane_id()] = h.d;
+        id[lane_id()] = h.id;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Ascending (key, id) order of lanes 0..cnt-1 (cnt uniform, <= 64; lanes >= cnt
 // keep their values): each lane counts the entries before it -- cnt uniform
@@ -614,5 +689,26 @@ __device__ __forceinline__ void rank_sort(int64_t& key, uint32_t& id, int cnt) {
     key = (int64_t)(((uint64_t)nhi << 32) | nlo);
 }
 
+// Tools-only cycle accounting of the compat walk (tools/Makefile.build with
+// BFLAGS=-DMH_COMPAT_PROF): per-phase clock deltas summed in LDS by the walking
+// wave and printed by the kernel at exit.  Compiled out of the product.
+#ifdef MH_COMPAT_PROF
+__shared__ unsigned long long mh_cprof[24];
+#define CPROF_T(v) long long v = clock64()
+#define CPROF_ADD(v, s)                                                                 \
+    do {                                                                                \
+        const long long n_ = clock64();                                                 \
+        if (lane_id() == 0) atomicAdd(&mh_cprof[s], (unsigned long long)(n_ - (v)));    \
+        v = n_;                                                                         \
+    } while (0)
+#define CPROF_CNT(s, x)                                                                 \
+    do {                                                                                \
+        if (lane_id() == 0) atomicAdd(&mh_cprof[s], (unsigned long long)(x));           \
+    } while (0)
+#else
+#define CPROF_T(v)
+#define CPROF_ADD(v, s)
+#define CPROF_CNT(s, x)
+#endif
 
 }  // namespace mh

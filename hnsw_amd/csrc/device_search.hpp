@@ -250,6 +250,19 @@ struct WaveEval {
             eval_list<C, G>(g, q, qn, cid, c, metric, sink);
         }
     }
+    // rows list[0, cnt): distance e into outd[e], the row into outi[e]
+    template <class C, int G>
+    __device__ __forceinline__ void score(const GraphDev& g, const QReg<C>& q, float qn, int cnt, int metric,
+                                          float* outd, uint32_t* outi) const {
+        int t = 0;
+        run_list<C, G>(g, q, qn, cnt, metric, [&](float d, uint32_t u) {
+            if (lane_id() == 0) {
+                outd[t] = d;
+                outi[t] = u;
+            }
+            ++t;
+        });
+    }
     __device__ __forceinline__ void sync() const { __syncthreads(); }
 };
 
@@ -391,28 +404,30 @@ struct CompatSmem {
     uint32_t* ri;  // result heap [k+2]
 };
 
-template <class C, int G, bool COH = false, class Ev = WaveEval>
-__device__ __forceinline__ int compat_layer(const GraphDev& g, int layer, uint32_t entry, int k, int ef, const QReg<C>& q, float qn,
-                            CompatSmem& S, WaveStats& st, int& err, const Ev& ev = Ev()) {
+// HP: GHeap (LDS arrays S.cd/S.ci and S.rd/S.ri) or RHeap (one slot per lane,
+// when ef + 1 and k + 1 fit the wave); the result heap ends in S.rd / S.ri
+// either way, in heap order.
+template <class C, int G, bool COH, class Ev, class HP>
+__device__ __forceinline__ int compat_layer_h(const GraphDev& g, int layer, uint32_t entry, int k, int ef,
+                                              const QReg<C>& q, float qn, CompatSmem& S, WaveStats& st, int& err,
+                                              const Ev& ev, HP cand, HP res) {
     const int lane = lane_id();
-    if (entry == EMPTY_ID) return 0;
     const int vsize = 1 << S.vlog2, vmask = vsize - 1;
     vis_clear(S.vis, vsize);
     ev.sync();
-    GHeap cand{S.cd, S.ci, 0}, res{S.rd, S.ri, 0};
     float d0 = 0.f;
     ev.template run<C, G>(g, q, qn, entry, 1, g.metric, [&](float d, uint32_t) { d0 = d; });  // graph.go:112
     st.E += 1;
     if (lane == 0) vis_probe(S.vis, vmask, kid_of(g, entry));  // graph.go:123 visited[n.Key]
-    gh_push(cand, d0, entry);                        // graph.go:109-114
-    gh_push(res, cand.d[0], cand.id[0]);             // graph.go:122
+    hp_push(cand, d0, entry);                          // graph.go:109-114
+    hp_push(res, hp_d(cand, 0), hp_id(cand, 0));       // graph.go:122
     const int32_t* degp = g.layers[layer].deg;
     const int32_t* adjp = g.layers[layer].adj;
     const int capl = g.layers[layer].cap;
     while (cand.n > 0) {
         float cdist;
         uint32_t cur;
-        gh_pop(cand, cdist, cur);  // graph.go:127
+        hp_pop(cand, cdist, cur);  // graph.go:127
         bool improved = false;
         const uint32_t cg = guard_id(g, cur);
         // the row is loaded with its degree (one round trip, entries past deg ignored)
@@ -435,19 +450,30 @@ __device__ __forceinline__ int compat_layer(const GraphDev& g, int layer, uint32
         const uint32_t cid = compact(nb, pr == 1, cnt);
         st.E += cnt;
         ev.template run<C, G>(g, q, qn, cid, cnt, g.metric, [&](float dist, uint32_t u) {  // graph.go:146-159
-            improved = improved || (res.n > 0 && dist < res.d[0]);
+            improved = improved || (res.n > 0 && dist < hp_d(res, 0));
             if (res.n < k) {
-                gh_push(res, dist, u);
-            } else if (dist < res.d[res.n - 1]) {
-                gh_poplast(res);
-                gh_push(res, dist, u);
+                hp_push(res, dist, u);
+            } else if (dist < hp_d(res, res.n - 1)) {
+                hp_poplast(res);
+                hp_push(res, dist, u);
             }
-            gh_push(cand, dist, u);
-            if (cand.n > ef) gh_poplast(cand);
+            hp_push(cand, dist, u);
+            if (cand.n > ef) hp_poplast(cand);
         });
         if (!improved && res.n >= k) break;  // graph.go:164-166
     }
+    hp_store(res, S.rd, S.ri);
     return res.n;
+}
+
+template <class C, int G, bool COH = false, class Ev = WaveEval>
+__device__ __forceinline__ int compat_layer(const GraphDev& g, int layer, uint32_t entry, int k, int ef, const QReg<C>& q, float qn,
+                            CompatSmem& S, WaveStats& st, int& err, const Ev& ev = Ev()) {
+    if (entry == EMPTY_ID) return 0;
+    if (ef < 64 && k < 64)  // at most ef + 1 / k + 1 entries at a time
+        return compat_layer_h<C, G, COH>(g, layer, entry, k, ef, q, qn, S, st, err, ev, RHeap{}, RHeap{});
+    return compat_layer_h<C, G, COH>(g, layer, entry, k, ef, q, qn, S, st, err, ev, GHeap{S.cd, S.ci, 0},
+                                     GHeap{S.rd, S.ri, 0});
 }
 
 }  // namespace mh
