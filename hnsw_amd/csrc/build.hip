@@ -482,10 +482,13 @@ struct MwHdr {
 };
 constexpr int MW_EVAL = 0, MW_EXIT = 1;
 
+// Everything exchanged here lives in LDS (workers read only immutable rows from
+// HBM), so the fences order LDS alone: the master's graph stores are not waited
+// for at every hand-off.
 __device__ __forceinline__ void mw_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 // rows [0, cnt) of ids, wave w of nw: canonical distances into dist[]
@@ -566,10 +569,7 @@ struct MwEval {
         }
     }
     // the master's own lanes only (workers never touch graph state)
-    __device__ __forceinline__ void sync() const {
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-    }
+    __device__ __forceinline__ void sync() const { wave_sync(); }
 };
 
 template <class C, int G>

@@ -228,6 +228,16 @@ struct WaveStats {
     unsigned long long S = 0, F = 0;  // rows screened on the fp16 copy / rows evaluated in f32
 };
 
+// Orders the lanes of ONE wave (compiler ordering only: a wave's vector memory
+// and LDS operations are performed in issue order, so a lane's load after
+// another lane's store to the same address sees it -- no waitcnt for the
+// store's acknowledgement).  The sequential walks mutate graph state from a
+// single wave; nothing else reads it while they run.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // How the sequential (compat) walks evaluate distances and order their own
 // lanes.  WaveEval: everything on the calling wave (a 64-thread workgroup, so
 // __syncthreads only orders this wave).  The multi-wave build evaluator
@@ -263,7 +273,7 @@ struct WaveEval {
             ++t;
         });
     }
-    __device__ __forceinline__ void sync() const { __syncthreads(); }
+    __device__ __forceinline__ void sync() const { wave_sync(); }
 };
 
 // ---------------------------------------------------------------------------
