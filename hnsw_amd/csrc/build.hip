@@ -50,7 +50,7 @@ __device__ __forceinline__ void list_remove(const GraphDev& g, int l, uint32_t n
     const int capl = g.layers[l].cap;
     int32_t* row = g.layers[l].adj + (size_t)n * capl;
     const int32_t rv = lane < capl ? ld_i32<true>(row + lane) : -1;
-    const int d = ld_i32<true>(g.layers[l].deg + n);
+    const int d = uni(ld_i32<true>(g.layers[l].deg + n));  // uniform: scalar loop bounds
     if (d <= 0) return;
     // delete(n.neighbors, v.Key): the entry of v's key, whichever row it holds
     const bool hit = lane < d && kid_of(g, guard_id(g, (uint32_t)rv)) == kid_of(g, v);
@@ -76,20 +76,21 @@ __device__ __forceinline__ int list_append(const GraphDev& g, int l, uint32_t n,
     const int capl = g.layers[l].cap;
     int32_t* row = g.layers[l].adj + (size_t)n * capl;
     const int32_t rv = lane < capl ? ld_i32<true>(row + lane) : -1;
-    int d = ld_i32<true>(g.layers[l].deg + n);
+    int d = uni(ld_i32<true>(g.layers[l].deg + n));
     if (d < 0) d = 0;  // graph.go:46-48 allocate the map
     const bool pres = lane < d && kid_of(g, guard_id(g, (uint32_t)rv)) == kid_of(g, nw);
     const unsigned long long pm = __ballot(pres);
     const bool present = pm != 0;
     const int pos = present ? __ffsll((long long)pm) - 1 : d;
+    const int nd = uni(present ? d : d + 1);  // (computed outside the lane-0 stores: stays scalar)
     ev.sync();
     if (lane == 0) {
         st_i32(row + pos, (int32_t)nw);
-        st_i32(g.layers[l].deg + n, present ? d : d + 1);
+        st_i32(g.layers[l].deg + n, nd);
     }
     ev.sync();
     if (rowout) *rowout = lane == pos ? (int32_t)nw : rv;
-    return present ? d : d + 1;
+    return nd;
 }
 
 // graph.go:172-219 when the outcome does not depend on the walk order.  With
@@ -206,7 +207,7 @@ __device__ __forceinline__ void replenish(const GraphDev& g, int l, uint32_t n, 
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
     const int32_t rv = lane < capl ? ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane) : -1;
-    int dn = ld_i32<true>(g.layers[l].deg + n);
+    int dn = uni(ld_i32<true>(g.layers[l].deg + n));
     if (dn < 0) dn = 0;
     if (dn >= m) return;
     CPROF_T(tr);
@@ -349,7 +350,7 @@ __device__ __forceinline__ void replenish(const GraphDev& g, int l, uint32_t n, 
     };
     if (!fast) replay();
     for (;;) {
-        int cur = ld_i32<true>(g.layers[l].deg + n);
+        int cur = uni(ld_i32<true>(g.layers[l].deg + n));
         if (cur < 0) cur = 0;
         if (cur >= m) break;
         uint32_t best;
@@ -398,14 +399,16 @@ __device__ __forceinline__ void add_neighbor(const GraphDev& g, int l, uint32_t 
     const int lane = lane_id();
     int32_t rv;
     CPROF_T(ta);
+    // n's row goes out with the append's loads (one round trip for both; most
+    // appends overflow the row and evict)
+    QReg<C> q;
+    load_query(q, g.vecs + (size_t)n * g.pitch);
+    const float qn = g.norms[n];
     const int d = list_append(g, l, n, nw, ev, &rv);
     CPROF_ADD(ta, 1);
     if (d <= m) return;
     CPROF_CNT(17, 1);
     uint32_t nb = lane < d ? guard_id(g, (uint32_t)rv) : 0xFFFFFFFFu;
-    QReg<C> q;
-    load_query(q, g.vecs + (size_t)n * g.pitch);
-    const float qn = g.norms[n];
     float worst_d = -__int_as_float(0x7f800000);
     uint32_t worst = EMPTY_ID;
     st.E += d;
@@ -440,7 +443,7 @@ __device__ __forceinline__ void add_neighbor(const GraphDev& g, int l, uint32_t 
     CPROF_ADD(ta, 2);
     if (worst == EMPTY_ID) return;
     list_remove<C, G>(g, l, n, worst, ev);  // graph.go:74
-    if (ld_i32<true>(g.layers[l].deg + worst) >= 0) list_remove<C, G>(g, l, worst, n, ev);  // graph.go:76-78
+    if (uni(ld_i32<true>(g.layers[l].deg + worst)) >= 0) list_remove<C, G>(g, l, worst, n, ev);  // graph.go:76-78
     CPROF_ADD(ta, 3);
     replenish<C, G>(g, l, worst, m, S, st, err, ev);  // graph.go:79
     CPROF_ADD(ta, 4);
@@ -454,7 +457,7 @@ __device__ __forceinline__ void isolate(const GraphDev& g, int l, uint32_t n, in
                         const Ev& ev) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
-    const int dn = min(ld_i32<true>(g.layers[l].deg + n), capl);
+    const int dn = min(uni(ld_i32<true>(g.layers[l].deg + n)), capl);
     if (dn < 0) return;  // nil neighbour map
     uint32_t mine = 0xFFFFFFFFu;
     int64_t key = INT64_MAX;
@@ -465,7 +468,7 @@ __device__ __forceinline__ void isolate(const GraphDev& g, int l, uint32_t n, in
     rank_sort(key, mine, dn);
     for (int j = 0; j < dn; ++j) {
         const uint32_t x = rl_u(mine, j);
-        if (ld_i32<true>(g.layers[l].deg + x) < 0) continue;  // neighbor.neighbors == nil
+        if (uni(ld_i32<true>(g.layers[l].deg + x)) < 0) continue;  // neighbor.neighbors == nil
         list_remove<C, G>(g, l, x, n, ev);                     // graph.go:232 delete(neighbor.neighbors, n.Key)
         replenish<C, G>(g, l, x, m, S, st, err, ev);           // graph.go:232
     }
@@ -584,6 +587,19 @@ __device__ __forceinline__ void mw_worker(const GraphDev& g, const MwEval<C>& ev
         mw_share<C, G>(g, q, ev.hdr->qn, ev.list, ev.dist, ev.hdr->cnt, ev.hdr->metric, w, ev.nw);
         mw_barrier();
     }
+}
+
+// The sequential kernels re-read a layer's descriptor (row cap, adjacency and
+// degree arrays) at every step of the walk; from HBM each read is one more
+// dependent round trip (vector loads: the walk's own stores could alias the
+// table, so the scalar cache is out).  A copy in LDS makes it a few dozen
+// cycles.  Returns the graph view to walk with.
+__device__ __forceinline__ GraphDev lds_layers(const GraphDev& g, LayerDev* tab) {
+    for (int i = threadIdx.x; i < g.nlayers; i += blockDim.x) tab[i] = g.layers[i];
+    __syncthreads();
+    GraphDev v = g;
+    v.layers = tab;
+    return v;
 }
 
 // LDS of the compat walks: visited set, compat heaps, replenish heap + staging
@@ -714,6 +730,8 @@ __device__ __forceinline__ void compat_inserts(const CompatBuildArgs& a, BuildSm
 template <class C, int G>
 __global__ __launch_bounds__(64) void k_build_compat(CompatBuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    __shared__ LayerDev ltab[MH_MAXL];
+    a.g = lds_layers(a.g, ltab);
     BuildSmem S;
     uint32_t* p = build_smem(smem, a.vis_log2, a.M, a.ef, S);
     WaveEval ev;
@@ -733,6 +751,8 @@ __global__ __launch_bounds__(64) void k_build_compat(CompatBuildArgs a) {
 template <class C, int G, int NW>
 __global__ __launch_bounds__(64 * NW) void k_build_compat_mw(CompatBuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    __shared__ LayerDev ltab[MH_MAXL];
+    a.g = lds_layers(a.g, ltab);
     BuildSmem S;
     uint32_t* p = build_smem(smem, a.vis_log2, a.M, a.ef, S);
     MwEval<C> ev;
@@ -776,6 +796,9 @@ __global__ __launch_bounds__(64 * NW) void k_build_compat_mw(CompatBuildArgs a) 
 }
 
 constexpr int MW_WAVES = 8;
+// dynamic LDS a sequential kernel may ask for: 160 KiB less its static layer
+// table (and the tools-only counters)
+constexpr size_t CW_LDS_MAX = 160 * 1024 - MH_MAXL * sizeof(LayerDev) - 256;
 
 template <class C, int G>
 static int launch_build_compat_t(const CompatBuildArgs& a, int waves, hipStream_t s) {
@@ -783,11 +806,11 @@ static int launch_build_compat_t(const CompatBuildArgs& a, int waves, hipStream_
     const int hcap = (a.M + 1) * (a.M + 1) + 2;
     if (waves <= 1 || C::VPL >= 16) {  // 4096-d: the walking wave alone (register budget)
         const size_t lds = (base + hcap) * 4;
-        if (lds > 160 * 1024) return -2;
+        if (lds > CW_LDS_MAX) return -2;
         hipLaunchKernelGGL((k_build_compat<C, G>), dim3(1), dim3(64), lds, s, a);
     } else {
         const size_t lds = (base + 3 + 4 + 4 * 64 * (size_t)C::VPL + 2 * (size_t)hcap) * 4;
-        if (lds > 160 * 1024) return -2;
+        if (lds > CW_LDS_MAX) return -2;
         hipLaunchKernelGGL((k_build_compat_mw<C, G, MW_WAVES>), dim3(1), dim3(64 * MW_WAVES), lds, s, a);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1206,6 +1229,8 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
 template <class C, int G>
 __global__ __launch_bounds__(64) void k_delete_compat(DeleteArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    __shared__ LayerDev ltab[MH_MAXL];
+    a.g = lds_layers(a.g, ltab);
     const int lane = lane_id();
     BuildSmem S;
     uint32_t* p = build_smem(smem, a.vis_log2, a.M, 0, S);
@@ -1216,7 +1241,7 @@ __global__ __launch_bounds__(64) void k_delete_compat(DeleteArgs a) {
     for (int64_t i = 0; i < a.nids; ++i) {
         const uint32_t id = a.ids[i];
         const int l = (int)a.lay[i];
-        if (ld_i32<true>(a.g.layers[l].deg + id) == -2) continue;
+        if (uni(ld_i32<true>(a.g.layers[l].deg + id)) == -2) continue;
         isolate<C, G>(a.g, l, id, a.M, S, st, err, ev);
     }
     if (lane == 0) {
@@ -1349,7 +1374,7 @@ __global__ __launch_bounds__(64) void k_delete_repair(DeleteArgs a) {
 template <class C, int G>
 static int launch_delete_compat_t(const DeleteArgs& a, hipStream_t s) {
     const size_t words = build_smem_words(a.vis_log2, a.M, 0) + (size_t)((a.M + 1) * (a.M + 1) + 2);
-    if (words * 4 > 160 * 1024) return -2;
+    if (words * 4 > CW_LDS_MAX) return -2;
     hipLaunchKernelGGL((k_delete_compat<C, G>), dim3(1), dim3(64), words * 4, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

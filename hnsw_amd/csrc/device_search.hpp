@@ -20,15 +20,20 @@ namespace mh {
 // the vector L1 (workgroup scope would add sc0, sending every dependent load
 // of the walk to L2); the wave's own program order and __syncthreads /
 // ev.sync() order its lanes.
+// The pointers come from the layer table, so the compiler cannot tell their
+// address space: the casts make these global (not flat) operations, which do
+// not count against lgkmcnt (a flat load holds up every LDS wait behind it).
+typedef __attribute__((address_space(1))) int32_t g_i32;
 template <bool COH>
 __device__ __forceinline__ int32_t ld_i32(const int32_t* p) {
+    const g_i32* gp = (const g_i32*)p;
     if constexpr (COH)
-        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        return __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     else
-        return *p;
+        return *gp;
 }
 __device__ __forceinline__ void st_i32(int32_t* p, int32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_store((g_i32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
 // `layers[l].nodes[*elevator]` (graph.go:497, 574): the layer's node of the
@@ -326,7 +331,7 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
                 st.X += 1;
                 const uint32_t cg = guard_id(g, cur[w]);
                 rowv[w] = lane < capl ? ld_i32<COH>(adjp + (size_t)cg * capl + lane) : -1;
-                deg[w] = min(ld_i32<COH>(degp + cg), capl);
+                deg[w] = min(uni(ld_i32<COH>(degp + cg)), capl);
             }
         }
         uint32_t cids[XW];
@@ -442,7 +447,7 @@ __device__ __forceinline__ int compat_layer_h(const GraphDev& g, int layer, uint
         const uint32_t cg = guard_id(g, cur);
         // the row is loaded with its degree (one round trip, entries past deg ignored)
         const int32_t rowv = lane < capl ? ld_i32<COH>(adjp + (size_t)cg * capl + lane) : -1;
-        const int deg = min(ld_i32<COH>(degp + cg), capl);
+        const int deg = min(uni(ld_i32<COH>(degp + cg)), capl);
         if (deg < 0) continue;  // graph.go:131-133 (nil neighbor map)
         st.X += 1;
         const bool have = lane < deg;
@@ -459,6 +464,7 @@ __device__ __forceinline__ int compat_layer_h(const GraphDev& g, int layer, uint
         int cnt;
         const uint32_t cid = compact(nb, pr == 1, cnt);
         st.E += cnt;
+        CPROF_T(tq);
         ev.template run<C, G>(g, q, qn, cid, cnt, g.metric, [&](float dist, uint32_t u) {  // graph.go:146-159
             improved = improved || (res.n > 0 && dist < hp_d(res, 0));
             if (res.n < k) {
@@ -470,6 +476,8 @@ __device__ __forceinline__ int compat_layer_h(const GraphDev& g, int layer, uint
             hp_push(cand, dist, u);
             if (cand.n > ef) hp_poplast(cand);
         });
+        CPROF_ADD(tq, 22);
+        CPROF_CNT(23, cnt);
         if (!improved && res.n >= k) break;  // graph.go:164-166
     }
     hp_store(res, S.rd, S.ri);
