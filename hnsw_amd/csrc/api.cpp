@@ -76,6 +76,7 @@ struct mhnsw_index {
     int exact_tile = 0;       // GEMM variant (exact.hip: launch_split_scores, launch_h1)
     int compat_waves = 8;     // compat insert: waves scoring each distance batch (1 = the walking wave alone)
     int upper_ef = 1;         // beam search: upper-layer descent width
+    int64_t beam_mw_max_b = 512;  // beam search: batches up to this size run one workgroup of 4 waves per query
     int screen = 1;           // beam search / batched insert fp16 screening copy (results unchanged)
     int fuse_descent = 1;     // batched insert: all greedy descents of a batch in one launch (same graph)
     int time_build = 0;       // batched insert: time its search kernels with HIP events (stats [12])
@@ -1537,6 +1538,7 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         a.vis_log2 = h->vis_log2;
         a.vis_n = beam_vis_entries(h);
         a.upper_ef = h->upper_ef;
+        a.mw_max_b = h->beam_mw_max_b;
         if (mode == MHNSW_MODE_BEAM) {
             if (std::max(ef, k) > 512) return fail(h, MHNSW_EUNSUPPORTED, "beam mode supports max(ef,k) <= 512");
             if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
@@ -1782,6 +1784,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
 #endif
         if (!ok) return fail(h, MHNSW_EINVAL, "exact_tile must be 0-3, 5 or 34");
         h->exact_tile = (int)v;
+    } else if (n == "beam_mw_max_b") {
+        if (v < 0) return fail(h, MHNSW_EINVAL, "beam_mw_max_b must be >= 0");
+        h->beam_mw_max_b = v;
     } else if (n == "upper_ef") {
         if (v < 1 || v > 64) return fail(h, MHNSW_EINVAL, "upper_ef must be in [1, 64]");
         h->upper_ef = (int)v;
@@ -1849,6 +1854,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "exact_tile") *v = h->exact_tile;
     else if (n == "compat_waves") *v = h->compat_waves;
     else if (n == "upper_ef") *v = h->upper_ef;
+    else if (n == "beam_mw_max_b") *v = h->beam_mw_max_b;
     else if (n == "screen") *v = h->screen;
     else if (n == "fuse_descent") *v = h->fuse_descent;
     else if (n == "time_build") *v = h->time_build;

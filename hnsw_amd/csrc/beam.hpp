@@ -28,16 +28,12 @@ int launch_beam_cfg(const SearchArgs& a, hipStream_t s);
 // ---------------------------------------------------------------------------
 // batched search: one wave per query
 // ---------------------------------------------------------------------------
-template <class C, int R, int G, bool SCREEN>
-__global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const int64_t b = blockIdx.x;
-    if (b >= a.B) return;
+// One query b: greedy descent, the layer-0 beam, and its first k live entries
+// into the outputs.  BEv scores each batch of candidates (beam_layer).
+template <class C, int R, int G, bool SCREEN, class BEv>
+__device__ __forceinline__ void beam_query(const SearchArgs& a, int64_t b, const QReg<C>& q, float qn, uint32_t* smem,
+                                           WaveStats& st, const BEv& bev) {
     const int lane = lane_id();
-    QReg<C> q;
-    load_query(q, a.q + (size_t)b * C::PITCH);
-    const float qn = query_norm(q);
-    WaveStats st;
     uint32_t ep = a.entry;
     {
         BList<1> L1;
@@ -47,7 +43,7 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
                 if (e < 0) continue;
                 ep = (uint32_t)e;
             }
-            beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, a.upper_ef, q, qn, L1, smem, a.vis_n, st);
+            beam_layer<C, 1, G, false, SCREEN, 1>(a.g, l, ep, a.upper_ef, q, qn, L1, smem, a.vis_n, st, bev);
             float d;
             uint32_t id;
             bl_at(L1, 0, d, id);
@@ -57,7 +53,7 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
     BList<R> L;
     const int efl = a.ef > a.k ? a.ef : a.k;
     if (a.g.layers[0].deg[ep] == -2) ep = (uint32_t)a.layer_entry[0];
-    beam_layer<C, R, G, false, SCREEN>(a.g, 0, ep, efl, q, qn, L, smem, a.vis_n, st);
+    beam_layer<C, R, G, false, SCREEN, 1>(a.g, 0, ep, efl, q, qn, L, smem, a.vis_n, st, bev);
     // compact the sorted list into the first k live entries (deleted rows
     // route the search but are never returned)
     int nvalid = 0;
@@ -81,8 +77,11 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
         a.out_dist[b * a.k + i] = __int_as_float(0x7f800000);
         if (a.out_ids) a.out_ids[b * a.k + i] = -1;
     }
-    if (lane == 0) {
-        a.out_n[b] = nvalid;
+    if (lane == 0) a.out_n[b] = nvalid;
+}
+
+__device__ __forceinline__ void beam_stats(const SearchArgs& a, const WaveStats& st) {
+    if (lane_id() == 0) {
         atomicAdd(&a.stats[0], st.E);
         atomicAdd(&a.stats[1], st.X);
         if (st.resets) atomicAdd(&a.stats[2], st.resets);
@@ -91,9 +90,145 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
     }
 }
 
+template <class C, int R, int G, bool SCREEN>
+__global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int64_t b = blockIdx.x;
+    if (b >= a.B) return;
+    QReg<C> q;
+    load_query(q, a.q + (size_t)b * C::PITCH);
+    const float qn = query_norm(q);
+    WaveStats st;
+    beam_query<C, R, G, SCREEN>(a, b, q, qn, smem, st, WaveBatch());
+    beam_stats(a, st);
+}
+
+// ---------------------------------------------------------------------------
+// small batches (the reference's ParallelSearch, graph.go:631-790: one query's
+// neighbour distances fanned out over workers): one workgroup of BMW_WAVES
+// waves per query.  Wave 0 runs the list, the visited set and the expansions
+// exactly as k_search_beam; each batch of new candidates is split over the
+// waves (screen + f32 on each wave's rows, in one round trip instead of one
+// per 16 rows), and the survivors come back to wave 0's list.  The list is the
+// best ef of everything inserted whatever the insertion order, so the results
+// are k_search_beam's bit for bit (test_gpu_parity.py: batches below and above
+// BMW_MAX_B compared).
+// ---------------------------------------------------------------------------
+constexpr int BMW_WAVES = 4;
+constexpr int BMW_SCORE = 0, BMW_EXIT = 1;
+struct BmwShare {
+    int cmd, cnt;
+    float wd;
+    int pad_;
+    uint32_t list[64];
+    int scnt[BMW_WAVES];
+    float sd[BMW_WAVES * 64];
+    uint32_t si[BMW_WAVES * 64];
+};
+
+// everything handed between the waves is in LDS (rows and norms are only read)
+__device__ __forceinline__ void bmw_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// wave w's rows of the posted batch, [w*ch, min(cnt, (w+1)*ch)): screened
+// against the posted worst, survivors (f32 distance, id) into sd / si
+template <class C, int G, bool SCREEN>
+__device__ __forceinline__ int bmw_share(const GraphDev& g, const QReg<C>& q, float qn, BmwShare* sh, int w,
+                                         bool screen, float margin, unsigned long long& s16) {
+    const int lane = lane_id();
+    const int cnt = uni(sh->cnt);
+    const float wd = __int_as_float(uni(__float_as_int(sh->wd)));
+    const int ch = (cnt + BMW_WAVES - 1) / BMW_WAVES;
+    const int t0 = w * ch;
+    const int c = min(cnt - t0, ch);
+    int k = 0, f = 0;
+    if (c > 0) {
+        const uint32_t cid = lane < c ? sh->list[t0 + lane] : 0u;
+        auto sink = [&](float d, uint32_t u) {
+            if (lane == 0) {
+                sh->sd[w * 64 + k] = d;
+                sh->si[w * 64 + k] = u;
+            }
+            ++k;
+        };
+        f = WaveBatch().template score<C, G, SCREEN>(g, q, qn, cid, c, wd, screen, margin, sink, s16);
+    }
+    if (lane == 0) sh->scnt[w] = k;
+    return f;
+}
+
+struct MwBatch {
+    BmwShare* sh;
+    template <class C, int G, bool SCREEN, class Sink>
+    __device__ __forceinline__ int score(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int cnt,
+                                         float wd, bool screen, float margin, Sink&& sink,
+                                         unsigned long long& s16) const {
+        const int lane = lane_id();
+        if (lane < cnt) sh->list[lane] = cid;
+        if (lane == 0) {
+            sh->cmd = BMW_SCORE;
+            sh->cnt = cnt;
+            sh->wd = wd;
+        }
+        bmw_barrier();  // post
+        const int f = bmw_share<C, G, SCREEN>(g, q, qn, sh, 0, screen, margin, s16);
+        bmw_barrier();  // collect
+#pragma unroll
+        for (int w = 0; w < BMW_WAVES; ++w) {
+            const int n = uni(sh->scnt[w]);
+            const float dv = lane < n ? sh->sd[w * 64 + lane] : 0.f;
+            const uint32_t iv = lane < n ? sh->si[w * 64 + lane] : 0u;
+            for (int t = 0; t < n; ++t) sink(rl_f(dv, t), rl_u(iv, t));
+        }
+        return f;  // this wave's rows (the others count theirs)
+    }
+};
+
+template <class C, int R, int G, bool SCREEN>
+__global__ __launch_bounds__(64 * BMW_WAVES) void k_search_beam_mw(SearchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    __shared__ BmwShare sh;
+    const int64_t b = blockIdx.x;
+    if (b >= a.B) return;  // (whole workgroup)
+    const int wave = threadIdx.x >> 6;
+    QReg<C> q;
+    load_query(q, a.q + (size_t)b * C::PITCH);
+    const float qn = query_norm(q);
+    WaveStats st;
+    if (wave == 0) {
+        beam_query<C, R, G, SCREEN>(a, b, q, qn, smem, st, MwBatch{&sh});
+        if (lane_id() == 0) sh.cmd = BMW_EXIT;
+        bmw_barrier();  // releases the other waves
+    } else {
+        const bool screen = SCREEN && h16_query_ok(qn);
+        float margin = 0.f;
+        if constexpr (SCREEN) {
+            const float e = a.g.h16err ? *a.g.h16err : 0.00048828125f;
+            margin = a.g.metric == EUCLIDEAN ? h16_margin_l2(e) : h16_margin_cos(e);
+        }
+        for (;;) {
+            bmw_barrier();
+            if (sh.cmd == BMW_EXIT) break;
+            st.F += bmw_share<C, G, SCREEN>(a.g, q, qn, &sh, wave, screen, margin, st.S);
+            bmw_barrier();
+        }
+    }
+    beam_stats(a, st);
+}
+
 template <class C, int R, int G>
 static int launch_beam_t(const SearchArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 * (size_t)a.vis_n;
+    if (R <= 2 && a.B <= a.mw_max_b) {  // small batch: a workgroup per query
+        if (a.g.h16)
+            hipLaunchKernelGGL((k_search_beam_mw<C, R, G, true>), dim3((unsigned)a.B), dim3(64 * BMW_WAVES), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_search_beam_mw<C, R, G, false>), dim3((unsigned)a.B), dim3(64 * BMW_WAVES), lds, s, a);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (a.g.h16)
         hipLaunchKernelGGL((k_search_beam<C, R, G, true>), dim3((unsigned)a.B), dim3(64), lds, s, a);
     else

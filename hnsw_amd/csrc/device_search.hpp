@@ -281,6 +281,22 @@ struct WaveEval {
     __device__ __forceinline__ void sync() const { wave_sync(); }
 };
 
+// How beam_layer scores one batch of new candidates (ids in lanes 0..cnt-1 of
+// cid) and hands the survivors to its sink: WaveBatch does it on the calling
+// wave; the multi-wave single-query kernel (beam.hpp MwBatch) spreads the rows
+// over the workgroup's waves.  Returns the rows evaluated in f32.
+struct WaveBatch {
+    template <class C, int G, bool SCREEN, class Sink>
+    __device__ __forceinline__ int score(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int cnt,
+                                         float wd, bool screen, float margin, Sink&& sink,
+                                         unsigned long long& s16) const {
+        if (SCREEN && screen && wd < __int_as_float(0x7f800000))
+            return eval_screened<C, G>(g, q, qn, cid, cnt, g.metric, wd, sink, s16, margin);
+        eval_list<C, G>(g, q, qn, cid, cnt, g.metric, sink);
+        return cnt;
+    }
+};
+
 // ---------------------------------------------------------------------------
 // beam: sorted list of <= ef entries; stop when every entry is expanded
 // ---------------------------------------------------------------------------
@@ -290,14 +306,14 @@ struct WaveEval {
 // expanded together -- their adjacency rows fetched in one round trip and
 // their new neighbours evaluated as one batch -- which halves the dependent
 // round trips of a search whose expansions yield few new candidates.
-template <class C, int R, int G, bool COH = false, bool SCREEN = false, int XW = 1>
+template <class C, int R, int G, bool COH = false, bool SCREEN = false, int XW = 1, class BEv = WaveBatch>
 __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_t entry, int ef, const QReg<C>& q, float qn,
-                           BList<R>& L, uint32_t* vis, int vsize, WaveStats& st) {
+                           BList<R>& L, uint32_t* vis, int vsize, WaveStats& st, const BEv& bev = BEv()) {
     const int lane = lane_id();
     bl_init(L);
     if (entry == EMPTY_ID) return;
     vis_clear(vis, vsize);
-    __syncthreads();
+    wave_sync();  // (the list and the visited set belong to this wave alone)
     if (lane == 0) vis_probe_n(vis, (uint32_t)vsize, entry);
     int vcount = 1;
     eval_list<C, G>(g, q, qn, entry, 1, g.metric, [&](float d, uint32_t u) { bl_insert(L, ef, d, u); });
@@ -380,17 +396,12 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
             const uint32_t cid = cids[w];
             st.E += cnt;
             auto sink = [&](float d, uint32_t u) { bl_insert(L, ef, d, u); };
-            if (SCREEN && screen && wd < __int_as_float(0x7f800000)) {
-                st.F += eval_screened<C, G>(g, q, qn, cid, cnt, g.metric, wd, sink, st.S, margin);
-            } else {
-                st.F += cnt;
-                eval_list<C, G>(g, q, qn, cid, cnt, g.metric, sink);
-            }
+            st.F += bev.template score<C, G, SCREEN>(g, q, qn, cid, cnt, wd, screen, margin, sink, st.S);
         }
         if (vcount > (vsize >> 1) + (vsize >> 2)) {  // forget: results unchanged
-            __syncthreads();
+            wave_sync();
             vis_clear(vis, vsize);
-            __syncthreads();
+            wave_sync();
             // the list's members stay visited: they are the neighbourhood the
             // next expansions keep meeting (fewer re-evaluations)
             int seeded = 0;
@@ -400,7 +411,7 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
                 const bool ins = id != EMPTY_ID && vis_probe_n(vis, (uint32_t)vsize, id & ID_MASK) == 1;
                 seeded += __popcll(__ballot(ins));
             }
-            __syncthreads();
+            wave_sync();
             vcount = seeded;
             st.resets += 1;
         }

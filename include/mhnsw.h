@@ -92,7 +92,10 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * 5 the ring kernel's fused filter (128x256), which also runs every shape
  * k_h1_pp16 does not admit), "compat_waves" (1 or 8 waves scoring the compat insert's
  * distance batches), "upper_ef" (beam mode: upper-layer descent width, 1 =
- * greedy), "screen" (beam mode and batched insert, default 1: keep an fp16
+ * greedy), "beam_mw_max_b" (beam mode, ef and k <= 128: batches of at most this
+ * many queries run one workgroup of 4 waves per query -- the single-query
+ * latency path of ParallelSearch, graph.go:631-790; default 512, 0 = never;
+ * results are identical either way), "screen" (beam mode and batched insert, default 1: keep an fp16
  * copy of the rows; a candidate is skipped only when the copy proves the f32
  * distance rejects it, so results are unchanged);
  * "max_rows" (row capacity limit, 0 = none: an Add that would need more rows
