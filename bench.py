@@ -43,7 +43,7 @@ import hnsw_amd as H  # noqa: E402
 
 # revision of the search/build kernels the recorded PMC passes (profiles/*_pmc_*.json)
 # were taken on; a pass recorded on another revision is not attached as `traffic`
-KERNEL_REV = "r03"
+KERNEL_REV = "r04"
 from hnsw_amd.shard import engine_local_search, gather_topk, merge_topk, shard_range, sharded_search  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -90,8 +90,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline time box (0 disables)")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
     p.add_argument("--one-gpu", action="store_true", help="map every rank to cuda:0 (multi-rank rehearsal)")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03_pmc_search.json"))
-    p.add_argument("--pmc-build-json", default=os.path.join(ROOT, "profiles", "r03_pmc_build.json"))
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04_pmc_search.json"))
+    p.add_argument("--pmc-build-json", default=os.path.join(ROOT, "profiles", "r04_pmc_build.json"))
     return p.parse_args()
 
 

@@ -2,7 +2,9 @@
 kernel (MI355X_MICROARCH.md 'HBM': FETCH_SIZE reports 1/2 of the bytes of a
 wide coalesced streaming read on gfx950 -> doubled; WRITE_SIZE exact for
 16-B/lane stores).  Usage:
-  python tools/pmc_summary.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR OUT.json key=value...
+  python tools/pmc_summary.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR[@GRID] OUT.json key=value...
+(@GRID keeps only the dispatches of that grid size, e.g. the headline batch's
+launches of a kernel the same run also launches on smaller batches)
 """
 import csv
 import glob
@@ -12,12 +14,15 @@ import sys
 
 
 def per_dispatch(d, counter, kernel):
+    grid = None
+    if "@" in kernel:
+        kernel, grid = kernel.split("@")
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
             cname = r.get("Counter_Name") or r.get("Counter-Name") or ""
-            if kernel in name and cname == counter:
+            if kernel in name and cname == counter and (grid is None or r.get("Grid_Size") == grid):
                 did = r.get("Dispatch_Id") or r.get("Dispatch-Id") or str(len(vals))
                 vals[did] = vals.get(did, 0.0) + float(r.get("Counter_Value") or r.get("Counter-Value") or 0)
     return list(vals.values())
@@ -38,6 +43,7 @@ def main():
         "fetch_size_kb_raw": fk,
         "write_size_kb": wk,
         "hbm_bytes_per_launch": int(2 * fk * 1024 + wk * 1024),
+        "hbm_bytes_total": int((2 * fk * 1024 + wk * 1024) * len(f)),
         "correction": "FETCH_SIZE x2 (gfx950 wide-load half count), WRITE_SIZE x1; KB units",
     }
     for k, v in extra.items():
