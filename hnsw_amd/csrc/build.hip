@@ -44,13 +44,13 @@ struct BuildSmem {
 
 // Rows are loaded together with their degree (one round trip; entries past
 // the degree are ignored): the sequential walk is bound by dependent loads.
-template <class C, int G, class Ev>
-__device__ __forceinline__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v, const Ev& ev) {
+// list_remove_in: n's row already in registers (lane i: entry i, d entries);
+// both are updated to the row after the removal, so the next step on n (the
+// replenish after an eviction) needs no reload.
+template <class Ev>
+__device__ __forceinline__ void list_remove_in(const GraphDev& g, int l, uint32_t n, int32_t& rv, int& d, uint32_t v,
+                                               const Ev& ev) {
     const int lane = lane_id();
-    const int capl = g.layers[l].cap;
-    int32_t* row = g.layers[l].adj + (size_t)n * capl;
-    const int32_t rv = lane < capl ? ld_i32<true>(row + lane) : -1;
-    const int d = uni(ld_i32<true>(g.layers[l].deg + n));  // uniform: scalar loop bounds
     if (d <= 0) return;
     // delete(n.neighbors, v.Key): the entry of v's key, whichever row it holds
     const bool hit = lane < d && kid_of(g, guard_id(g, (uint32_t)rv)) == kid_of(g, v);
@@ -60,10 +60,20 @@ __device__ __forceinline__ void list_remove(const GraphDev& g, int l, uint32_t n
     const int32_t last = __shfl(rv, d - 1, 64);
     ev.sync();
     if (lane == 0) {
-        st_i32(row + pos, last);
+        st_i32(g.layers[l].adj + (size_t)n * g.layers[l].cap + pos, last);
         st_i32(g.layers[l].deg + n, d - 1);
     }
     ev.sync();
+    if (lane == pos) rv = last;
+    d = d - 1;
+}
+template <class C, int G, class Ev>
+__device__ __forceinline__ void list_remove(const GraphDev& g, int l, uint32_t n, uint32_t v, const Ev& ev) {
+    const int lane = lane_id();
+    const int capl = g.layers[l].cap;
+    int32_t rv = lane < capl ? ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane) : -1;
+    int d = uni(ld_i32<true>(g.layers[l].deg + n));  // uniform: scalar loop bounds
+    list_remove_in(g, l, n, rv, d, v, ev);
 }
 
 // graph.go:50 n.neighbors[nw.Key] = nw: overwrite the entry of nw's key (which
@@ -203,11 +213,12 @@ __device__ __forceinline__ bool replenish_set(const GraphDev& g, int l, uint32_t
 // pushes in the same order as a per-neighbour loop would produce.
 template <class C, int G, class Ev>
 __device__ __forceinline__ void replenish(const GraphDev& g, int l, uint32_t n, int m, BuildSmem& S, WaveStats& st, int& err,
-                          const Ev& ev) {
+                          const Ev& ev, const int32_t* known_row = nullptr, int known_deg = 0) {
     const int lane = lane_id();
     const int capl = g.layers[l].cap;
-    const int32_t rv = lane < capl ? ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane) : -1;
-    int dn = uni(ld_i32<true>(g.layers[l].deg + n));
+    // n's row and degree: from the caller's registers when it just changed them
+    const int32_t rv = known_row ? *known_row : lane < capl ? ld_i32<true>(g.layers[l].adj + (size_t)n * capl + lane) : -1;
+    int dn = known_row ? known_deg : uni(ld_i32<true>(g.layers[l].deg + n));
     if (dn < 0) dn = 0;
     if (dn >= m) return;
     CPROF_T(tr);
@@ -442,10 +453,17 @@ __device__ __forceinline__ void add_neighbor(const GraphDev& g, int l, uint32_t 
     }
     CPROF_ADD(ta, 2);
     if (worst == EMPTY_ID) return;
-    list_remove<C, G>(g, l, n, worst, ev);  // graph.go:74
-    if (uni(ld_i32<true>(g.layers[l].deg + worst)) >= 0) list_remove<C, G>(g, l, worst, n, ev);  // graph.go:76-78
+    {
+        int dd = d;
+        list_remove_in(g, l, n, rv, dd, worst, ev);  // graph.go:74 (n's row is in registers since the append)
+    }
+    // worst's row, read after that removal (worst may be n itself)
+    const int capl = g.layers[l].cap;
+    int32_t wrow = lane < capl ? ld_i32<true>(g.layers[l].adj + (size_t)worst * capl + lane) : -1;
+    int wdeg = uni(ld_i32<true>(g.layers[l].deg + worst));
+    if (wdeg >= 0) list_remove_in(g, l, worst, wrow, wdeg, n, ev);  // graph.go:76-78
     CPROF_ADD(ta, 3);
-    replenish<C, G>(g, l, worst, m, S, st, err, ev);  // graph.go:79
+    replenish<C, G>(g, l, worst, m, S, st, err, ev, &wrow, wdeg);  // graph.go:79
     CPROF_ADD(ta, 4);
 }
 
@@ -468,9 +486,11 @@ __device__ __forceinline__ void isolate(const GraphDev& g, int l, uint32_t n, in
     rank_sort(key, mine, dn);
     for (int j = 0; j < dn; ++j) {
         const uint32_t x = rl_u(mine, j);
-        if (uni(ld_i32<true>(g.layers[l].deg + x)) < 0) continue;  // neighbor.neighbors == nil
-        list_remove<C, G>(g, l, x, n, ev);                     // graph.go:232 delete(neighbor.neighbors, n.Key)
-        replenish<C, G>(g, l, x, m, S, st, err, ev);           // graph.go:232
+        int32_t xrow = lane < capl ? ld_i32<true>(g.layers[l].adj + (size_t)x * capl + lane) : -1;
+        int xdeg = uni(ld_i32<true>(g.layers[l].deg + x));
+        if (xdeg < 0) continue;                            // neighbor.neighbors == nil
+        list_remove_in(g, l, x, xrow, xdeg, n, ev);        // graph.go:232 delete(neighbor.neighbors, n.Key)
+        replenish<C, G>(g, l, x, m, S, st, err, ev, &xrow, xdeg);  // graph.go:232
     }
 }
 
