@@ -40,6 +40,13 @@ struct BuildSmem {
     int hcap;
     uint32_t* radj;  // replenish: staged neighbour rows (hcap entries)
     int64_t* rkey;   // ... and their keys
+    // eviction speculation (k_build_compat_mw): the neighbourhood's rows as the
+    // layer's addNeighbor pairs start, each followed by the new node, and the
+    // distances of every such entry to its row's owner (stride pstride)
+    int32_t* prow = nullptr;  // [pgroups * pstride] entry i of neighbour j's row
+    int* pdeg = nullptr;      // [pgroups] its degree (-1 nil)
+    float* pdist = nullptr;   // [pgroups * pstride] distance of entry i to neighbour j (entry deg: the new node)
+    int pgroups = 0, pstride = 0;
 };
 
 // Rows are loaded together with their degree (one round trip; entries past
@@ -403,68 +410,162 @@ __device__ __forceinline__ void replenish(const GraphDev& g, int l, uint32_t n, 
     CPROF_ADD(tr, 9);
 }
 
-// graph.go:41-81
+// What add_neighbor(n, nw) needs from before its own append, staged for the
+// whole neighbourhood at once (compat_insert): n's row and degree, and the
+// distance from n to each entry (entry deg: to nw).
+struct EvictSpec {
+    const int32_t* row;
+    int deg;
+    const float* dist;
+};
+
+// graph.go:41-81.  Returns the evicted neighbour (EMPTY_ID: none).
 template <class C, int G, class Ev>
-__device__ __forceinline__ void add_neighbor(const GraphDev& g, int l, uint32_t n, uint32_t nw, int m, BuildSmem& S, WaveStats& st,
-                             int& err, const Ev& ev) {
+__device__ __forceinline__ uint32_t add_neighbor(const GraphDev& g, int l, uint32_t n, uint32_t nw, int m, BuildSmem& S,
+                                                 WaveStats& st, int& err, const Ev& ev,
+                                                 bool have_sp = false, EvictSpec sp = {}) {
     const int lane = lane_id();
+    const int capl = g.layers[l].cap;
     int32_t rv;
-    CPROF_T(ta);
-    // n's row goes out with the append's loads (one round trip for both; most
-    // appends overflow the row and evict)
-    QReg<C> q;
-    load_query(q, g.vecs + (size_t)n * g.pitch);
-    const float qn = g.norms[n];
-    const int d = list_append(g, l, n, nw, ev, &rv);
-    CPROF_ADD(ta, 1);
-    if (d <= m) return;
-    CPROF_CNT(17, 1);
-    uint32_t nb = lane < d ? guard_id(g, (uint32_t)rv) : 0xFFFFFFFFu;
+    int d;
     float worst_d = -__int_as_float(0x7f800000);
     uint32_t worst = EMPTY_ID;
-    st.E += d;
-    // graph.go:60-71 takes the first maximum in map order.  A unique maximum and
-    // no NaN make the order irrelevant: score the row as it lies, and rank it
-    // by key (the map-order stand-in) only when a tie or a NaN needs it.
-    int nmax = 0;
-    bool nan = false;
-    ev.template run<C, G>(g, q, qn, nb, d, g.metric, [&](float dd, uint32_t u) {
-        nan |= !(dd == dd);
-        if (dd > worst_d || worst == EMPTY_ID) {
-            worst_d = dd;
-            worst = u;
-            nmax = 1;
-        } else if (dd == worst_d) {
-            ++nmax;
+    bool decided = false;
+    CPROF_T(ta);
+    QReg<C> q;
+    float qn = 0.f;
+    if (have_sp) {
+        // the append of list_append from the staged row (graph.go:50), then the
+        // staged distances: entry i of the row after it is the old entry i, or
+        // nw where nw went (the slot of its key, else slot deg)
+        const int d0 = sp.deg < 0 ? 0 : sp.deg;  // graph.go:46-48 allocate the map
+        const int32_t r0 = lane < capl ? sp.row[lane] : -1;
+        const bool pres = lane < d0 && kid_of(g, guard_id(g, (uint32_t)r0)) == kid_of(g, nw);
+        const unsigned long long pm = __ballot(pres);
+        const int pos = pm ? __ffsll((long long)pm) - 1 : d0;
+        d = uni(pm ? d0 : d0 + 1);
+        ev.sync();
+        if (lane == 0) {
+            st_i32(g.layers[l].adj + (size_t)n * capl + pos, (int32_t)nw);
+            st_i32(g.layers[l].deg + n, d);
         }
-    });
-    if (nan || nmax > 1) {
-        int64_t key = lane < d ? g.keys[nb] : INT64_MAX;
-        rank_sort(key, nb, d);  // Go map order -> ascending key
-        worst_d = -__int_as_float(0x7f800000);
-        worst = EMPTY_ID;
+        ev.sync();
+        rv = lane == pos ? (int32_t)nw : r0;
+        CPROF_ADD(ta, 1);
+        if (d <= m) return EMPTY_ID;
+        CPROF_CNT(17, 1);
         st.E += d;
-        ev.template run<C, G>(g, q, qn, nb, d, g.metric, [&](float dd, uint32_t u) {  // graph.go:60-71
-            if (dd > worst_d || worst == EMPTY_ID) {
-                worst_d = dd;
-                worst = u;
-            }
-        });
+        const float dl = lane < d ? sp.dist[lane == pos ? d0 : lane] : -__int_as_float(0x7f800000);
+        const bool nan = __ballot(lane < d && !(dl == dl)) != 0ull;
+        float wm = dl;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o, 64));
+        const unsigned long long at = __ballot(lane < d && dl == wm);
+        if (!nan && __popcll(at) == 1) {  // a unique maximum: the map order is irrelevant
+            worst = (uint32_t)guard_id(g, (uint32_t)__shfl(rv, __ffsll((long long)at) - 1, 64));
+            worst_d = wm;
+            decided = true;
+        } else {
+            load_query(q, g.vecs + (size_t)n * g.pitch);
+            qn = g.norms[n];
+        }
+    } else {
+        // n's row goes out with the append's loads (one round trip for both; most
+        // appends overflow the row and evict)
+        load_query(q, g.vecs + (size_t)n * g.pitch);
+        qn = g.norms[n];
+        d = list_append(g, l, n, nw, ev, &rv);
+        CPROF_ADD(ta, 1);
+        if (d <= m) return EMPTY_ID;
+        CPROF_CNT(17, 1);
+        st.E += d;
+    }
+    uint32_t nb = lane < d ? guard_id(g, (uint32_t)rv) : 0xFFFFFFFFu;
+    if (!decided) {
+        // graph.go:60-71 takes the first maximum in map order.  A unique maximum and
+        // no NaN make the order irrelevant: score the row as it lies, and rank it
+        // by key (the map-order stand-in) only when a tie or a NaN needs it.
+        int nmax = 0;
+        bool nan = false;
+        if (!have_sp) {
+            ev.template run<C, G>(g, q, qn, nb, d, g.metric, [&](float dd, uint32_t u) {
+                nan |= !(dd == dd);
+                if (dd > worst_d || worst == EMPTY_ID) {
+                    worst_d = dd;
+                    worst = u;
+                    nmax = 1;
+                } else if (dd == worst_d) {
+                    ++nmax;
+                }
+            });
+        }
+        if (have_sp || nan || nmax > 1) {
+            int64_t key = lane < d ? g.keys[nb] : INT64_MAX;
+            rank_sort(key, nb, d);  // Go map order -> ascending key
+            worst_d = -__int_as_float(0x7f800000);
+            worst = EMPTY_ID;
+            st.E += d;
+            ev.template run<C, G>(g, q, qn, nb, d, g.metric, [&](float dd, uint32_t u) {  // graph.go:60-71
+                if (dd > worst_d || worst == EMPTY_ID) {
+                    worst_d = dd;
+                    worst = u;
+                }
+            });
+        }
     }
     CPROF_ADD(ta, 2);
-    if (worst == EMPTY_ID) return;
+    if (worst == EMPTY_ID) return EMPTY_ID;
     {
         int dd = d;
         list_remove_in(g, l, n, rv, dd, worst, ev);  // graph.go:74 (n's row is in registers since the append)
     }
     // worst's row, read after that removal (worst may be n itself)
-    const int capl = g.layers[l].cap;
     int32_t wrow = lane < capl ? ld_i32<true>(g.layers[l].adj + (size_t)worst * capl + lane) : -1;
     int wdeg = uni(ld_i32<true>(g.layers[l].deg + worst));
     if (wdeg >= 0) list_remove_in(g, l, worst, wrow, wdeg, n, ev);  // graph.go:76-78
     CPROF_ADD(ta, 3);
     replenish<C, G>(g, l, worst, m, S, st, err, ev, &wrow, wdeg);  // graph.go:79
     CPROF_ADD(ta, 4);
+    return worst;
+}
+
+// Stage EvictSpec for add_neighbor(c_j, nw), j < cnt (lane j of nbh: c_j): the
+// rows as they stand now, and one MW_PAIRS batch of every entry's distance to
+// its row's owner plus nw's.  False when the staging area is too small (then
+// every pair takes the plain path).
+template <class C, int G, class Ev>
+__device__ __forceinline__ bool stage_evictions(const GraphDev& g, int l, uint32_t nbh, int cnt, uint32_t nw,
+                                                BuildSmem& S, const Ev& ev) {
+    const int lane = lane_id();
+    const int capl = g.layers[l].cap;
+    if (!S.prow || cnt > S.pgroups || capl + 1 > S.pstride || cnt <= 0) return false;
+    const int ps = S.pstride;
+    const int tot = cnt * capl;
+    for (int e0 = 0; e0 < tot; e0 += 64) {  // uniform trip count: the shuffles see every lane
+        const int e = e0 + lane;
+        const int j = min(e / capl, 63), i = e % capl;
+        const uint32_t c = shfl_u(nbh, j);
+        if (e < tot) S.prow[j * ps + i] = ld_i32<true>(g.layers[l].adj + (size_t)c * capl + i);
+    }
+    const int dj = lane < cnt ? ld_i32<true>(g.layers[l].deg + guard_id(g, nbh)) : -1;  // lane j: c_j's degree
+    if (lane < cnt) S.pdeg[lane] = dj;
+    ev.sync();
+    // the pairs table: entries of row j (past its degree: none), then nw
+    for (int e0 = 0; e0 < cnt * ps; e0 += 64) {
+        const int e = e0 + lane;
+        const int j = min(e / ps, 63), i = e % ps;
+        const int djj = __shfl(dj, j, 64);
+        const int dd = djj < 0 ? 0 : min(djj, capl);
+        if (e < cnt * ps && i < dd) ev.pc[e] = (int32_t)guard_id(g, (uint32_t)S.prow[j * ps + i]);
+        if (e < cnt * ps && i == dd) ev.pc[e] = (int32_t)nw;
+    }
+    if (lane < cnt) {
+        ev.pq[lane] = nbh;
+        ev.pn[lane] = (dj < 0 ? 0 : min(dj, capl)) + 1;
+    }
+    ev.sync();
+    ev.template pairs<C, G>(g, cnt, g.metric);
+    return true;
 }
 
 // graph.go:221-235 isolate: neighbours in ascending key order (the map-order
@@ -503,7 +604,7 @@ struct MwHdr {
     int cmd, cnt, metric;
     float qn;
 };
-constexpr int MW_EVAL = 0, MW_EXIT = 1;
+constexpr int MW_EVAL = 0, MW_EXIT = 1, MW_PAIRS = 2;
 
 // Everything exchanged here lives in LDS (workers read only immutable rows from
 // HBM), so the fences order LDS alone: the master's graph stores are not waited
@@ -542,11 +643,18 @@ __device__ __forceinline__ void mw_share(const GraphDev& g, const QReg<C>& q, fl
 
 template <class C>
 struct MwEval {
+    static constexpr bool kPairs = true;
     MwHdr* hdr;
     float4* qbuf;     // [VPL * 64] the master's query registers, lane-major
     uint32_t* list;   // ids of the posted batch (also replenish's candidate list)
     float* dist;      // [cap] distances back
     int nw;
+    // MW_PAIRS: group j scores rows pc[j * ps, + pn[j]) against row pq[j] into pd
+    uint32_t* pq = nullptr;
+    int* pn = nullptr;
+    int32_t* pc = nullptr;
+    float* pd = nullptr;
+    int ps = 0;
     template <class C2, int G, class Sink>
     __device__ __forceinline__ void run_list(const GraphDev& g, const QReg<C2>& q, float qn, int cnt, int metric,
                                              Sink&& sink, bool sinks = true) const {
@@ -591,22 +699,59 @@ struct MwEval {
             outi[e] = list[e];
         }
     }
+    // every group j of the posted pairs table scored by the waves (pq / pn / pc
+    // written by the caller), distances into pd
+    template <class C2, int G>
+    __device__ __forceinline__ void pairs(const GraphDev& g, int ngroups, int metric) const;
     // the master's own lanes only (workers never touch graph state)
     __device__ __forceinline__ void sync() const { wave_sync(); }
 };
+
+// MW_PAIRS, wave w of nw: whole groups j = w, w + nw, ... (each group's rows
+// against its own owner row, loaded here)
+template <class C, int G>
+__device__ __forceinline__ void mw_pairs_share(const GraphDev& g, const MwEval<C>& ev, int ngroups, int metric, int w,
+                                               int nw) {
+    for (int j = w; j < ngroups; j += nw) {
+        const uint32_t o = guard_id(g, uni(ev.pq[j]));
+        QReg<C> q;
+        load_query(q, g.vecs + (size_t)o * g.pitch);
+        mw_share<C, G>(g, q, g.norms[o], reinterpret_cast<const uint32_t*>(ev.pc) + (size_t)j * ev.ps,
+                       ev.pd + (size_t)j * ev.ps, uni(ev.pn[j]), metric, 0, 1);
+    }
+}
 
 template <class C, int G>
 __device__ __forceinline__ void mw_worker(const GraphDev& g, const MwEval<C>& ev, int w) {
     for (;;) {
         mw_barrier();
-        if (ev.hdr->cmd == MW_EXIT) break;
-        QReg<C> q;
-        const int lane = lane_id();
+        const int cmd = ev.hdr->cmd;
+        if (cmd == MW_EXIT) break;
+        if (cmd == MW_PAIRS) {
+            mw_pairs_share<C, G>(g, ev, ev.hdr->cnt, ev.hdr->metric, w, ev.nw);
+        } else {
+            QReg<C> q;
+            const int lane = lane_id();
 #pragma unroll
-        for (int v = 0; v < C::VPL; ++v) q.v[v] = ev.qbuf[v * 64 + lane];
-        mw_share<C, G>(g, q, ev.hdr->qn, ev.list, ev.dist, ev.hdr->cnt, ev.hdr->metric, w, ev.nw);
+            for (int v = 0; v < C::VPL; ++v) q.v[v] = ev.qbuf[v * 64 + lane];
+            mw_share<C, G>(g, q, ev.hdr->qn, ev.list, ev.dist, ev.hdr->cnt, ev.hdr->metric, w, ev.nw);
+        }
         mw_barrier();
     }
+}
+
+template <class C>
+template <class C2, int G>
+__device__ __forceinline__ void MwEval<C>::pairs(const GraphDev& g, int ngroups, int metric) const {
+    if (ngroups <= 0) return;
+    if (lane_id() == 0) {
+        hdr->cmd = MW_PAIRS;
+        hdr->cnt = ngroups;
+        hdr->metric = metric;
+    }
+    mw_barrier();  // post
+    mw_pairs_share<C, G>(g, *this, ngroups, metric, 0, nw);
+    mw_barrier();  // collect
 }
 
 // The sequential kernels re-read a layer's descriptor (row cap, adjacency and
@@ -703,10 +848,29 @@ __device__ __forceinline__ bool compat_insert(const CompatBuildArgs& a, BuildSme
             if (lane == 0) st_i32(a.g.layers[l].deg + id, -1);
             ev.sync();
             CPROF_T(tn);
+            // Eviction speculation: the neighbourhood's rows and their distances
+            // are staged in one batch; pair j uses them unless an earlier pair of
+            // this loop changed c_j's row -- which only an eviction of c_j does
+            // (an addNeighbor pair writes its own two rows, and the evicted row
+            // with its replenish): then it reads the row as usual.
+            bool staged = false;
+            if constexpr (Ev::kPairs) staged = stage_evictions<C, G>(a.g, l, nbh, cnt, id, S, ev);
+            uint32_t evicted = EMPTY_ID;  // lane k: the k-th row evicted in this loop
+            int nev = 0;
             for (int j = 0; j < cnt; ++j) {
                 const uint32_t c = rl_u(nbh, j);
-                add_neighbor<C, G>(a.g, l, c, id, a.M, S, st, err, ev);
-                add_neighbor<C, G>(a.g, l, id, c, a.M, S, st, err, ev);
+                const bool fresh = staged && nev < 64 && __ballot(lane < nev && evicted == c) == 0ull;
+                const EvictSpec sp{S.prow + j * S.pstride, uni(S.pdeg[j]), S.pdist + j * S.pstride};
+                const uint32_t w1 = add_neighbor<C, G>(a.g, l, c, id, a.M, S, st, err, ev, fresh, sp);
+                if (w1 != EMPTY_ID) {
+                    if (lane == nev) evicted = w1;
+                    ++nev;
+                }
+                const uint32_t w2 = add_neighbor<C, G>(a.g, l, id, c, a.M, S, st, err, ev);
+                if (w2 != EMPTY_ID) {
+                    if (lane == nev) evicted = w2;
+                    ++nev;
+                }
             }
             CPROF_ADD(tn, 13);
         }
@@ -784,7 +948,25 @@ __global__ __launch_bounds__(64 * NW) void k_build_compat_mw(CompatBuildArgs a) 
     ev.list = p;
     p += S.hcap;
     ev.dist = reinterpret_cast<float*>(p);
+    p += S.hcap;
     ev.nw = NW;
+    // eviction speculation staging (stage_evictions): M groups of M + 2
+    S.pgroups = a.M;
+    S.pstride = a.M + 2;
+    const int pt = S.pgroups * S.pstride;
+    S.prow = reinterpret_cast<int32_t*>(p);
+    p += pt;
+    ev.pc = reinterpret_cast<int32_t*>(p);
+    p += pt;
+    ev.pd = reinterpret_cast<float*>(p);
+    S.pdist = ev.pd;
+    p += pt;
+    S.pdeg = reinterpret_cast<int*>(p);
+    p += 64;
+    ev.pq = p;
+    p += 64;
+    ev.pn = reinterpret_cast<int*>(p);
+    ev.ps = S.pstride;
     const int wave = threadIdx.x >> 6;
     if (wave != 0) {
         mw_worker<C, G>(a.g, ev, wave);
@@ -829,7 +1011,8 @@ static int launch_build_compat_t(const CompatBuildArgs& a, int waves, hipStream_
         if (lds > CW_LDS_MAX) return -2;
         hipLaunchKernelGGL((k_build_compat<C, G>), dim3(1), dim3(64), lds, s, a);
     } else {
-        const size_t lds = (base + 3 + 4 + 4 * 64 * (size_t)C::VPL + 2 * (size_t)hcap) * 4;
+        const size_t spec = 3 * (size_t)a.M * (a.M + 2) + 3 * 64;  // eviction speculation staging
+        const size_t lds = (base + 3 + 4 + 4 * 64 * (size_t)C::VPL + 2 * (size_t)hcap + spec) * 4;
         if (lds > CW_LDS_MAX) return -2;
         hipLaunchKernelGGL((k_build_compat_mw<C, G, MW_WAVES>), dim3(1), dim3(64 * MW_WAVES), lds, s, a);
     }

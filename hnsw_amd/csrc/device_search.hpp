@@ -249,6 +249,7 @@ __device__ __forceinline__ void wave_sync() {
 // (build.hip MwEval) has the same interface and spreads each batch of rows
 // over the workgroup's other waves.
 struct WaveEval {
+    static constexpr bool kPairs = false;  // no batched per-row scoring (build.hip MwEval::pairs)
     uint32_t* list = nullptr;  // LDS candidate list (run_list)
     template <class C, int G, class Sink>
     __device__ __forceinline__ void run(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int cnt,
