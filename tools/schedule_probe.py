@@ -18,14 +18,23 @@ from bench import Searcher, gen_vectors, recall_at_k  # noqa: E402
 
 dev = torch.device("cuda")
 n, d = 1_000_000, 768
-X = gen_vectors(n, d, 1234, 12, 1000, dev, "cosine")
-Q = gen_vectors(4096, d, 1234 + 7777, 12, 1000, dev, "cosine")
+# CFG2=1: BASELINE configs[2] instead (1M x 768 Euclidean, M0 48, efC 64, closest-M fill off; bench.py config2)
+cfg2 = os.environ.get("CFG2", "0") == "1"
+if cfg2:
+    X = gen_vectors(n, d, 77, 12, 1000, dev, "euclidean")
+    Q = gen_vectors(4096, d, 78, 12, 1000, dev, "euclidean")
+    base = dict(Distance=H.EuclideanDistance, Rng=5, m0=48, ef_construction=64, heuristic=2)
+else:
+    X = gen_vectors(n, d, 1234, 12, 1000, dev, "cosine")
+    Q = gen_vectors(4096, d, 1234 + 7777, 12, 1000, dev, "cosine")
+    base = dict(Distance=H.CosineDistance, Rng=1234, m0=40, ef_construction=400, heuristic=2, keep_pruned=1,
+                prune_alpha_pct=115)
 sets = [dict(kv.split("=") for kv in s_.split(",") if kv) for s_ in os.environ.get("BUILD_OPTS", "").split(";")]
 truth = None
 for opts in sets:
-    g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=1234, build_mode=H.BUILD_BATCH, m0=40,
-                ef_construction=400, heuristic=2, keep_pruned=1, prune_alpha_pct=115,
-                **{k: int(v) for k, v in opts.items()})
+    kw = dict(base)
+    kw.update({k: int(v) for k, v in opts.items()})
+    g = H.Graph(M=16, Ml=0.25, EfSearch=64, build_mode=H.BUILD_BATCH, **kw)
     g.reserve(n, d)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
