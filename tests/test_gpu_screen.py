@@ -153,6 +153,18 @@ def test_screened_batch_build_identical(H, metric, alpha):
         ex2.append(g.export())
         g.close()
     _same_graph(ex2[0], ex2[1])
+    # batches of 20 % of the index (bench.py's schedule for the bench index and
+    # configs[2]): again the same graph with and without the screen
+    ex3 = []
+    for screen in (0, 1):
+        g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
+                    ef_construction=80, heuristic=2, keep_pruned=1, screen=screen, prune_alpha_pct=alpha,
+                    batch_ratio_pct=20)
+        g.add_arrays(np.arange(n // 3), X[: n // 3])
+        g.add_arrays(np.arange(n // 3, n), X[n // 3:])
+        ex3.append(g.export())
+        g.close()
+    _same_graph(ex3[0], ex3[1])
 
 
 @pytest.mark.parametrize("d", [1024, 1536])
