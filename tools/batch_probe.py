@@ -23,11 +23,16 @@ g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=1234, bui
 g.reserve(n, d)
 g.add_device(np.arange(n), X.data_ptr(), n, d)
 del X
+modes = [(0, 1), (1 << 30, 1)]
+if os.environ.get("SCREEN_OFF") == "1":  # also the 4-wave kernel without the fp16 screen
+    modes.append((1 << 30, 0))
 for B in bs:
     S = Searcher(g, B, 10, d, dev)
     row = []
-    for mw in (0, 1 << 30):
+    for mw, scr in modes:
         g.set_option("beam_mw_max_b", mw)
+        if g.get_option("screen") != scr:
+            g.set_option("screen", scr)
         reps = max(5, min(400, 40000 // B))
         S.run(Q[:B], H.MODE_BEAM, 64)
         torch.cuda.synchronize()
@@ -36,5 +41,8 @@ for B in bs:
             S.run(Q[:B], H.MODE_BEAM, 64)
         torch.cuda.synchronize()
         row.append((time.perf_counter() - t0) / reps * 1e3)
-    print(f"B={B} one_wave_ms={row[0]:.4f} four_wave_ms={row[1]:.4f} ratio={row[0] / row[1]:.3f}", flush=True)
+    extra = f" four_wave_noscreen_ms={row[2]:.4f}" if len(row) > 2 else ""
+    print(f"B={B} one_wave_ms={row[0]:.4f} four_wave_ms={row[1]:.4f} ratio={row[0] / row[1]:.3f}{extra}", flush=True)
+    if len(row) > 2:
+        g.set_option("screen", 1)
 g.close()
