@@ -282,6 +282,12 @@ struct WaveEval {
     __device__ __forceinline__ void sync() const { wave_sync(); }
 };
 
+// the visited set's fill at which beam_layer forgets (3/4; a tools build may
+// set another fraction to measure the probe-length / re-evaluation trade)
+#ifndef MH_VIS_FULL
+#define MH_VIS_FULL(n) (((n) >> 1) + ((n) >> 2))
+#endif
+
 // How beam_layer scores one batch of new candidates (ids in lanes 0..cnt-1 of
 // cid) and hands the survivors to its sink: WaveBatch does it on the calling
 // wave; the multi-wave single-query kernel (beam.hpp MwBatch) spreads the rows
@@ -399,7 +405,7 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
             auto sink = [&](float d, uint32_t u) { bl_insert(L, ef, d, u); };
             st.F += bev.template score<C, G, SCREEN>(g, q, qn, cid, cnt, wd, screen, margin, sink, st.S);
         }
-        if (vcount > (vsize >> 1) + (vsize >> 2)) {  // forget: results unchanged
+        if (vcount > MH_VIS_FULL(vsize)) {  // forget: results unchanged
             wave_sync();
             vis_clear(vis, vsize);
             wave_sync();
