@@ -950,11 +950,12 @@ __global__ __launch_bounds__(64 * NW) void k_build_compat_mw(CompatBuildArgs a) 
     ev.dist = reinterpret_cast<float*>(p);
     p += S.hcap;
     ev.nw = NW;
-    // eviction speculation staging (stage_evictions): M groups of M + 2
-    S.pgroups = a.M;
+    // eviction speculation staging (stage_evictions): M groups of M + 2, when
+    // the launch found room for it
+    S.pgroups = a.spec ? a.M : 0;
     S.pstride = a.M + 2;
     const int pt = S.pgroups * S.pstride;
-    S.prow = reinterpret_cast<int32_t*>(p);
+    S.prow = a.spec ? reinterpret_cast<int32_t*>(p) : nullptr;
     p += pt;
     ev.pc = reinterpret_cast<int32_t*>(p);
     p += pt;
@@ -1012,9 +1013,12 @@ static int launch_build_compat_t(const CompatBuildArgs& a, int waves, hipStream_
         hipLaunchKernelGGL((k_build_compat<C, G>), dim3(1), dim3(64), lds, s, a);
     } else {
         const size_t spec = 3 * (size_t)a.M * (a.M + 2) + 3 * 64;  // eviction speculation staging
-        const size_t lds = (base + 3 + 4 + 4 * 64 * (size_t)C::VPL + 2 * (size_t)hcap + spec) * 4;
+        const size_t core = (base + 3 + 4 + 4 * 64 * (size_t)C::VPL + 2 * (size_t)hcap) * 4;
+        CompatBuildArgs b = a;
+        b.spec = core + spec * 4 <= CW_LDS_MAX ? 1 : 0;  // large M: no staging (same graph)
+        const size_t lds = core + (b.spec ? spec * 4 : 0);
         if (lds > CW_LDS_MAX) return -2;
-        hipLaunchKernelGGL((k_build_compat_mw<C, G, MW_WAVES>), dim3(1), dim3(64 * MW_WAVES), lds, s, a);
+        hipLaunchKernelGGL((k_build_compat_mw<C, G, MW_WAVES>), dim3(1), dim3(64 * MW_WAVES), lds, s, b);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

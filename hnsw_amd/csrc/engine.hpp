@@ -96,6 +96,7 @@ struct CompatBuildArgs {
     uint32_t rep_a, rep_b;        // its rows above i0 (EMPTY_ID: none needed) / from i0 down
     const int32_t* rep_entry;     // [MH_MAXL] entry() of each layer at its turn (the row itself: empty then)
     const int32_t* rep_sweep;     // [MH_MAXL] row the sweep deletes + isolates in layer l (-1 none)
+    int spec;                     // set by the launch: the eviction-staging area fits in LDS
 };
 int launch_build_compat(const CompatBuildArgs& a, int lpr, int vpl, int waves, hipStream_t s);  // waves: 1 or 8
 

@@ -173,6 +173,11 @@ def test_fixture_build_and_search(H, name):
     (600, 3, 1, 6, 0.5, 20),
     (300, 3072, 0, 8, 0.25, 16),
     (250, 4096, 1, 6, 0.3, 16),
+    # large M: the layer's eviction staging with 40-wide rows, and (M 60) a walk
+    # whose staging area does not fit in LDS next to the rest (the plain path);
+    # ef 64 also takes the LDS Go heaps instead of the register ones
+    (700, 128, 1, 40, 0.25, 40),
+    (500, 256, 0, 60, 0.25, 64),
 ])
 def test_compat_build_parity(H, O, n, d, metric, M, ml, ef):
     rng = np.random.default_rng(n + d)
