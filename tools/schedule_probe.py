@@ -20,7 +20,14 @@ dev = torch.device("cuda")
 n, d = 1_000_000, 768
 # CFG2=1: BASELINE configs[2] instead (1M x 768 Euclidean, M0 48, efC 64, closest-M fill off; bench.py config2)
 cfg2 = os.environ.get("CFG2", "0") == "1"
-if cfg2:
+hard = os.environ.get("HARD", "0") == "1"  # the harder-data leg (latent 32, M 32, M0 63, efC 512)
+efs = (256, 512) if hard else (48, 64)
+if hard:
+    X = gen_vectors(n, d, 4321, 32, 1000, dev, "cosine")
+    Q = gen_vectors(4096, d, 4321 + 7777, 32, 1000, dev, "cosine")
+    base = dict(Distance=H.CosineDistance, Rng=5, m0=63, ef_construction=512, heuristic=2, keep_pruned=1,
+                prune_alpha_pct=115, build_expand=2, M=32)
+elif cfg2:
     X = gen_vectors(n, d, 77, 12, 1000, dev, "euclidean")
     Q = gen_vectors(4096, d, 78, 12, 1000, dev, "euclidean")
     base = dict(Distance=H.EuclideanDistance, Rng=5, m0=48, ef_construction=64, heuristic=2)
@@ -34,7 +41,8 @@ truth = None
 for opts in sets:
     kw = dict(base)
     kw.update({k: int(v) for k, v in opts.items()})
-    g = H.Graph(M=16, Ml=0.25, EfSearch=64, build_mode=H.BUILD_BATCH, **kw)
+    kw.setdefault("M", 16)
+    g = H.Graph(Ml=0.25, EfSearch=64, build_mode=H.BUILD_BATCH, **kw)
     g.reserve(n, d)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -45,8 +53,9 @@ for opts in sets:
         truth = tuple(x.clone() for x in Searcher(g, 4096, 10, d, dev).run(Q, H.MODE_EXACT, 0))
     S = Searcher(g, 4096, 10, d, dev)
     recs = []
-    for ef in (48, 64):
+    for ef in efs:
         k_, _, n_ = S.run(Q, H.MODE_BEAM, ef)
         recs.append(recall_at_k(k_, n_, truth[0], truth[2], 10))
-    print(f"{opts}: {n / dt:.0f} inserts/s ({dt:.2f} s), recall@10 ef48 {recs[0]:.4f} ef64 {recs[1]:.4f}", flush=True)
+    print(f"{opts}: {n / dt:.0f} inserts/s ({dt:.2f} s), recall@10 ef{efs[0]} {recs[0]:.4f} ef{efs[1]} {recs[1]:.4f}",
+          flush=True)
     g.close()
