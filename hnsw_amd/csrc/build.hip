@@ -1662,9 +1662,10 @@ MH_DECL_PARTS(3)
 
 int MH_PARTFN(launch_build_compat)(const CompatBuildArgs& a, int lpr, int vpl, int waves, hipStream_t s) {
     // the sequential build keeps three query rows live (search / addNeighbor /
-    // replenish): two rows in flight per group keeps it spill-free
+    // replenish): up to 4 rows in flight per group to 768-d, 2 above (spill-free)
 #define X_(L, V, G) \
-    if (lpr == L && vpl == V) return launch_build_compat_t<Cfg<L, V>, (G < 2 ? G : 2)>(a, waves, s);
+    if (lpr == L && vpl == V)    \
+        return launch_build_compat_t<Cfg<L, V>, (V <= 3 ? (G < 4 ? G : 4) : (G < 2 ? G : 2))>(a, waves, s);
     MH_FOR_EACH_CFG(X_)
 #undef X_
     return -3;
