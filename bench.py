@@ -178,11 +178,13 @@ def cpu_model():
 
 
 def build_roofline(bs, secs, n, dim, m0, metric, traffic=None):
-    """Batched insert: the search kernels' algorithmic bytes -- f32 rows (4d + 4:
+    """Batched insert: the insert kernels' algorithmic bytes -- f32 rows (4d + 4:
     row + norm) for every f32 evaluation and neighbour-selection row, fp16 rows
     (2d, + 8 for L2's {unscale, |x|}) for every screened candidate, one layer-0
     adjacency row per expansion, the new row and its adjacency/proposal writes --
-    over their device time (HIP events around each launch)."""
+    over the device time of every insert kernel (k_batch_descend, k_batch_search
+    and k_batch_commit; HIP events around each layer's launches).  `wall_frac`
+    puts the same bytes over the whole Add call's wall time."""
     F, Sc, Xp = bs["build_f32_rows"], bs["build_screened"], bs["build_expansions"]
     aux = 8 if metric == "euclidean" else 0
     byts = F * (4 * dim + 4) + Sc * (2 * dim + aux) + Xp * 4 * (m0 + 1) + n * (4 * dim + 16 * m0)
@@ -192,11 +194,23 @@ def build_roofline(bs, secs, n, dim, m0, metric, traffic=None):
             "dist_evals_per_insert": round(bs["build_dist_evals"] / n, 1),
             "f32_rows_per_insert": round(F / n, 1), "screened_per_insert": round(Sc / n, 1),
             "expansions_per_insert": round(Xp / n, 1), "dropped_proposals": bs["dropped_proposals"],
-            "roofline": {"bound": "hbm", "kernel": "k_batch_search + k_batch_descend",
+            "roofline": {"bound": "hbm", "kernel": "k_batch_descend + k_batch_search + k_batch_commit",
                          "kernel_ms_total": round(us / 1e3, 2), "alg_bytes": int(byts),
                          "achieved": round(gbs, 1) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None,
+                         "wall_frac": round(byts / secs / 1e9 / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_kernel": "k_batch_search"}}
+
+
+def list_checksum(keys, dists, n):
+    """order-sensitive int64 checksum of a batch of result lists (keys, distance
+    bits, counts): equal on every rank when every rank merged the same lists"""
+    B, k = keys.shape
+    m = torch.arange(k, device=keys.device)[None, :] < n[:, None].long()
+    kk = torch.where(m, keys, torch.full_like(keys, -1))
+    db = torch.where(m, dists.contiguous().view(torch.int32).long(), torch.zeros_like(keys))
+    w = torch.arange(1, B * k + 1, device=keys.device, dtype=torch.int64).view(B, k) * 0x9E3779B1 + 1
+    return int(((kk * w) ^ (db * 0x2545F491)).sum().item() + int(n.long().sum().item()))
 
 
 def timed(fn, reps=1):
@@ -221,28 +235,33 @@ def config0(device, seconds):
     X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
     Qh = rng.uniform(-1, 1, (nq, d)).astype(np.float32)
     g = H.Graph(M=16, Ml=0.25, EfSearch=20, Distance=H.CosineDistance, Rng=42)  # compat build (reference Add)
+    lv = g.preview_levels(n)  # the levels the engine's seed-42 stream gives (injected into the oracle)
     bt, _ = timed(lambda: g.add_arrays(np.arange(n), X))
     Q = torch.from_numpy(Qh).to(device)
     S = Searcher(g, nq, k, d, device)
     S.run(Q, H.MODE_COMPAT, 20)
-    st, (ck, _, cn) = timed(lambda: S.run(Q, H.MODE_COMPAT, 20), reps=20)
+    st, (ck, cd, cn) = timed(lambda: S.run(Q, H.MODE_COMPAT, 20), reps=20)
     g.device_status()
-    ck, cn = ck.clone(), cn.clone()
+    ck, cd, cn = ck.clone(), cd.clone(), cn.clone()
     tk, _, tn = (x.clone() for x in Searcher(g, nq, k, d, device).run(Q, H.MODE_EXACT, 0))
     rec = recall_at_k(ck, cn, tk, tn, k)
-    o = O.Graph(metric=O.COSINE, order=O.ORDER_REF, M=16, Ml=0.25, EfSearch=20)
-    o.import_graph(**g.export())
+    # the reference's Add (graph.go:437-531) in the reference's arithmetic (ORDER_REF),
+    # the same levels, the whole 10k walk -- timed as the CPU baseline and compared
+    ob = O.Graph(metric=O.COSINE, order=O.ORDER_REF, M=16, Ml=0.25, EfSearch=20)
+    cbt, _ = timed(lambda: ob.add(np.arange(n), X, lv))
+    from oracle.parity import compare_lists, same_graph
+
+    graph_same = same_graph(g.export(), ob.export())
+    par = compare_lists(tuple(x.cpu().numpy() for x in (ck, cd, cn)), ob.search(Qh, k, mode=O.MODE_COMPAT), k,
+                        truth=(tk.cpu().numpy(), tn.cpu().numpy()))
     cpu = {}
     for name, nt in (("1_thread", 1), ("all_threads", host_threads())):
         chunk = max(nq, 64 * nt)
         done, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < seconds / 4:
-            o.search(Qh[np.arange(done, done + chunk) % nq], k, mode=O.MODE_COMPAT, threads=nt)
+            ob.search(Qh[np.arange(done, done + chunk) % nq], k, mode=O.MODE_COMPAT, threads=nt)
             done += chunk
         cpu[name] = round(done / (time.perf_counter() - t0), 1)
-    ob = O.Graph(metric=O.COSINE, order=O.ORDER_REF, M=16, Ml=0.25, EfSearch=20, seed=42)
-    nb = 2000  # bounded sample of the reference Add walk
-    cbt, _ = timed(lambda: ob.add(np.arange(nb), X[:nb]))
     g.close()
     return {"workload": "10k x 128-d U[-1,1) cosine, M=16 Ml=0.25 EfSearch=20, k=10, 1000 queries (reference "
                         "semantics: compat Add + compat Search)",
@@ -250,8 +269,11 @@ def config0(device, seconds):
             "recall_at_10_compat": round(rec, 4),
             "cpu_compat_search_qps": cpu["1_thread"], "cpu_compat_search_qps_all_threads": cpu["all_threads"],
             "cpu_threads": host_threads(), "cpu_model": cpu_model(),
-            "cpu_compat_add_inserts_per_s": round(nb / cbt, 1), "cpu_compat_add_sample": nb,
-            "cpu_kind": "port (oracle/: C restatement of graph.go, ORDER_REF sequential fp32; the Go toolchain is absent)"}
+            "cpu_compat_add_inserts_per_s": round(n / cbt, 1), "cpu_compat_add_sample": n,
+            "cpu_kind": "port (oracle/: C restatement of graph.go, ORDER_REF sequential fp32; the Go toolchain is absent)",
+            "parity_vs_order_ref": dict(par, graph_identical=bool(graph_same),
+                                        what="GPU compat build + compat Search vs the oracle's Add + Search in "
+                                             "ORDER_REF from the same levels (a = GPU, b = ORDER_REF)")}
 
 
 def config2(device):
@@ -361,30 +383,63 @@ def config_harder(device, batch=16384, efs=(64, 128, 256, 512)):
             "at_recall_0.99": next((p_ for p_ in points if p_["recall_at_10"] >= 0.99), None)}
 
 
-def cpu_baseline(g, queries_np, k, ef, metric, seconds):
-    """The CPU restatement (oracle/, test infrastructure) timed on this host on a
-    bounded sample: same graph, same beam algorithm; plus the reference's
-    compat Search() semantics.  Single thread, sequential queries
-    (= BatchSearch's loop, graph.go:1075)."""
+def oracle_leg(g, Q, truth, k, ef, metric, seconds, device, nparity=1024):
+    """Outside every timed region, on one oracle handle holding the engine's
+    exported graph (oracle/: test infrastructure, the checker and the CPU
+    baseline only):
+
+    parity -- the north star's criterion (recall@k equal, distances within
+      1e-5) on `nparity` of the step's queries, for the beam search (the
+      headline) and the reference's Search() semantics (compat): the engine's
+      lists against the oracle in ORDER_DEV (the engine's summation tree:
+      expected bit-identical) and in ORDER_REF (sequential fp32, the
+      reference's arithmetic stand-in), recall against the exact path's truth;
+    cpu baseline -- the same graph searched on this host on a bounded sample:
+      beam single thread (= BatchSearch's loop, graph.go:1075), the reference's
+      compat Search single thread, and beam on every usable CPU (concurrent
+      Search, graph_benchmark_test.go:70-89)."""
     import oracle as O  # checker / baseline only
+    from oracle.parity import compare_lists
 
     ex = g.export()
-    o = O.Graph(metric=O.COSINE if metric == "cosine" else O.EUCLIDEAN, order=O.ORDER_REF, M=g.M,
+    o = O.Graph(metric=O.COSINE if metric == "cosine" else O.EUCLIDEAN, order=O.ORDER_DEV, M=g.M,
                 M0=g.get_option("m0"), Ml=g.Ml, EfSearch=ef)
     o.import_graph(**ex)
     del ex
-    out = {}
     threads = host_threads()
-    nq = len(queries_np)
+    B = min(nparity, Q.shape[0], truth[0].shape[0])
+    Qp = Q[:B].contiguous()
+    Qh = Qp.cpu().numpy()
+    tr = (truth[0][:B].cpu().numpy(), truth[1][:B].cpu().numpy())
+    gpu = {}
+    for tag, mode in (("beam", H.MODE_BEAM), ("compat", H.MODE_COMPAT)):
+        gpu[tag] = tuple(x.clone().cpu().numpy() for x in Searcher(g, B, k, Q.shape[1], device).run(Qp, mode, ef))
+    g.device_status()
+    par = {"queries": B, "k": k, "ef": ef, "criterion": "recall delta <= 0.002, max |dist diff| <= 1e-5 (north_star)"}
+    ok = True
+    for tag, mode in (("beam", O.MODE_BEAM), ("compat", O.MODE_COMPAT)):
+        o.set_order(O.ORDER_DEV)
+        dev = compare_lists(gpu[tag], o.search(Qh, k, mode=mode, ef=ef, threads=threads), k, bitwise=True)
+        o.set_order(O.ORDER_REF)
+        ref = compare_lists(gpu[tag], o.search(Qh, k, mode=mode, ef=ef, threads=threads), k, truth=tr)
+        par[tag] = {"order_dev_identical": dev["identical_lists"], "order_ref_identical": ref["identical_lists"],
+                    "recall_gpu": ref["recall_a"], "recall_order_ref": ref["recall_b"],
+                    "recall_delta": ref["recall_delta"], "max_abs_dist_diff": ref["max_abs_dist_diff"],
+                    "common_pairs": ref["common_pairs"]}
+        ok = ok and dev["identical_lists"] == 1.0 and ref["recall_delta"] <= 0.002 and ref["max_abs_dist_diff"] <= 1e-5
+    par["pass"] = bool(ok)
+    # CPU baseline, ORDER_REF
+    out = {}
+    nq = len(Qh)
     for name, mode, nt, frac in (("beam", O.MODE_BEAM, 1, 0.4), ("compat", O.MODE_COMPAT, 1, 0.3),
                                  ("beam_mt", O.MODE_BEAM, threads, 0.3)):
         chunk = 32 * nt  # 32 queries per thread per call (thread start-up amortised)
         done, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < seconds * frac:  # cycles through the sample
-            o.search(queries_np[np.arange(done, done + chunk) % nq], k, mode=mode, ef=ef, threads=nt)
+            o.search(Qh[np.arange(done, done + chunk) % nq], k, mode=mode, ef=ef, threads=nt)
             done += chunk
         out[name] = (done / (time.perf_counter() - t0), done, nt)
-    return out
+    return out, par
 
 
 def main():
@@ -513,7 +568,19 @@ def main():
         def sstep():
             return sharded_search(engine_local_search(gs, a.k, H.MODE_BEAM, a.ef), Qs, a.k)
 
-        sk, _, sn = (x.clone() for x in sstep())
+        sk, sd, sn = (x.clone() for x in sstep())
+        # readiness of the N-rank path, readable without trusting prose: how many
+        # ranks took part, that the shards cover the dataset, and that every rank
+        # merged the same lists (one all_reduce each of max / min of the checksum)
+        csum = list_checksum(sk, sd, sn)
+        ready = {"ranks_seen": world, "rows_total": hi - lo, "merged_checksum": csum, "checksums_agree": True}
+        if world > 1:
+            t_ = torch.tensor([1, hi - lo, csum, -csum], dtype=torch.int64, device=device)
+            dist.all_reduce(t_[:2])
+            mm = t_[2:].clone()
+            dist.all_reduce(mm, op=dist.ReduceOp.MAX)
+            ready.update(ranks_seen=int(dist.get_world_size()), ranks_reporting=int(t_[0]), rows_total=int(t_[1]),
+                         checksums_agree=bool(int(mm[0]) == -int(mm[1])))
         ek, ed, en = sharded_search(engine_local_search(gs, a.k, H.MODE_EXACT, 0), Qs[:ngt], a.k)
         torch.cuda.synchronize()
         srecall = mean_over_ranks(recall_at_k(sk[:ngt], sn[:ngt], ek, en, a.k))
@@ -572,6 +639,7 @@ def main():
             "recall_reference": "sharded exact search (per-shard MFMA exact + the same gather + merge)",
             "build_inserts_per_s_per_rank": round((hi - lo) / sbuild_s, 1),
             "phases": phases,
+            "readiness": ready,
             "operating_points": spoints,
             "at_recall_0.99": sat99,
             "scaling": "strong (fixed total rows; BASELINE configs[3] at 8 ranks)",
@@ -698,9 +766,7 @@ def main():
             "parallelism": f"{'shard' if shard else 'replica'}{world}",
         },
         "recall_at_10": round(recall, 4),
-        "parity": ("results bit-identical to oracle/, a C restatement of graph.go/distance.go (the Go toolchain "
-                   "is absent, so parity is to the restatement, pinned by the reference's own test vectors: "
-                   "tests/golden/reference_goldens.json); checked by pytest -m gpu, not inside this run"),
+        "parity": ("measured at N=1 (rank 0, outside the timed region): see the N=1 line" if world > 1 else None),
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -720,12 +786,15 @@ def main():
     if shard_out is not None and not shard_only:
         out["shard"] = shard_out
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
-        qn = Q[: min(a.batch, 4096)].cpu().numpy()
-        cb = cpu_baseline(g, qn, a.k, a.ef, a.metric, a.cpu_seconds)
+        cb, par = oracle_leg(g, Q[: min(a.batch, 4096)], (tk, tn), a.k, a.ef, a.metric, a.cpu_seconds, device)
+        par["oracle"] = ("oracle/: C restatement of graph.go/heap.go/distance.go (the Go toolchain is absent) on the "
+                         "engine's exported graph; ORDER_DEV = the engine's summation tree, ORDER_REF = sequential "
+                         "fp32, pinned by the reference's own vectors (tests/golden/reference_goldens.json)")
+        out["parity"] = par
         out["cpu_baseline"] = {
             "value": round(cb["beam"][0], 2), "unit": "queries/s", "cores": 1, "kind": "port",
-            "sample": f"{cb['beam'][1]} of the same queries, same 1M graph, oracle beam search (ORDER_REF "
-                      f"sequential fp32), single thread, ~{a.cpu_seconds * 0.4:.0f}s time box",
+            "sample": f"{cb['beam'][1]} searches cycling over 4096 of the step's queries, same 1M graph, oracle "
+                      f"beam search (ORDER_REF sequential fp32), single thread, ~{a.cpu_seconds * 0.4:.0f}s time box",
             "compat_search_qps": round(cb["compat"][0], 2), "compat_sample": cb["compat"][1],
             "beam_mt_qps": round(cb["beam_mt"][0], 2), "beam_mt_threads": cb["beam_mt"][2],
             "beam_mt_sample": cb["beam_mt"][1], "host_cpus": os.cpu_count(), "affinity_cpus": host_threads(),

@@ -49,6 +49,7 @@ SIGNATURES = {
     "mhnsw_lookup": (C.c_int, [_vp, C.c_int64, _f32p]),
     "mhnsw_contains": (C.c_int, [_vp, _i64p, C.c_int64, _u8p]),
     "mhnsw_add_plan": (C.c_int, [_vp, _i64p, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int)]),
+    "mhnsw_add_reached": (C.c_int, [_vp, C.POINTER(C.c_int64)]),
     "mhnsw_num_layers": (C.c_int, [_vp]),
     "mhnsw_layer_count": (C.c_int64, [_vp, C.c_int]),
     "mhnsw_connectivity": (C.c_int, [_vp, _P(C.c_double), C.c_int]),

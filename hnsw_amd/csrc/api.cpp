@@ -1,195 +1,16 @@
-// api.cpp -- C ABI (include/mhnsw.h) over the HIP kernels.
-//
-// Host side of the engine: owns the device-resident index (row-major vector
-// store, per-layer fixed-stride adjacency, norms, keys), draws levels like
-// graph.go:388-417, schedules the compat or batched build, and runs searches.
+// api.cpp -- C ABI (include/mhnsw.h) over the HIP kernels: handle lifecycle,
+// options, Add / BatchAdd (levels drawn like graph.go:388-417, the compat and
+// batched build schedules), Delete, statistics.  Searches: search_host.cpp;
+// export / import and string keys: io_host.cpp; the shared state: index.hpp.
 // The graph lives in HBM; the host keeps only the key -> internal-id map,
 // per-node levels and per-layer counts/entries.
-#include <hip/hip_runtime.h>
+#include "index.hpp"
 
-#include <errno.h>
-#include <fcntl.h>
-#include <unistd.h>
+using namespace mhh;
 
-#include <algorithm>
-#include <cmath>
-#include <cstdarg>
-#include <cstdio>
-#include <cstring>
-#include <map>
-#include <mutex>
-#include <shared_mutex>
-#include <string>
-#include <unordered_map>
-#include <vector>
-
-#include "../../include/mhnsw.h"
-#include "codec.hpp"
-#include "engine.hpp"
-
-using namespace mh;
-
-namespace {
+namespace mhh {
 
 thread_local std::string g_create_err;
-
-template <class T>
-struct DevBuf {
-    T* p = nullptr;
-    size_t n = 0;
-};
-
-struct Layer {
-    int32_t* deg = nullptr;
-    int32_t* adj = nullptr;
-    float* adjd = nullptr;
-    int cap = 0;
-    int64_t count = 0;
-    int32_t entry = -1;
-};
-
-}  // namespace
-
-struct mhnsw_index {
-    // public fields (graph.go:305-326)
-    int metric = COSINE;
-    int M = 16;
-    double ml = 0.25;
-    int ef = 20;
-    uint64_t rng = 0;
-    // engine options
-    int build_mode = MHNSW_BUILD_COMPAT;
-    int m0 = 0;  // 0 => 2*M in batch mode, M in compat mode
-    int efc = 0; // 0 => EfSearch
-    int heuristic = 1;
-    int keep_pruned = 0;
-    int build_expand = 2;     // batched insert: entries expanded per step of its layer searches (1-4)
-    int alpha_pct = 100;
-    int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
-    int vis_log2 = 12;
-    int vis_entries = 0;      // beam search's visited set; 0 = 1.25 * 2^vis_log2 (beam_vis_entries)
-    int exact_kk = 0;
-    int exact_sample = 64;   // fused preselection: row tiles in the threshold sample (at most; stride = ceil(tiles / this))
-    int exact_thr_rank = 0;  // fused preselection: the sample's J-th best is the threshold (0 = max(k, kk / 8))
-    int exact_precision = 3;  // scores: 0 f32-input MFMA, 1 bf16x3 split, 2 fp16 2-product split,
-                              // 3 fp16 1-product with the fused preselection (all certified, same results)
-    int exact_tile = 0;       // GEMM variant (exact.hip: launch_split_scores, launch_h1)
-    int compat_waves = 8;     // compat insert: waves scoring each distance batch (1 = the walking wave alone)
-    int upper_ef = 1;         // beam search: upper-layer descent width
-    int64_t beam_mw_max_b = 512;  // beam search: batches up to this size run one workgroup of 4 waves per query
-    int screen = 1;           // beam search / batched insert fp16 screening copy (results unchanged)
-    int fuse_descent = 1;     // batched insert: all greedy descents of a batch in one launch (same graph)
-    int time_build = 0;       // batched insert: time its search kernels with HIP events (stats [12])
-    int64_t max_rows = 0;     // row capacity limit (0 = none): an Add past it fails with MHNSW_ENOMEM, index unchanged
-    std::vector<hipEvent_t> tev;  // event pairs around the timed launches of the current Add
-    size_t tev_used = 0;
-    double build_search_us = 0;
-    // shape
-    int dim = 0, pitch = 0, lpr = 0, vpl = 0;
-    bool layers_exist = false;
-    int64_t n = 0, capn = 0;
-    int device = 0;
-    hipStream_t stream = nullptr;
-    // device state
-    float* vecs = nullptr;
-    float* norms = nullptr;
-    uint16_t* h16 = nullptr;  // fp16 screening copy [capn * pitch] (screen = 1)
-    float2* h16aux = nullptr;  // [capn] L2 screening {unscale, |x|}
-    int h16_metric = -1;       // metric the copies were written for
-    float* h16err = nullptr;   // [1] the copy's measured max relative rounding (screening margin)
-    int64_t* keys = nullptr;
-    int32_t* levels = nullptr;
-    uint8_t* dead = nullptr;  // [capn] deleted rows (graph.go:843-864)
-    bool any_dead = false;
-    // key identity (compat; GraphDev::kid): allocated at the first replaced or re-added key
-    int32_t* kid = nullptr;      // [capn] first row that held the row's key
-    int32_t* kidlive = nullptr;  // [capn] by kid: the key's newest live row (-1 none)
-    int32_t* kprev = nullptr;    // [capn] the next older live row of the same key (-1 none; GraphDev::kprev)
-    bool aliased = false;
-    uint32_t* cur_entry = nullptr;
-    int32_t* inc_cnt = nullptr;
-    uint32_t* inc_src = nullptr;
-    float* inc_dist = nullptr;
-    int inc_cap = 64;
-    uint32_t* touched = nullptr;
-    size_t touched_cap = 0;
-    int32_t* touched_cnt = nullptr;
-    int32_t* d_layer_entry = nullptr;
-    LayerDev* d_layers = nullptr;
-    LayerDev layers_host[MH_MAXL] = {};
-    unsigned long long* d_stats = nullptr;
-    // d_err[0]: error word of the current synchronous call (zeroed per call);
-    // d_err[1]: sticky word of *_device searches, which return before their
-    // kernels run -- read and cleared by mhnsw_device_status
-    int* d_err = nullptr;
-    std::vector<Layer> layers;
-    // scratch
-    DevBuf<float> qpad, qnorm, scores, tmp;
-    DevBuf<uint32_t> cand;
-    DevBuf<uint32_t> border;           // batched insert: batch nodes by level, descending
-    uint32_t* ord_pin = nullptr;       // ... staged in pinned memory
-    int64_t ord_cap = 0;
-    hipEvent_t ord_ev = nullptr;       // the staging copy has been consumed
-    bool ord_pending = false;
-    DevBuf<int64_t> okeys;
-    DevBuf<float> odist;
-    DevBuf<int32_t> on;
-    DevBuf<float> nq, nneg, ncd;  // negatives: queries, padded negative rows, candidate distances
-    DevBuf<int64_t> nck, nok;
-    DevBuf<int32_t> ncn, nci, noff, non;
-    DevBuf<float> nos;
-    // exact path: cached bf16 hi/lo planes of the first xsplit_rows rows (rows are
-    // immutable once added; import resets), per-chunk query planes, certificate state
-    DevBuf<uint16_t> xsplit, qsplit;
-    int64_t xsplit_rows = 0, xsplit_plane = 0;  // rows converted; plane stride they were written with
-    int xsplit_kind = 0;                        // 1: bf16 hi/lo planes, 2: fp16 hi plane + xinv (exact_precision)
-    DevBuf<float> xinv, qinv;                   // exact_precision 2: per-row / per-query unscale
-    DevBuf<float> xerr;                         // ... and the rows' max relative fp16 rounding
-    // exact_precision 3 (fp16 1-product, fused preselection): sample thresholds,
-    // filter constants, tile regions + counts, per-query buckets, the queries' rounding
-    DevBuf<float> h1thr, h1c, h1s, qerr;
-    DevBuf<float> h1xw;  // [4 capn] per-row filter constants of k_h1_pp16 (k_h1_rowconst)
-    DevBuf<uint2> h1region, h1bucket;
-    DevBuf<int32_t> h1rcnt, h1qcnt;
-    DevBuf<uint8_t> h1ovf;
-    DevBuf<float> xbound, xmaxn, xsegd;
-    DevBuf<uint32_t> xsegi;
-    DevBuf<uint8_t> xflag;
-    DevBuf<uint8_t> xgone;     // exact path: rows to skip when some live row is not in layer 0
-    int64_t partial_rows = 0;  // rows neither deleted nor in layer 0 (left by failed inserts, graph.go:1009)
-    uint64_t mut_epoch = 0;            // bumped by every Add / Delete / Import: row membership may have changed
-    uint64_t xgone_epoch = ~0ull;      // the epoch xgone was built at
-    DevBuf<int32_t> xflagged, xnflag;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    hipEvent_t gev0 = nullptr, gev1 = nullptr;  // the exact path's score GEMM (first query chunk)
-    bool have_gemm_timing = false;
-    // cross-stream ordering: a *_device search returns once enqueued on the
-    // caller's stream; the next call on another stream (or a mutation) must
-    // not reuse scratch / rewrite the graph under it
-    hipEvent_t scr_ev = nullptr, meta_ev = nullptr;
-    hipStream_t scr_stream = nullptr;
-    bool scr_valid = false;
-    bool have_timing = false;
-    // host mirrors
-    std::unordered_map<int64_t, int32_t> key2id;  // live keys only
-    // Go string keys (Graph[string]): order-maintenance labels -- every string
-    // ever added maps to an int64 label in lexicographic order, so the engine's
-    // key comparisons (compat expansion order, tie-breaks) see the string order
-    std::map<std::string, int64_t> s2l;
-    std::unordered_map<int64_t, std::string> l2s;
-    int64_t relabels = 0;
-    std::vector<int32_t> hlevels;
-    std::vector<uint32_t> hmask;  // bit l: row is in layer l (compat may promote into emptied layers)
-    std::vector<uint8_t> hdead;
-    std::vector<int32_t> hkid;                       // kid mirror (aliased only)
-    std::vector<int32_t> hprev;                      // kprev mirror (aliased only)
-    std::unordered_map<int64_t, int32_t> dead_kid;   // deleted keys -> kid, for a later re-add
-    int64_t stats_host[8] = {0};
-    std::string err;
-    mutable std::shared_mutex mu;
-};
-
-namespace {
 
 int fail(mhnsw_index* h, int code, const char* fmt, ...) {
     char buf[512];
@@ -203,18 +24,6 @@ int fail(mhnsw_index* h, int code, const char* fmt, ...) {
         g_create_err = buf;
     return code;
 }
-
-#define HIPCHK(h, x)                                                                          \
-    do {                                                                                      \
-        hipError_t e_ = (x);                                                                  \
-        if (e_ != hipSuccess) return fail(h, MHNSW_EDEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
-    } while (0)
-
-#define LCHK(h, x)                                                              \
-    do {                                                                        \
-        int r_ = (x);                                                           \
-        if (r_ != 0) return fail(h, r_ == -4 ? MHNSW_EUNSUPPORTED : MHNSW_EDEVICE, "kernel launch failed (%d) at %s", r_, #x); \
-    } while (0)
 
 // graph.go:916-937
 int validate(mhnsw_index* h) {
@@ -263,36 +72,7 @@ int cap_of(const mhnsw_index* h, int l) {
     return m + 1;  // addNeighbor overflows by one before evicting (graph.go:50-53)
 }
 
-template <class T>
-int ensure_buf(mhnsw_index* h, DevBuf<T>& b, size_t n) {
-    if (b.n >= n) return 0;
-    if (b.p) (void)hipFree(b.p);
-    b.p = nullptr;
-    b.n = 0;
-    size_t want = std::max(n, b.n * 2);
-    if (hipMalloc(&b.p, want * sizeof(T)) != hipSuccess) return fail(h, MHNSW_ENOMEM, "device allocation of %zu bytes failed", want * sizeof(T));
-    b.n = want;
-    return 0;
-}
 
-template <class T>
-int grow(mhnsw_index* h, T*& p, int64_t old_elems, int64_t new_elems, int fill_byte, bool fill32 = false,
-         uint32_t fill_val = 0) {
-    T* np = nullptr;
-    if (hipMalloc(&np, (size_t)new_elems * sizeof(T)) != hipSuccess)
-        return fail(h, MHNSW_ENOMEM, "device allocation of %lld bytes failed", (long long)(new_elems * sizeof(T)));
-    if (fill32)
-        HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)np, (int)fill_val, (size_t)new_elems * sizeof(T) / 4, h->stream));
-    else if (fill_byte >= 0)
-        HIPCHK(h, hipMemsetAsync(np, fill_byte, (size_t)new_elems * sizeof(T), h->stream));
-    if (p && old_elems > 0) HIPCHK(h, hipMemcpyAsync(np, p, (size_t)old_elems * sizeof(T), hipMemcpyDeviceToDevice, h->stream));
-    if (p) {
-        HIPCHK(h, hipStreamSynchronize(h->stream));
-        (void)hipFree(p);
-    }
-    p = np;
-    return 0;
-}
 
 int ensure_layer(mhnsw_index* h, int l) {
     while ((int)h->layers.size() <= l) {
@@ -588,7 +368,7 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         a.touched_cnt = h->touched_cnt;
         a.stats = h->d_stats + 4;
         a.vis_log2 = h->vis_log2;
-        // time_build: HIP events around the search launches (descent + layer searches)
+        // time_build: HIP events around every insert kernel (descent, layer searches, commits)
         auto tmark = [&]() -> int {
             if (!h->time_build) return 0;
             if (h->tev_used == h->tev.size()) {
@@ -612,8 +392,8 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         HIPCHK(h, hipMemsetAsync(h->touched_cnt, 0, 4, h->stream));
         if ((r = tmark())) return r;
         LCHK(h, launch_build_batch_search(a, h->lpr, h->vpl, h->stream));
-        if ((r = tmark())) return r;
         if (maxlvl >= l) LCHK(h, launch_build_batch_commit(a, h->lpr, h->vpl, (a1 - a0) * mcap, h->stream));
+        if ((r = tmark())) return r;
     }
     return 0;
 }
@@ -738,8 +518,14 @@ int32_t key_row_in(const mhnsw_index* h, int64_t key, int l) {
     return -1;
 }
 
-int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_on_device, int64_t n, int dim,
-             const int32_t* levels) {
+// One step of BatchAdd's walk (graph.go:950-1039) over nodes [0, n): *reached =
+// the inserts it got to (levels consumed, graph.go:962), the replacing or
+// failing one included; *cont > 0 when the walk goes on at node *cont (a key
+// whose nodes sat only in upper layers was replaced and Len() grew).
+int add_step(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_on_device, int64_t n, int dim,
+             const int32_t* levels, int64_t* reached, int64_t* cont_out) {
+    *reached = 0;
+    *cont_out = -1;
     int r = validate(h);
     if (r) return r;
     if (n <= 0) return 0;
@@ -1008,6 +794,7 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     auto unwind = [&](int64_t fail_row, int fail_layer) -> int {
         const bool rep_failed = rep >= 0 && (fail_row == ida || fail_row == idb);
         const int64_t i_f = rep_failed ? rep : fail_row - n0;
+        *reached = i_f + 1;
         for (size_t l = 0; l < h->layers.size(); ++l) {
             h->layers[l].count = l < snap_layers.size() ? snap_layers[l].first : 0;
             h->layers[l].entry = l < snap_layers.size() ? snap_layers[l].second : -1;
@@ -1136,6 +923,7 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
             // graph.go:1035-1037: a replacement of a key that layer 0 held leaves Len()
             // unchanged -- "node not added" ends the walk; one whose nodes sat only in
             // upper layers (left by a failed insert) grows it, and the walk goes on
+            *reached = nproc;  // up to the replacing insert
             if (rep_in0)
                 r = fail(h, MHNSW_EINTERNAL, "node not added");
             else
@@ -1151,423 +939,28 @@ int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
         h->build_search_us += ms * 1e3;
     }
     h->tev_used = 0;
-    if (r == 0 && cont > 0 && cont < n)  // the rest of the walk (graph.go:950: the next node)
-        return add_impl(h, keys + cont, vecs + (size_t)cont * dim, vecs_on_device, n - cont, dim,
-                        levels ? levels + cont : nullptr);
+    if (r == 0) *reached = nproc;
+    *cont_out = cont;
     return r;
 }
 
-// Mutations (Add / Delete / Reserve / Import) first let every enqueued
-// search finish: they rewrite or reallocate what those kernels read.
-// The beam search kernel is held to 2 waves per SIMD by its VGPRs (8 per CU),
-// which leaves 20 KiB of the CU's 160 KiB LDS per wave: its visited set takes
-// 1.25 * 2^vis_log2 entries (5,120 at the default), fewer resets at large ef.
-int beam_vis_entries(const mhnsw_index* h) {
-    if (h->vis_entries > 0) return h->vis_entries;
-    return std::min(32768, 5 << (h->vis_log2 - 2));
+int add_impl(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_on_device, int64_t n, int dim,
+             const int32_t* levels) {
+    h->add_reached = 0;
+    for (;;) {
+        int64_t reached = 0, cont = -1;
+        const int r = add_step(h, keys, vecs, vecs_on_device, n, dim, levels, &reached, &cont);
+        h->add_reached += reached;
+        if (r || cont <= 0 || cont >= n) return r;
+        // the rest of the walk (graph.go:950: the next node)
+        keys += cont;
+        vecs += (size_t)cont * dim;
+        n -= cont;
+        if (levels) levels += cont;
+    }
 }
 
-int drain(mhnsw_index* h) {
-    if (h->scr_valid) HIPCHK(h, hipEventSynchronize(h->scr_ev));
-    h->scr_valid = false;
-    return 0;
-}
-
-int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B, int dim, int k, int mode, int ef,
-                const int64_t* entry_key, int64_t* okeys, float* odist, int32_t* on, hipStream_t s, bool timing,
-                int32_t* out_ids, bool sticky);
-
-// every search: order after the previous scratch user (another stream), and
-// after the metadata copies this call makes on the handle's stream.  sticky:
-// the kernels report into d_err[1] (an asynchronous *_device search the caller
-// checks with mhnsw_device_status); otherwise into d_err[0], zeroed first.
-int search_impl(mhnsw_index* h, const float* queries, bool on_device, int64_t B, int dim, int k, int mode, int ef,
-                const int64_t* entry_key, int64_t* okeys, float* odist, int32_t* on, hipStream_t s, bool timing,
-                int32_t* out_ids = nullptr, bool sticky = false) {
-    if (h->scr_valid && h->scr_stream != s) HIPCHK(h, hipStreamWaitEvent(s, h->scr_ev, 0));
-    const int r = search_body(h, queries, on_device, B, dim, k, mode, ef, entry_key, okeys, odist, on, s, timing,
-                              out_ids, sticky);
-    HIPCHK(h, hipEventRecord(h->scr_ev, s));
-    h->scr_stream = s;
-    h->scr_valid = true;
-    return r;
-}
-
-// the search kernels run on the caller's stream; metadata goes up on the handle's
-int order_meta(mhnsw_index* h, hipStream_t s) {
-    if (s == h->stream) return 0;
-    HIPCHK(h, hipEventRecord(h->meta_ev, h->stream));
-    HIPCHK(h, hipStreamWaitEvent(s, h->meta_ev, 0));
-    return 0;
-}
-
-int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B, int dim, int k, int mode, int ef,
-                const int64_t* entry_key, int64_t* okeys, float* odist, int32_t* on, hipStream_t s, bool timing,
-                int32_t* out_ids, bool sticky) {
-    int r = validate(h);
-    if (r) return r;
-    h->have_gemm_timing = false;  // last_gemm_ns describes this search or none
-    if (k <= 0) return fail(h, MHNSW_EK, "k must be greater than 0, got %d", k);  // graph.go:542-544
-    if (h->layers_exist && h->dim != dim) {                                          // graph.go:547-552
-        if (B == 1) return fail(h, MHNSW_EDIM, "embedding dimension mismatch: %d != %d", h->dim, dim);
-        return fail(h, MHNSW_EDIM, "embedding dimension mismatch for query %d: %d != %d", 0, h->dim, dim);
-    }
-    if (mode < 0 || mode > 2) return fail(h, MHNSW_EINVAL, "unknown search mode %d", mode);
-    if (h->build_mode == MHNSW_BUILD_FLAT && mode != MHNSW_MODE_EXACT)
-        return fail(h, MHNSW_EUNSUPPORTED, "flat index (build_mode 2) supports exact search only");
-    if (B <= 0) return 0;
-    if (!h->layers_exist || live_count(h) == 0) {  // graph.go:554-556: nil, nil
-        if (on_device)
-            HIPCHK(h, hipMemsetAsync(on, 0, B * 4, s));
-        else
-            memset(on, 0, B * 4);
-        return 0;
-    }
-    if (ef <= 0) ef = h->ef;
-    const int top = top_live_layer(h);
-    uint32_t entry = (uint32_t)h->layers[top].entry;
-    if (entry_key) {
-        const int32_t e = key_row_in(h, *entry_key, top);
-        if (e < 0) return fail(h, MHNSW_EINVAL, "entry key %lld not in top layer", (long long)*entry_key);
-        entry = (uint32_t)e;
-    }
-    if ((r = ensure_buf(h, h->qpad, (size_t)B * h->pitch))) return r;
-    const float* qsrc = queries;
-    if (!on_device) {
-        if ((r = ensure_buf(h, h->tmp, (size_t)B * dim))) return r;
-        HIPCHK(h, hipMemcpyAsync(h->tmp.p, queries, (size_t)B * dim * 4, hipMemcpyHostToDevice, s));
-        qsrc = h->tmp.p;
-    }
-    LCHK(h, launch_pad_rows(qsrc, B, dim, h->qpad.p, h->pitch, s));
-    int64_t* dk = okeys;
-    float* dd = odist;
-    int32_t* dn = on;
-    if (!on_device) {
-        if ((r = ensure_buf(h, h->okeys, (size_t)B * k)) || (r = ensure_buf(h, h->odist, (size_t)B * k)) ||
-            (r = ensure_buf(h, h->on, (size_t)B)))
-            return r;
-        dk = h->okeys.p;
-        dd = h->odist.p;
-        dn = h->on.p;
-    }
-    int* errw = sticky ? h->d_err + 1 : h->d_err;
-    if (!sticky) HIPCHK(h, hipMemsetAsync(h->d_err, 0, sizeof(int), s));
-    if (mode == MHNSW_MODE_EXACT) {
-        if (k > 256) return fail(h, MHNSW_EUNSUPPORTED, "exact mode supports k <= 256");
-        const bool split = h->exact_precision != 0;
-        // fp16 1-product with the fused preselection (needs one full sample tile of rows)
-        const bool h1 = h->exact_precision == 3 && h->n >= H1_BN;
-        const bool h2 = h->exact_precision >= 2;  // fp16 row plane (1- and 2-product)
-        // preselect width: the fp16 2-product scores carry a ~2x larger error bound, so the
-        // kk-th score must sit further from the k-th distance for the certificate
-        const int kk = h->exact_kk > 0 ? std::min(256, std::max(h->exact_kk, k))
-                                       : std::min(256, h2 ? std::max(2 * k, 64) : std::max(2 * k, k + 16));
-        const int64_t ldS = (h->n + 255) / 256 * 256;
-        const int64_t budget = (int64_t)4 << 30;  // score workspace bytes
-        int64_t qc = std::max<int64_t>(1, std::min<int64_t>(B, budget / (ldS * 4)));
-        qc = std::min<int64_t>(qc, 4096);
-        if ((r = ensure_buf(h, h->qnorm, (size_t)B)) ||
-            (r = ensure_buf(h, h->cand, (size_t)qc * kk)) || (r = ensure_buf(h, h->xbound, (size_t)qc)) ||
-            (r = ensure_buf(h, h->xflag, (size_t)qc)) || (r = ensure_buf(h, h->xflagged, (size_t)qc)) ||
-            (r = ensure_buf(h, h->xnflag, 1)) || (r = ensure_buf(h, h->xmaxn, 1)))
-            return r;
-        // selection: enough (query, row-segment) waves to stream the score rows at full rate
-        auto segs = [&](int64_t rows, int& ns, int64_t& sl) {
-            ns = (int)std::min<int64_t>(16, std::max<int64_t>(1, (16384 + qc - 1) / qc));
-            ns = (int)std::max<int64_t>(1, std::min<int64_t>(ns, (rows + 4095) / 4096));
-            ns = std::max(1, std::min(ns, 1024 / kk));  // merge holds nseg * kk entries
-            sl = ((rows + ns - 1) / ns + 1023) / 1024 * 1024;
-        };
-        int nseg;
-        int64_t seglen;
-        segs(h->n, nseg, seglen);
-        if ((r = ensure_buf(h, h->xsegd, (size_t)qc * nseg * kk)) || (r = ensure_buf(h, h->xsegi, (size_t)qc * nseg * kk)))
-            return r;
-        // fused preselection (h1): the sample = every stride-th full row tile (about 32
-        // tiles), its J-th best score per query is the threshold (J = kk when the
-        // sample is every tile); a row passes at a rate of ~J / sample rows
-        // the GEMM variant this search runs (exact_tile 0: the default, k_h1_pp16; a shape
-        // it does not admit runs the ring kernel's filter)
-        const int ev = h1_effective_variant(h->exact_tile, h->pitch, std::max<int64_t>(qc, h->capn));
-        const int bm = h1_tile_bm(ev);
-        const int64_t nnt = (h->n + H1_BN - 1) / H1_BN, nqt = (qc + bm - 1) / bm;
-        const int stride = (int)std::max<int64_t>(1, std::min<int64_t>(128, (nnt + h->exact_sample - 1) / h->exact_sample));
-        const int64_t nsamp = h1 ? ((h->n / H1_BN) - 1) / stride + 1 : 0;  // sampled full tiles
-        const int J = stride < 8 ? kk : h->exact_thr_rank > 0 ? std::min(kk, std::max(k, h->exact_thr_rank)) : std::max(k, kk / 8);
-        // the score workspace: every (query, row) score (precisions 0-2, and their
-        // fallback), or only the sample's (fused path: its fallback streams distances
-        // into per-segment lists, k_fallback_select)
-        if ((r = ensure_buf(h, h->scores, (size_t)qc * (h1 ? (size_t)std::max<int64_t>(nsamp, 1) * H1_BN : (size_t)ldS))))
-            return r;
-        int sseg = 1;
-        int64_t sseglen = 0;
-        if (h1) {
-            segs(nsamp * H1_BN, sseg, sseglen);
-            sseg = std::max(1, std::min(sseg, 1024 / J));
-        }
-        // pairs per tile region / per query sub-bucket: 4x what the threshold lets
-        // through on average (~J N / ns per query, ~bm J BN / ns per tile), with floors
-        const int64_t ns = std::max<int64_t>(1, nsamp * H1_BN);
-        // (a multiple of 8: k_h1_pp16 splits each tile's region among its 8 waves)
-        // record-mode variants: per wave 4x the expected records (<= one per passing pair,
-        // at most 8 block rows x 64 lanes), H1_REC uint2 each
-        const int rcap = h1_records(ev)
-                             ? 8 * H1_REC * (int)std::min<int64_t>(512, std::max<int64_t>(64, 4 * bm * J * H1_BN / ns / 8))
-                             : (int)std::min<int64_t>((int64_t)bm * H1_BN, std::max<int64_t>(2048, 4 * bm * J * H1_BN / ns) + 7) / 8 * 8;
-        const int rsub = h1_region_split(ev);
-        const int scap = (int)std::min<int64_t>(std::max<int64_t>(h->n, 1),
-                                                std::max<int64_t>(512, 8 * J * h->n / ns / H1_BSUB));
-        if (h1 && ((r = ensure_buf(h, h->h1thr, (size_t)qc)) || (r = ensure_buf(h, h->h1c, (size_t)nqt * bm + 256)) ||
-                   (r = ensure_buf(h, h->h1s, (size_t)nqt * bm + 256)) ||
-                   (r = ensure_buf(h, h->h1region, (size_t)nqt * nnt * rcap)) ||
-                   (r = ensure_buf(h, h->h1rcnt, (size_t)nqt * nnt * rsub)) ||
-                   (r = ensure_buf(h, h->h1xw, (size_t)std::max<int64_t>(h->n, 1) * 4)) ||
-                   (r = ensure_buf(h, h->h1qcnt, (size_t)qc * H1_BSUB * H1_CSTRIDE)) || (r = ensure_buf(h, h->h1ovf, (size_t)qc)) ||
-                   (r = ensure_buf(h, h->h1bucket, (size_t)qc * H1_BSUB * scap)) || (r = ensure_buf(h, h->qerr, 1)) ||
-                   (r = ensure_buf(h, h->xsegd, (size_t)qc * sseg * J)) ||
-                   (r = ensure_buf(h, h->xsegi, (size_t)qc * sseg * J))))
-            return r;
-        if (split) {
-            const int64_t plane = h->capn * h->pitch;
-            const int kind = h2 ? 2 : 1;
-            if (h->xsplit.n < (size_t)plane * 2 || h->xsplit_plane != plane || h->xsplit_kind != kind) {
-                if ((r = ensure_buf(h, h->xsplit, (size_t)plane * 2))) return r;
-                h->xsplit_rows = 0;
-                h->xsplit_plane = plane;
-                h->xsplit_kind = kind;
-            }
-            if ((r = ensure_buf(h, h->qsplit, (size_t)qc * h->pitch * 2))) return r;
-            if (h2 && ((r = ensure_buf(h, h->xinv, (size_t)h->capn)) || (r = ensure_buf(h, h->qinv, (size_t)qc)) ||
-                       (r = ensure_buf(h, h->xerr, 1))))
-                return r;
-        }
-        LCHK(h, launch_norms(h->qpad.p, 0, B, h->pitch, h->lpr, h->vpl, h->qnorm.p, s));
-        if ((r = sync_layer_table(h)) || (r = order_meta(h, s))) return r;
-        GraphDev g = graph_view(h);
-        g.err = errw;
-        // rows the brute force skips: deleted ones, and the live rows of a failed
-        // insert that never reached layer 0 (graph.go:1009 leaves them in upper
-        // layers only; Search cannot return them)
-        const uint8_t* xdead = h->any_dead ? h->dead : nullptr;
-        if (h->partial_rows) {  // rebuilt only after a mutation
-            if (h->xgone_epoch != h->mut_epoch) {
-                std::vector<uint8_t> gone((size_t)h->n);
-                for (int64_t i = 0; i < h->n; ++i) gone[i] = h->hdead[i] || !in_layer(h, i, 0);
-                if ((r = ensure_buf(h, h->xgone, (size_t)std::max<int64_t>(h->n, 1)))) return r;
-                HIPCHK(h, hipMemcpyAsync(h->xgone.p, gone.data(), (size_t)h->n, hipMemcpyHostToDevice, s));
-                HIPCHK(h, hipStreamSynchronize(s));
-                h->xgone_epoch = h->mut_epoch;
-            }
-            xdead = h->xgone.p;
-        }
-        g.dead = xdead;
-        // certificate constants (u = 2^-24; gamma_n = n u / (1 - n u) bounds any
-        // order of n-term f32 summation relative to the sum of magnitudes)
-        const double u = std::ldexp(1.0, -24);
-        auto gam = [&](double nn) { return nn * u / (1.0 - nn * u); };
-        // products per element: f32 1, bf16x3 3, fp16 2-product 2, fp16 1-product 1.  Split
-        // error: bf16x3 drops ql.xl and the planes' tails (3.02 * 2^-16); fp16 2-product
-        // rounds the rows to fp16 (2^-11 |x|, Cauchy-Schwarz) and the queries to hi + lo
-        // (2^-21); fp16 1-product rounds both once
-        const double g_mfma = gam((h1 ? 1.0 : h2 ? 2.0 : split ? 3.0 : 1.0) * h->pitch + 1);
-        // (fp16: the rows' part -- and the queries' in the 1-product -- is the measured
-        // max |x' - x| / |x| <= 2^-11, added on the device)
-        const double e_split = h1 ? 0.0 : h2 ? std::ldexp(1.0, -21) : split ? 3.02 * std::ldexp(1.0, -16) : 0.0;
-        const double g_can = gam(4.0 * h->vpl + 8);  // canonical: 4*VPL fmaf per lane + 6 butterfly levels
-        CertArgs cert{};
-        cert.qnorm = h->qnorm.p;
-        cert.xmax = h->xmaxn.p;
-        cert.eps_cos = (float)(1.01 * ((g_mfma + e_split + g_can) * (1.0 + 1e-4) + 16 * u));
-        cert.eps_dot = (float)(1.01 * (g_mfma + e_split + g_can));
-        cert.c_l2 = (float)(1.01 * (2.0 * gam(4.0 * h->vpl + 10) + 16 * u));
-        cert.flag = h->xflag.p;
-        cert.flagged = h->xflagged.p;
-        cert.nflag = h->xnflag.p;
-        cert.stats = h->d_stats + 3;
-        cert.xerr = h2 ? h->xerr.p : nullptr;
-        cert.qerr = h1 ? h->qerr.p : nullptr;
-        if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
-        if (split && h->xsplit_rows < h->n) {
-            uint16_t* xh = h->xsplit.p;
-            uint16_t* xl = h->xsplit.p + (size_t)h->capn * h->pitch;
-            if (h2) {
-                if (h->xsplit_rows == 0) HIPCHK(h, hipMemsetAsync(h->xerr.p, 0, sizeof(float), s));
-                LCHK(h, launch_split_h16(h->vecs, h->xsplit_rows, h->n, h->pitch, h->capn, xh, nullptr, h->xinv.p,
-                                         h->xerr.p, s));
-            }
-            else
-                LCHK(h, launch_split_rows(h->vecs, h->xsplit_rows, h->n, h->pitch, h->capn, xh, xl, s));
-            h->xsplit_rows = h->n;
-        }
-        if (h->metric == EUCLIDEAN) {
-            HIPCHK(h, hipMemsetAsync(h->xmaxn.p, 0, sizeof(float), s));
-            LCHK(h, launch_max_norm(h->norms, h->n, h->xmaxn.p, s));
-        }
-        for (int64_t q0 = 0; q0 < B; q0 += qc) {
-            const int64_t nb = std::min(qc, B - q0);
-            ExactArgs a{};
-            a.X = h->vecs;
-            a.xnorm = h->norms;
-            a.dead = xdead;
-            a.N = h->n;
-            a.Q = h->qpad.p + (size_t)q0 * h->pitch;
-            a.qnorm = h->qnorm.p + q0;
-            a.B = nb;
-            a.pitch = h->pitch;
-            a.dim = h->dim;
-            a.metric = h->metric;
-            a.scores = h->scores.p;
-            a.ldS = ldS;
-            a.kk = kk;
-            a.cand = h->cand.p;
-            a.bound = h->xbound.p;
-            a.nseg = nseg;
-            a.seglen = seglen;
-            a.seg_d = h->xsegd.p;
-            a.seg_i = h->xsegi.p;
-            int64_t* ok_ = dk + q0 * k;
-            float* od_ = dd + q0 * k;
-            int32_t* on_ = dn + q0;
-            int32_t* oi_ = out_ids ? out_ids + q0 * k : nullptr;
-            if (split) {
-                a.Xh = h->xsplit.p;
-                a.Xl = h->xsplit.p + (size_t)h->capn * h->pitch;
-                a.ldXs = h->capn;
-                a.Qh = h->qsplit.p;
-                a.Ql = h->qsplit.p + (size_t)qc * h->pitch;
-                a.ldQs = qc;
-                if (h1) {
-                    a.xinv = h->xinv.p;
-                    a.qinv = h->qinv.p;
-                    HIPCHK(h, hipMemsetAsync(h->qerr.p, 0, sizeof(float), s));
-                    LCHK(h, launch_split_h16(a.Q, 0, nb, h->pitch, qc, h->qsplit.p, nullptr, h->qinv.p, h->qerr.p, s));
-                    // 1. sample: every score of the sampled row tiles -> the kk-th best per query
-                    ExactArgs as = a;
-                    as.tile_stride = stride;
-                    as.nsample_tiles = nsamp;
-                    as.ldS = nsamp * H1_BN;
-                    LCHK(h, launch_h1_sample(as, ev, s));
-                    as.N = nsamp * H1_BN;
-                    as.kk = J;
-                    as.nseg = sseg;
-                    as.seglen = sseglen;
-                    as.bound = h->h1thr.p;
-                    LCHK(h, launch_exact_select(as, s));
-                    // 2. the full GEMM keeps the pairs that can beat it; 3. per-query buckets; 4. top-kk
-                    LCHK(h, launch_ring_prep(h->h1thr.p, a.qnorm, a.qinv, nb, h->metric, h->h1c.p, h->h1s.p, s));
-                    HIPCHK(h, hipMemsetAsync(h->h1qcnt.p, 0, (size_t)nb * H1_BSUB * H1_CSTRIDE * 4, s));
-                    HIPCHK(h, hipMemsetAsync(h->h1ovf.p, 0, (size_t)nb, s));
-                    a.tile_stride = 1;
-                    a.ring_c = h->h1c.p;
-                    a.ring_s = h->h1s.p;
-                    a.region = h->h1region.p;
-                    a.region_cnt = h->h1rcnt.p;
-                    a.rcap = rcap;
-                    a.xw = reinterpret_cast<const float4*>(h->h1xw.p);
-                    if (q0 == 0)
-                        LCHK(h, launch_h1_rowconst(h->xinv.p, h->norms, xdead, h->n, h->metric,
-                                                   reinterpret_cast<float4*>(h->h1xw.p), s));
-                    if (timing && q0 == 0) HIPCHK(h, hipEventRecord(h->gev0, s));
-                    LCHK(h, launch_h1_filter(a, ev, s));
-                    if (timing && q0 == 0) {
-                        HIPCHK(h, hipEventRecord(h->gev1, s));
-                        h->have_gemm_timing = true;
-                    }
-                    const int64_t bqt = (nb + bm - 1) / bm;
-                    LCHK(h, launch_bucket(h->h1region.p, h->h1rcnt.p, rcap, bqt * nnt, bqt, bm, H1_BN, nb, h->h1qcnt.p,
-                                          h->h1bucket.p, scap, h->h1ovf.p, rsub, h1_records(ev) ? 1 : 0, a, s));
-                    LCHK(h, launch_select_bucket(a, h->h1qcnt.p, h->h1bucket.p, scap, h->h1ovf.p, h->h1thr.p, s));
-                } else if (h2) {
-                    a.xinv = h->xinv.p;
-                    a.qinv = h->qinv.p;
-                    LCHK(h, launch_split_h16(a.Q, 0, nb, h->pitch, qc, h->qsplit.p, h->qsplit.p + (size_t)qc * h->pitch,
-                                             h->qinv.p, nullptr, s));
-                    LCHK(h, launch_exact_scores_x2h(a, h->exact_tile, s));
-                } else {
-                    LCHK(h, launch_split_rows(a.Q, 0, nb, h->pitch, qc, h->qsplit.p,
-                                              h->qsplit.p + (size_t)qc * h->pitch, s));
-                    LCHK(h, launch_exact_scores_x3(a, h->exact_tile, s));
-                }
-            } else {
-                LCHK(h, launch_exact_scores(a, s));
-            }
-            if (!h1) LCHK(h, launch_exact_select(a, s));
-            if (h1 && h1_timing_diag(ev)) continue;  // timing diagnostic: no re-rank, no results
-            HIPCHK(h, hipMemsetAsync(h->xnflag.p, 0, sizeof(int32_t), s));
-            CertArgs c1 = cert;
-            c1.bound = h->xbound.p;
-            c1.qnorm = h->qnorm.p + q0;
-            LCHK(h, launch_rerank(a.Q, g, h->cand.p, kk, nb, h->lpr, h->vpl, k, ok_, od_, on_, oi_, c1, s));
-            // uncertified queries: canonical distances of every row, then select + re-rank again
-            ExactArgs a2 = a;
-            a2.only = h->xflag.p;
-            a2.bound = nullptr;
-            if (h1) {
-                LCHK(h, launch_fallback_select(a.Q, g, a2, h->lpr, h->vpl, s));
-            } else {
-                LCHK(h, launch_exact_fallback(a.Q, g, h->n, h->xflagged.p, h->xnflag.p, h->scores.p, ldS, h->lpr,
-                                              h->vpl, s));
-                LCHK(h, launch_exact_select(a2, s));
-            }
-            CertArgs c2{};
-            c2.only = h->xflag.p;
-            LCHK(h, launch_rerank(a.Q, g, h->cand.p, kk, nb, h->lpr, h->vpl, k, ok_, od_, on_, oi_, c2, s));
-        }
-        if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));
-        if (h->exact_precision == 3 && h->n >= H1_BN && h1_timing_diag(ev))
-            return fail(h, MHNSW_EUNSUPPORTED, "exact_tile %d is a timing diagnostic: no results", h->exact_tile);
-    } else {
-        if ((r = sync_layer_entries(h))) return r;
-        if ((r = sync_layer_table(h)) || (r = order_meta(h, s))) return r;
-        SearchArgs a;
-        a.g = graph_view(h);
-        a.g.err = errw;
-        a.q = h->qpad.p;
-        a.B = B;
-        a.k = k;
-        a.ef = ef;
-        a.top = top;
-        a.entry = entry;
-        a.layer_entry = h->d_layer_entry;
-        a.out_keys = dk;
-        a.out_dist = dd;
-        a.out_n = dn;
-        a.out_ids = out_ids;
-        a.stats = h->d_stats;
-        a.err = errw;
-        a.vis_log2 = h->vis_log2;
-        a.vis_n = beam_vis_entries(h);
-        a.upper_ef = h->upper_ef;
-        a.mw_max_b = h->beam_mw_max_b;
-        if (mode == MHNSW_MODE_BEAM) {
-            if (std::max(ef, k) > 512) return fail(h, MHNSW_EUNSUPPORTED, "beam mode supports max(ef,k) <= 512");
-            if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
-            LCHK(h, launch_search_beam(a, h->lpr, h->vpl, s));
-            if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));
-        } else {
-            if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
-            int lr = launch_search_compat(a, h->lpr, h->vpl, s);
-            if (lr == -2) return fail(h, MHNSW_EUNSUPPORTED, "compat search LDS budget exceeded (ef=%d, k=%d)", ef, k);
-            LCHK(h, lr);
-            if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));
-        }
-    }
-    h->have_timing = timing;
-    h->stats_host[6] += B;
-    if (!on_device) {
-        HIPCHK(h, hipMemcpyAsync(okeys, dk, (size_t)B * k * 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(h, hipMemcpyAsync(odist, dd, (size_t)B * k * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(h, hipMemcpyAsync(on, dn, (size_t)B * 4, hipMemcpyDeviceToHost, s));
-        int err = 0;
-        HIPCHK(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
-        HIPCHK(h, hipStreamSynchronize(s));
-        if (err & 4) return fail(h, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
-        if (err) return fail(h, MHNSW_EINTERNAL, "visited set overflow (raise vis_log2)");
-    }
-    return 0;
-}
-
-}  // namespace
+}  // namespace mhh
 
 // ===========================================================================
 // C ABI
@@ -1776,13 +1169,13 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "exact_kk") {
         h->exact_kk = (int)v;
     } else if (n == "exact_tile") {
-        // precisions 1 / 2: 0-3 (the split GEMM's tiles); precision 3: 0, 5 or 34 (the
-        // tools build, MH_EXACT_DIAG, also 30 / 31: timing diagnostics)
-        bool ok = (v >= 0 && v <= 3) || v == 5 || v == 34;
+        // precisions 1 / 2: 0-3 (the split GEMM's tiles); precision 3: 0, 5, 33 or 34
+        // (the tools build, MH_EXACT_DIAG, also 30 / 31 / 32 / 36: timing diagnostics)
+        bool ok = (v >= 0 && v <= 3) || v == 5 || v == 33 || v == 34;
 #ifdef MH_EXACT_DIAG
-        ok = ok || v == 30 || v == 31;
+        ok = ok || v == 30 || v == 31 || v == 32 || v == 36;
 #endif
-        if (!ok) return fail(h, MHNSW_EINVAL, "exact_tile must be 0-3, 5 or 34");
+        if (!ok) return fail(h, MHNSW_EINVAL, "exact_tile must be 0-3, 5, 33 or 34");
         h->exact_tile = (int)v;
     } else if (n == "beam_mw_max_b") {
         if (v < 0) return fail(h, MHNSW_EINVAL, "beam_mw_max_b must be >= 0");
@@ -1985,6 +1378,13 @@ int mhnsw_add_plan(mhnsw_index* h, const int64_t* keys, int64_t n, int64_t* nwal
     return MHNSW_OK;
 }
 
+int mhnsw_add_reached(const mhnsw_index* h, int64_t* reached) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    if (!reached) return fail(nullptr, MHNSW_EINVAL, "reached must be non-NULL");
+    *reached = h->add_reached;
+    return MHNSW_OK;
+}
+
 int mhnsw_lookup(mhnsw_index* h, int64_t key, float* out) {
     std::shared_lock<std::shared_mutex> lk(h->mu);
     const int32_t r0 = key_row_in(h, key, 0);  // graph.go:906 layers[0].nodes[key]
@@ -2062,558 +1462,7 @@ int mhnsw_export(mhnsw_index* h, int64_t* keys, float* vecs, int32_t* deg, int32
 
 }  // extern "C"
 
-namespace {
-
-// drop every row and layer (Graph.Import replaces the graph, encode.go:208)
-void reset_graph(mhnsw_index* h) {
-    (void)hipStreamSynchronize(h->stream);
-    auto F = [](auto*& p) {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-    };
-    F(h->vecs);
-    F(h->norms);
-    F(h->h16);
-    F(h->h16aux);
-    F(h->keys);
-    F(h->levels);
-    F(h->dead);
-    F(h->cur_entry);
-    F(h->inc_cnt);
-    F(h->inc_src);
-    F(h->inc_dist);
-    for (auto& L : h->layers) {
-        F(L.deg);
-        F(L.adj);
-        F(L.adjd);
-    }
-    h->layers.clear();
-    memset(h->layers_host, 0, sizeof(h->layers_host));
-    h->capn = h->n = 0;
-    h->xsplit_rows = h->xsplit_plane = 0;
-    h->dim = h->pitch = h->lpr = h->vpl = 0;
-    h->layers_exist = h->any_dead = false;
-    F(h->kid);
-    F(h->kidlive);
-    F(h->kprev);
-    h->aliased = false;
-    h->hkid.clear();
-    h->hprev.clear();
-    h->dead_kid.clear();
-    h->key2id.clear();
-    h->hlevels.clear();
-    h->hmask.clear();
-    h->hdead.clear();
-    h->s2l.clear();
-    h->l2s.clear();
-    h->partial_rows = 0;
-    h->xgone_epoch = ~0ull;
-}
-
-int import_csr(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t* keys, const float* vecs,
-               const int32_t* deg, const int32_t* adj, const int32_t* entry, const uint8_t* dead) {
-    if (h->n > 0) return fail(h, MHNSW_EINVAL, "import requires an empty index");
-    if (L > MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "more than %d layers", MH_MAXL);
-    if (cap > 64) return fail(h, MHNSW_EUNSUPPORTED, "degree cap above 64 unsupported");
-    int r;
-    if ((r = set_shape(h, dim))) return r;
-    if ((r = ensure_capacity(h, std::max<int64_t>(N, 1)))) return r;
-    if ((r = ensure_layer(h, L - 1))) return r;
-    // make every layer at least `cap` wide
-    for (int l = 0; l < L; ++l) {
-        Layer& Ly = h->layers[l];
-        if (Ly.cap < cap) {
-            (void)hipFree(Ly.adj);
-            (void)hipFree(Ly.adjd);
-            Ly.adj = nullptr;
-            Ly.adjd = nullptr;
-            Ly.cap = cap;
-            if ((r = grow(h, Ly.adj, 0, h->capn * cap, 0xFF)) || (r = grow(h, Ly.adjd, 0, h->capn * cap, 0))) return r;
-        }
-    }
-    HIPCHK(h, hipMemcpy(h->keys, keys, N * 8, hipMemcpyHostToDevice));
-    if ((r = ensure_buf(h, h->tmp, (size_t)N * dim))) return r;
-    HIPCHK(h, hipMemcpy(h->tmp.p, vecs, (size_t)N * dim * 4, hipMemcpyHostToDevice));
-    LCHK(h, launch_pad_rows(h->tmp.p, N, dim, h->vecs, h->pitch, h->stream));
-    LCHK(h, launch_norms(h->vecs, 0, N, h->pitch, h->lpr, h->vpl, h->norms, h->stream));
-    if ((r = h16_rows(h, 0, N))) return r;
-    h->xsplit_rows = 0;
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    std::vector<int32_t> row;
-    h->hlevels.assign(N, 0);
-    h->hmask.assign(N, 0u);
-    h->hdead.assign(N, 0);
-    h->any_dead = false;
-    for (int64_t i = 0; i < N && dead; ++i) {
-        h->hdead[i] = dead[i] ? 1 : 0;
-        h->any_dead |= dead[i] != 0;
-    }
-    HIPCHK(h, hipMemcpy(h->dead, h->hdead.data(), (size_t)N, hipMemcpyHostToDevice));
-    for (int l = 0; l < L; ++l) {
-        Layer& Ly = h->layers[l];
-        HIPCHK(h, hipMemcpy(Ly.deg, deg + (size_t)l * N, N * 4, hipMemcpyHostToDevice));
-        row.assign((size_t)N * Ly.cap, -1);
-        Ly.count = 0;
-        for (int64_t i = 0; i < N; ++i) {
-            const int d = deg[(size_t)l * N + i];
-            if (d != -2) {
-                h->hmask[i] |= 1u << l;
-                h->hlevels[i] = std::max(h->hlevels[i], l);
-                if (!h->hdead[i]) Ly.count++;
-            }
-            for (int j = 0; j < d && j < cap; ++j) row[(size_t)i * Ly.cap + j] = adj[((size_t)l * N + i) * cap + j];
-        }
-        HIPCHK(h, hipMemcpy(Ly.adj, row.data(), row.size() * 4, hipMemcpyHostToDevice));
-        Ly.entry = entry[l];
-    }
-    HIPCHK(h, hipMemcpy(h->levels, h->hlevels.data(), N * 4, hipMemcpyHostToDevice));
-    // a key's live rows (disjoint layers): the newest heads its chain (key_rows)
-    h->key2id.clear();
-    std::vector<int32_t> prevl((size_t)N, -1);
-    for (int64_t i = 0; i < N; ++i) {
-        if (h->hdead[i]) continue;
-        auto it = h->key2id.find(keys[i]);
-        if (it != h->key2id.end()) prevl[i] = it->second;
-        h->key2id[keys[i]] = (int32_t)i;
-    }
-    h->n = N;
-    h->layers_exist = L > 0;
-    // key identity: several rows of one key (a replaced or re-added key) -> kids
-    std::unordered_map<int64_t, int32_t> first;
-    bool dup = false;
-    for (int64_t i = 0; i < N; ++i) dup |= !first.emplace(keys[i], (int32_t)i).second;
-    h->dead_kid.clear();
-    for (auto& kv : first)
-        if (!h->key2id.count(kv.first)) h->dead_kid[kv.first] = kv.second;
-    if (dup) {
-        if ((r = start_alias(h))) return r;  // kid = row, then rows of repeated keys take the first one's
-        std::vector<int32_t> live((size_t)N, -1);
-        for (int64_t i = 0; i < N; ++i) h->hkid[i] = first[keys[i]];
-        for (auto& kv : h->key2id) live[first[kv.first]] = kv.second;
-        h->hprev = prevl;
-        HIPCHK(h, hipMemcpy(h->kid, h->hkid.data(), (size_t)N * 4, hipMemcpyHostToDevice));
-        HIPCHK(h, hipMemcpy(h->kidlive, live.data(), (size_t)N * 4, hipMemcpyHostToDevice));
-        HIPCHK(h, hipMemcpy(h->kprev, h->hprev.data(), (size_t)N * 4, hipMemcpyHostToDevice));
-    }
-    // live rows outside layer 0 (an exported graph keeps a failed insert's upper rows):
-    // the brute force skips them as the reference's Search cannot reach them
-    h->partial_rows = 0;
-    for (int64_t i = 0; i < N; ++i) h->partial_rows += !h->hdead[i] && !in_layer(h, i, 0);
-    ++h->mut_epoch;
-    return 0;
-}
-
-const char* metric_name(int m) { return m == COSINE ? "cosine" : "euclidean"; }
-
-// ---- Go string keys: order-maintenance labels -------------------------------
-constexpr int64_t SK_LO = -(int64_t(1) << 62), SK_HI = int64_t(1) << 62, SK_STEP = int64_t(1) << 32;
-
-// Re-space every label evenly in string order and rewrite the keys stored on
-// the device (every row, deleted ones included -- compat search can still
-// return them) and in key2id.  Entries with label INT64_MIN are new strings
-// that are not on the device yet.
-int strkey_relabel(mhnsw_index* h) {
-    const int64_t n = (int64_t)h->s2l.size();
-    const int64_t step = (int64_t)(((uint64_t)SK_HI - (uint64_t)SK_LO) / (uint64_t)(n + 1));
-    std::unordered_map<int64_t, int64_t> remap;
-    remap.reserve((size_t)n * 2);
-    int64_t i = 1;
-    for (auto& kv : h->s2l) {
-        const int64_t nl = SK_LO + i++ * step;
-        if (kv.second != INT64_MIN) remap[kv.second] = nl;
-        kv.second = nl;
-    }
-    h->l2s.clear();
-    for (auto& kv : h->s2l) h->l2s[kv.second] = kv.first;
-    if (h->n > 0 && !remap.empty()) {
-        std::vector<int64_t> keys((size_t)h->n);
-        HIPCHK(h, hipStreamSynchronize(h->stream));
-        HIPCHK(h, hipMemcpy(keys.data(), h->keys, (size_t)h->n * 8, hipMemcpyDeviceToHost));
-        for (auto& k : keys) {
-            auto it = remap.find(k);
-            if (it != remap.end()) k = it->second;
-        }
-        HIPCHK(h, hipMemcpy(h->keys, keys.data(), (size_t)h->n * 8, hipMemcpyHostToDevice));
-    }
-    std::unordered_map<int64_t, int32_t> k2;
-    k2.reserve(h->key2id.size() * 2);
-    for (auto& kv : h->key2id) {
-        auto it = remap.find(kv.first);
-        k2[it != remap.end() ? it->second : kv.first] = kv.second;
-    }
-    h->key2id.swap(k2);
-    h->relabels++;
-    return 0;
-}
-
-// Label for a new string: a fixed step past the ends, the midpoint inside;
-// no room left -> relabel everything.
-int strkey_insert(mhnsw_index* h, const std::string& s) {
-    auto it = h->s2l.emplace(s, INT64_MIN).first;
-    const bool first = it == h->s2l.begin();
-    auto nx = std::next(it);
-    const bool last = nx == h->s2l.end();
-    const int64_t prev = first ? SK_LO : std::prev(it)->second;
-    const int64_t next = last ? SK_HI : nx->second;
-    int64_t lab = INT64_MIN;
-    if (last && !first && next - prev > SK_STEP) lab = prev + SK_STEP;
-    else if (first && !last && next - prev > SK_STEP) lab = next - SK_STEP;
-    else if (next - prev >= 2) lab = prev + (next - prev) / 2;
-    if (lab == INT64_MIN) return strkey_relabel(h);
-    it->second = lab;
-    h->l2s[lab] = s;
-    return 0;
-}
-
-// import: distinct strings (file order) -> labels evenly spaced in string order
-void strkey_table(mhnsw_index* h, const std::vector<std::string>& strs, std::vector<int64_t>& lab) {
-    h->s2l.clear();
-    h->l2s.clear();
-    for (const auto& x : strs) h->s2l.emplace(x, INT64_MIN);
-    (void)strkey_relabel(h);  // nothing on the device yet
-    h->relabels--;
-    lab.resize(strs.size());
-    for (size_t i = 0; i < strs.size(); ++i) lab[i] = h->s2l[strs[i]];
-}
-
-bool key_fits(const mhnsw_index* h, int64_t k, int kind) {
-    switch (kind) {
-        case KEY_STRING: return h->l2s.count(k) != 0;
-        case KEY_INT32: return k >= INT32_MIN && k <= INT32_MAX;
-        case KEY_UINT32: return k >= 0 && k <= (int64_t)UINT32_MAX;
-        case KEY_UINT64: return k >= 0;
-        default: return true;
-    }
-}
-
-// encode.go:128-174 Graph.Export: nodes in id (insertion) order, neighbour keys
-// ascending (Go writes both in map order, which is unspecified)
-int export_go(mhnsw_index* h, int key_kind, std::vector<uint8_t>& out) {
-    if (!key_kind_ok(key_kind)) return fail(h, MHNSW_EINVAL, "unsupported key kind %d", key_kind);
-    int r = validate(h);
-    if (r) return r;
-    GoWriter w;
-    w.strs = &h->l2s;
-    w.varint(1);  // encodingVersion
-    w.varint(h->M);
-    w.f64(h->ml);
-    w.varint(h->ef);
-    w.str(metric_name(h->metric));
-    const int L = (int)h->layers.size();
-    w.varint(L);
-    const int64_t N = h->n;
-    std::vector<int64_t> keys((size_t)std::max<int64_t>(N, 1));
-    std::vector<float> vecs((size_t)std::max<int64_t>(N, 1) * std::max(h->dim, 1));
-    if (N > 0) {
-        HIPCHK(h, hipMemcpy(keys.data(), h->keys, N * 8, hipMemcpyDeviceToHost));
-        HIPCHK(h, hipMemcpy2D(vecs.data(), (size_t)h->dim * 4, h->vecs, (size_t)h->pitch * 4, (size_t)h->dim * 4, N,
-                              hipMemcpyDeviceToHost));
-    }
-    std::vector<int32_t> deg, adj;
-    std::vector<int64_t> nb;
-    for (int l = 0; l < L; ++l) {
-        const Layer& Ly = h->layers[l];
-        deg.resize((size_t)N);
-        adj.resize((size_t)N * Ly.cap);
-        if (N > 0) {
-            HIPCHK(h, hipMemcpy(deg.data(), Ly.deg, N * 4, hipMemcpyDeviceToHost));
-            HIPCHK(h, hipMemcpy(adj.data(), Ly.adj, (size_t)N * Ly.cap * 4, hipMemcpyDeviceToHost));
-        }
-        w.varint(Ly.count);
-        for (int64_t i = 0; i < N; ++i) {
-            if (!in_layer(h, i, l) || h->hdead[i]) continue;
-            if (!key_fits(h, keys[i], key_kind)) return fail(h, MHNSW_EINVAL, "key %lld does not fit the key type", (long long)keys[i]);
-            w.key(keys[i], key_kind);
-            w.floats(vecs.data() + (size_t)i * h->dim, h->dim);
-            const int d = std::min(std::max(deg[i], 0), Ly.cap);
-            nb.clear();
-            for (int j = 0; j < d; ++j) nb.push_back(keys[(size_t)adj[(size_t)i * Ly.cap + j]]);
-            std::sort(nb.begin(), nb.end());
-            w.varint(d);
-            for (int64_t k : nb) w.key(k, key_kind);
-        }
-    }
-    out.swap(w.out);
-    return 0;
-}
-
-// encode.go:178-262 Graph.Import.  Neighbour keys that are not nodes of the
-// same layer (dangling edges to deleted nodes in a Go-written file) become nil
-// map entries in the reference; they are dropped here.
-int import_go(mhnsw_index* h, const uint8_t* buf, int64_t size, int key_kind) {
-    GoGraph gg;
-    const std::string e = go_decode(buf, (size_t)std::max<int64_t>(size, 0), key_kind, gg);
-    if (!e.empty()) return fail(h, MHNSW_EINVAL, "%s", e.c_str());
-    h->M = (int)gg.M;
-    h->ml = gg.ml;
-    h->ef = (int)gg.ef;
-    h->metric = gg.dist == "cosine" ? COSINE : EUCLIDEAN;
-    const int L = (int)gg.layers.size();
-    const int64_t N = L ? (int64_t)gg.layers[0].keys.size() : 0;
-    reset_graph(h);
-    if (key_kind == KEY_STRING) {  // ordinals -> evenly spaced labels in string order
-        std::vector<int64_t> lab;
-        strkey_table(h, gg.strkeys, lab);
-        for (auto& Ly : gg.layers) {
-            for (auto& k : Ly.keys) k = lab[(size_t)k];
-            for (auto& k : Ly.nb_keys) k = lab[(size_t)k];
-        }
-    }
-    if (N == 0) return 0;
-    if (L > MH_MAXL) return fail(h, MHNSW_EUNSUPPORTED, "more than %d layers", MH_MAXL);
-    std::unordered_map<int64_t, int32_t> id;
-    id.reserve((size_t)N * 2);
-    for (int64_t j = 0; j < N; ++j) id[gg.layers[0].keys[(size_t)j]] = (int32_t)j;
-    std::vector<int32_t> deg((size_t)L * N, -2), entry((size_t)L, -1);
-    std::vector<uint8_t> member((size_t)N);
-    std::vector<std::vector<int32_t>> rows((size_t)L);  // resolved neighbour ids, CSR per layer
-    std::vector<std::vector<int64_t>> roff((size_t)L);
-    int maxd = 0;
-    for (int l = 0; l < L; ++l) {
-        const GoLayer& G = gg.layers[(size_t)l];
-        std::fill(member.begin(), member.end(), 0);
-        std::vector<int32_t> ids(G.keys.size());
-        for (size_t j = 0; j < G.keys.size(); ++j) {
-            auto it = id.find(G.keys[j]);
-            if (it == id.end())
-                return fail(h, MHNSW_EINVAL, "node %lld of layer %d is missing from layer 0", (long long)G.keys[j], l);
-            ids[j] = it->second;
-            member[(size_t)it->second] = 1;
-            if (entry[(size_t)l] < 0 || it->second < entry[(size_t)l]) entry[(size_t)l] = it->second;
-        }
-        std::vector<int32_t>& R = rows[(size_t)l];
-        std::vector<int64_t>& O = roff[(size_t)l];
-        O.assign((size_t)N + 1, 0);
-        // resolve neighbours, bucket by node id
-        std::vector<int32_t> cnt((size_t)N, 0);
-        std::vector<int32_t> tmp;
-        std::vector<int64_t> tmpo(G.keys.size() + 1, 0);
-        for (size_t j = 0; j < G.keys.size(); ++j) {
-            for (int64_t t = G.nb_off[j]; t < G.nb_off[j + 1]; ++t) {
-                auto it = id.find(G.nb_keys[(size_t)t]);
-                if (it != id.end() && member[(size_t)it->second]) tmp.push_back(it->second);
-            }
-            tmpo[j + 1] = (int64_t)tmp.size();
-            cnt[(size_t)ids[j]] = (int32_t)(tmpo[j + 1] - tmpo[j]);
-            maxd = std::max(maxd, cnt[(size_t)ids[j]]);
-        }
-        for (int64_t i = 0; i < N; ++i) O[(size_t)i + 1] = O[(size_t)i] + cnt[(size_t)i];
-        R.assign((size_t)O[(size_t)N], 0);
-        for (size_t j = 0; j < G.keys.size(); ++j) {
-            const int32_t i = ids[j];
-            deg[(size_t)l * N + i] = cnt[(size_t)i];  // a decoded map is never nil (encode.go:237)
-            std::copy(tmp.begin() + tmpo[j], tmp.begin() + tmpo[j + 1], R.begin() + O[(size_t)i]);
-        }
-    }
-    int cap = 0;
-    for (int l = 0; l < L; ++l) cap = std::max(cap, cap_of(h, l));
-    cap = std::max(cap, maxd);
-    if (cap > 64) return fail(h, MHNSW_EUNSUPPORTED, "degree %d above 64 unsupported", maxd);
-    std::vector<int32_t> adj((size_t)L * N * cap, -1);
-    for (int l = 0; l < L; ++l)
-        for (int64_t i = 0; i < N; ++i)
-            for (int64_t t = roff[(size_t)l][(size_t)i]; t < roff[(size_t)l][(size_t)i + 1]; ++t)
-                adj[((size_t)l * N + i) * cap + (size_t)(t - roff[(size_t)l][(size_t)i])] = rows[(size_t)l][(size_t)t];
-    return import_csr(h, N, gg.dim, L, cap, gg.layers[0].keys.data(), gg.vals0.data(), deg.data(), adj.data(),
-                      entry.data(), nullptr);
-}
-
-}  // namespace
-
 extern "C" {
-
-int mhnsw_import(mhnsw_index* h, int64_t N, int dim, int L, int cap, const int64_t* keys, const float* vecs,
-                 const int32_t* deg, const int32_t* adj, const int32_t* entry, const uint8_t* dead) {
-    std::unique_lock<std::shared_mutex> lk(h->mu);
-    int r = drain(h);
-    if (r) return r;
-    return import_csr(h, N, dim, L, cap, keys, vecs, deg, adj, entry, dead);
-}
-
-int mhnsw_export_go(mhnsw_index* h, int key_kind, uint8_t* buf, int64_t cap, int64_t* size) {
-    std::shared_lock<std::shared_mutex> lk(h->mu);
-    std::vector<uint8_t> out;
-    int r = export_go(h, key_kind, out);
-    if (r) return r;
-    if (size) *size = (int64_t)out.size();
-    if (!buf) return 0;
-    if (cap < (int64_t)out.size())
-        return fail(h, MHNSW_EINVAL, "buffer too small: need %lld bytes", (long long)out.size());
-    memcpy(buf, out.data(), out.size());
-    return 0;
-}
-
-int mhnsw_import_go(mhnsw_index* h, const uint8_t* buf, int64_t size, int key_kind) {
-    std::unique_lock<std::shared_mutex> lk(h->mu);
-    int r = drain(h);
-    if (r) return r;
-    return import_go(h, buf, size, key_kind);
-}
-
-// encode.go:301-327 SavedGraph.Save (renameio): write a uniquely named temp file
-// in the target directory, fsync it, then rename it over path.  Concurrent
-// Saves (the read lock allows them) never share a temp file.
-int mhnsw_save(mhnsw_index* h, const char* path, int key_kind) {
-    std::shared_lock<std::shared_mutex> lk(h->mu);
-    std::vector<uint8_t> out;
-    int r = export_go(h, key_kind, out);
-    if (r) return r;
-    std::string tmpl = std::string(path) + ".tmp.XXXXXX";
-    std::vector<char> name(tmpl.begin(), tmpl.end());
-    name.push_back('\0');
-    const int fd = mkstemp(name.data());
-    if (fd < 0) return fail(h, MHNSW_EINVAL, "create temp file for %s failed", path);
-    size_t off = 0;
-    bool ok = true;
-    while (ok && off < out.size()) {
-        const ssize_t w = write(fd, out.data() + off, out.size() - off);
-        if (w < 0 && errno == EINTR) continue;
-        ok = w > 0;
-        if (ok) off += (size_t)w;
-    }
-    ok = ok && fsync(fd) == 0;
-    ok = (close(fd) == 0) && ok;
-    if (!ok) {
-        unlink(name.data());
-        return fail(h, MHNSW_EINVAL, "write %s failed", name.data());
-    }
-    if (rename(name.data(), path) != 0) {
-        unlink(name.data());
-        return fail(h, MHNSW_EINVAL, "rename to %s failed", path);
-    }
-    return 0;
-}
-
-// encode.go:280-299 LoadSavedGraph: a missing or empty file leaves the graph empty
-int mhnsw_load(mhnsw_index* h, const char* path, int key_kind) {
-    std::unique_lock<std::shared_mutex> lk(h->mu);
-    if (int r0 = drain(h)) return r0;
-    FILE* f = fopen(path, "rb");
-    if (!f) return 0;
-    std::vector<uint8_t> buf;
-    uint8_t tmp[1 << 16];
-    size_t got;
-    while ((got = fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + got);
-    fclose(f);
-    if (buf.empty()) return 0;
-    const int r = import_go(h, buf.data(), (int64_t)buf.size(), key_kind);
-    if (r) return fail(h, r, "import: %s", h->err.c_str());
-    return 0;
-}
-
-// graph.go:1116-1537 SearchWithNegative(s) / BatchSearchWithNegatives
-int mhnsw_search_negatives(mhnsw_index* h, const float* queries, int64_t B, int dim, const float* negatives,
-                           const int32_t* neg_count, int k, float neg_weight, int mode, int ef, int flags,
-                           int64_t* out_keys, float* out_score, int32_t* out_n) {
-    std::unique_lock<std::shared_mutex> lk(h->mu);
-    int r = validate(h);
-    if (r) return r;
-    if (k <= 0) return fail(h, MHNSW_EK, "k must be greater than 0, got %d", k);
-    if (!(neg_weight >= 0.0f && neg_weight <= 1.0f))
-        return fail(h, MHNSW_EINVAL, "negWeight must be between 0.0 and 1.0, got %f", (double)neg_weight);
-    if (h->layers_exist && h->dim != dim)
-        return fail(h, MHNSW_EDIM, "query embedding dimension mismatch: %d != %d", h->dim, dim);
-    if (B <= 0) return 0;
-    for (int64_t b = 0; b < B; ++b) out_n[b] = 0;
-    if (!h->layers_exist || live_count(h) == 0) return 0;  // graph.go:1144-1146
-    const int kx = std::max(3 * k, 10);                    // graph.go:1150-1153
-    if (kx > NEG_MAX_CAND) return fail(h, MHNSW_EUNSUPPORTED, "negatives support k <= %d", NEG_MAX_CAND / 3);
-    // queries without negatives are a plain Search(near, k) (graph.go:1395-1398)
-    std::vector<int64_t> plain, rer;
-    std::vector<int32_t> off(1, 0);
-    for (int64_t b = 0; b < B; ++b) {
-        if (neg_count[b] < 0) return fail(h, MHNSW_EINVAL, "negative count %d for query %lld", neg_count[b], (long long)b);
-        (neg_count[b] == 0 ? plain : rer).push_back(b);
-    }
-    const int64_t ntot = [&] {
-        int64_t t = 0;
-        for (int64_t b = 0; b < B; ++b) t += neg_count[b];
-        return t;
-    }();
-    hipStream_t s = h->stream;
-    if (!plain.empty()) {
-        std::vector<float> q(plain.size() * (size_t)dim);
-        for (size_t i = 0; i < plain.size(); ++i)
-            memcpy(&q[i * dim], queries + (size_t)plain[i] * dim, (size_t)dim * 4);
-        std::vector<int64_t> kk(plain.size() * (size_t)k);
-        std::vector<float> dd(plain.size() * (size_t)k);
-        std::vector<int32_t> nn(plain.size());
-        if ((r = search_impl(h, q.data(), false, (int64_t)plain.size(), dim, k, mode, ef, nullptr, kk.data(), dd.data(),
-                             nn.data(), s, false)))
-            return r;
-        for (size_t i = 0; i < plain.size(); ++i) {
-            memcpy(out_keys + (size_t)plain[i] * k, &kk[i * k], (size_t)k * 8);
-            memcpy(out_score + (size_t)plain[i] * k, &dd[i * k], (size_t)k * 4);
-            out_n[plain[i]] = nn[i];
-        }
-    }
-    if (rer.empty()) return 0;
-    const int64_t R = (int64_t)rer.size();
-    // gather the re-ranked queries and their negatives
-    std::vector<float> q((size_t)R * dim), ng((size_t)std::max<int64_t>(ntot, 1) * dim);
-    std::vector<int64_t> noff_b((size_t)B + 1, 0);
-    for (int64_t b = 0; b < B; ++b) noff_b[(size_t)b + 1] = noff_b[(size_t)b] + neg_count[b];
-    int64_t w = 0;
-    for (int64_t i = 0; i < R; ++i) {
-        const int64_t b = rer[(size_t)i];
-        memcpy(&q[(size_t)i * dim], queries + (size_t)b * dim, (size_t)dim * 4);
-        memcpy(&ng[(size_t)w * dim], negatives + (size_t)noff_b[(size_t)b] * dim, (size_t)neg_count[b] * dim * 4);
-        w += neg_count[b];
-        off.push_back((int32_t)w);
-    }
-    if ((r = ensure_buf(h, h->nq, (size_t)R * dim)) || (r = ensure_buf(h, h->nneg, (size_t)std::max<int64_t>(w, 1) * h->pitch)) ||
-        (r = ensure_buf(h, h->nck, (size_t)R * kx)) || (r = ensure_buf(h, h->ncd, (size_t)R * kx)) ||
-        (r = ensure_buf(h, h->nci, (size_t)R * kx)) || (r = ensure_buf(h, h->ncn, (size_t)R)) ||
-        (r = ensure_buf(h, h->noff, (size_t)R + 1)) || (r = ensure_buf(h, h->nok, (size_t)R * k)) ||
-        (r = ensure_buf(h, h->nos, (size_t)R * k)) || (r = ensure_buf(h, h->non, (size_t)R)))
-        return r;
-    HIPCHK(h, hipMemcpyAsync(h->nq.p, q.data(), q.size() * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(h, hipMemcpyAsync(h->noff.p, off.data(), off.size() * 4, hipMemcpyHostToDevice, s));
-    if (w > 0) {
-        if ((r = ensure_buf(h, h->tmp, (size_t)w * dim))) return r;
-        HIPCHK(h, hipMemcpyAsync(h->tmp.p, ng.data(), (size_t)w * dim * 4, hipMemcpyHostToDevice, s));
-        LCHK(h, launch_pad_rows(h->tmp.p, w, dim, h->nneg.p, h->pitch, s));
-    }
-    // candidates: Search(near, kx) in the requested mode, internal ids kept
-    if ((r = search_impl(h, h->nq.p, true, R, dim, kx, mode, ef, nullptr, h->nck.p, h->ncd.p, h->ncn.p, s, false,
-                         h->nci.p)))
-        return r;
-    if ((r = sync_layer_table(h))) return r;
-    NegArgs a;
-    a.g = graph_view(h);
-    a.neg = h->nneg.p;
-    a.neg_off = h->noff.p;
-    a.cand_ids = h->nci.p;
-    a.cand_d = h->ncd.p;
-    a.cand_n = h->ncn.p;
-    a.B = R;
-    a.kx = kx;
-    a.k = k;
-    a.w = neg_weight;
-    a.flags = flags;
-    a.out_keys = h->nok.p;
-    a.out_score = h->nos.p;
-    a.out_n = h->non.p;
-    LCHK(h, launch_negatives(a, h->lpr, h->vpl, s));
-    std::vector<int64_t> kk((size_t)R * k);
-    std::vector<float> ss((size_t)R * k);
-    std::vector<int32_t> nn((size_t)R);
-    HIPCHK(h, hipMemcpyAsync(kk.data(), h->nok.p, kk.size() * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipMemcpyAsync(ss.data(), h->nos.p, ss.size() * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipMemcpyAsync(nn.data(), h->non.p, nn.size() * 4, hipMemcpyDeviceToHost, s));
-    int err = 0;  // the candidate search and the re-ranking report into d_err[0]
-    HIPCHK(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipStreamSynchronize(s));
-    if (err & 4) return fail(h, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
-    if (err) return fail(h, MHNSW_EINTERNAL, "visited set overflow (raise vis_log2)");
-    for (int64_t i = 0; i < R; ++i) {
-        const int64_t b = rer[(size_t)i];
-        memcpy(out_keys + (size_t)b * k, &kk[(size_t)i * k], (size_t)k * 8);
-        memcpy(out_score + (size_t)b * k, &ss[(size_t)i * k], (size_t)k * 4);
-        out_n[b] = nn[(size_t)i];
-    }
-    return 0;
-}
 
 // graph.go:843-895 Delete / BatchDelete
 // ExactIndex replace-on-Add (hybrid/exact.go:28-59) on a FLAT handle: rows of
@@ -2812,63 +1661,3 @@ int mhnsw_merge_topk_device(const int64_t* keys_in, const float* dist_in, const 
 }
 
 }  // extern "C"
-
-// ---- Go string keys (Graph[string]) ------------------------------------------
-int mhnsw_strkeys_encode(mhnsw_index* h, const char* blob, const int64_t* offs, int64_t n, int assign,
-                         int64_t* out) {
-    std::unique_lock<std::shared_mutex> lk(h->mu);
-    if (n < 0) return fail(h, MHNSW_EINVAL, "negative key count");
-    if (assign) {  // a re-spacing rewrites the stored keys enqueued searches read
-        if (int r0 = drain(h)) return r0;
-    }
-    std::vector<std::string> ks((size_t)n);
-    for (int64_t i = 0; i < n; ++i) {
-        if (offs[i + 1] < offs[i]) return fail(h, MHNSW_EINVAL, "bad string offsets");
-        ks[(size_t)i].assign(blob + offs[i], (size_t)(offs[i + 1] - offs[i]));
-    }
-    int r;
-    if (assign) {
-        std::vector<const std::string*> fresh;
-        for (const auto& x : ks)
-            if (!h->s2l.count(x)) fresh.push_back(&x);
-        std::sort(fresh.begin(), fresh.end(), [](const std::string* a, const std::string* b) { return *a < *b; });
-        fresh.erase(std::unique(fresh.begin(), fresh.end(), [](const std::string* a, const std::string* b) { return *a == *b; }),
-                    fresh.end());
-        if (!fresh.empty()) {
-            if (fresh.size() * 4 > h->s2l.size()) {  // bulk: one even re-spacing
-                for (const auto* x : fresh) h->s2l.emplace(*x, INT64_MIN);
-                if ((r = strkey_relabel(h))) return r;
-            } else {
-                for (const auto* x : fresh)
-                    if ((r = strkey_insert(h, *x))) return r;
-            }
-        }
-    }
-    for (int64_t i = 0; i < n; ++i) {
-        auto it = h->s2l.find(ks[(size_t)i]);
-        out[i] = it == h->s2l.end() ? INT64_MIN : it->second;
-    }
-    return MHNSW_OK;
-}
-
-int mhnsw_strkeys_decode(mhnsw_index* h, const int64_t* labels, int64_t n, char* blob, int64_t cap, int64_t* offs,
-                         int64_t* need) {
-    std::shared_lock<std::shared_mutex> lk(h->mu);
-    int64_t tot = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        auto it = h->l2s.find(labels[i]);
-        if (it != h->l2s.end()) tot += (int64_t)it->second.size();
-    }
-    if (need) *need = tot;
-    if (!blob || cap < tot) return MHNSW_OK;
-    int64_t o = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        offs[i] = o;
-        auto it = h->l2s.find(labels[i]);
-        if (it == h->l2s.end()) continue;
-        memcpy(blob + o, it->second.data(), it->second.size());
-        o += (int64_t)it->second.size();
-    }
-    offs[n] = o;
-    return MHNSW_OK;
-}

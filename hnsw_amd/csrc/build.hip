@@ -860,7 +860,9 @@ __device__ __forceinline__ bool compat_insert(const CompatBuildArgs& a, BuildSme
             for (int j = 0; j < cnt; ++j) {
                 const uint32_t c = rl_u(nbh, j);
                 const bool fresh = staged && nev < 64 && __ballot(lane < nev && evicted == c) == 0ull;
-                const EvictSpec sp{S.prow + j * S.pstride, uni(S.pdeg[j]), S.pdist + j * S.pstride};
+                // the staged row is read only when fresh (S.pdeg / S.prow are null without staging)
+                const EvictSpec sp = fresh ? EvictSpec{S.prow + j * S.pstride, uni(S.pdeg[j]), S.pdist + j * S.pstride}
+                                           : EvictSpec{nullptr, 0, nullptr};
                 const uint32_t w1 = add_neighbor<C, G>(a.g, l, c, id, a.M, S, st, err, ev, fresh, sp);
                 if (w1 != EMPTY_ID) {
                     if (lane == nev) evicted = w1;
@@ -957,16 +959,18 @@ __global__ __launch_bounds__(64 * NW) void k_build_compat_mw(CompatBuildArgs a) 
     const int pt = S.pgroups * S.pstride;
     S.prow = a.spec ? reinterpret_cast<int32_t*>(p) : nullptr;
     p += pt;
-    ev.pc = reinterpret_cast<int32_t*>(p);
+    // without staging (large M: the launch found no room) every staging pointer
+    // stays null -- they lie past the dynamic LDS allocation
+    ev.pc = a.spec ? reinterpret_cast<int32_t*>(p) : nullptr;
     p += pt;
-    ev.pd = reinterpret_cast<float*>(p);
+    ev.pd = a.spec ? reinterpret_cast<float*>(p) : nullptr;
     S.pdist = ev.pd;
     p += pt;
-    S.pdeg = reinterpret_cast<int*>(p);
+    S.pdeg = a.spec ? reinterpret_cast<int*>(p) : nullptr;
     p += 64;
-    ev.pq = p;
+    ev.pq = a.spec ? p : nullptr;
     p += 64;
-    ev.pn = reinterpret_cast<int*>(p);
+    ev.pn = a.spec ? reinterpret_cast<int*>(p) : nullptr;
     ev.ps = S.pstride;
     const int wave = threadIdx.x >> 6;
     if (wave != 0) {

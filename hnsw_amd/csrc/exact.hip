@@ -723,17 +723,23 @@ __device__ __forceinline__ void wait_vm_plus(int extra, std::integer_sequence<in
 // 4 the filter's tests without the record stores (no pair passes: every query
 // takes the canonical fallback, results stay exact).
 // ---------------------------------------------------------------------------
-template <int EPI, int DIAG = 0>
+template <int EPI, int DIAG = 0, int NS = 4, int D = 2>
 __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
-    constexpr int NS = 4, D = 2, PS = 2;
-    static_assert(NS >= D + 2 && D >= 1, "ring depth");
+    constexpr int PS = 2;
+    // WAR: slice x + D overwrites the slot of slice x + D - NS.  NS >= D + 2: its
+    // last reads (group 1) retired two barrier intervals earlier.  NS = D + 1
+    // (RSYNC): group 1 retires its fragment reads before the barrier that ends
+    // its R phase, so they are done when group 0 issues that DMA one interval on.
+    static_assert(NS >= D + 1 && D >= 1, "ring depth");
+    constexpr bool RSYNC = NS < D + 2;
     constexpr int RB = 32 * PS;                // image row bytes (16 PS halves of K)
     constexpr int SL = (G_BM + G_BN) * RB;     // one slice: A then B image
     constexpr int CPR = 2 * PS, RPP = 32 / PS;  // 16-B chunks per row, rows per 1-KiB piece
     // EPI 1: per tile (double-buffered by tile parity) the filter constants, by
     // LDS-DMA: 256 rows x {w0, w1, dead, -} (4 KiB), then c and s of 256 queries
     constexpr int CST = 6144, CSTB = NS * SL;
-    __shared__ __attribute__((aligned(16))) uint8_t ring[NS * SL + (EPI == 1 ? 2 * CST : 0)];
+    constexpr bool CONSTS = EPI == 1 && DIAG != 1;  // the filter constants' LDS copy (not read without an epilogue)
+    __shared__ __attribute__((aligned(16))) uint8_t ring[NS * SL + (CONSTS ? 2 * CST : 0)];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 2, wc = wave & 3;
@@ -967,7 +973,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
             MH_DSR(fb[2], vb, 2048);
             MH_DSR(fb[3], vb, 3072);
         }
-        if (EPI == 1 && c_kt == 0) {
+        if (CONSTS && c_kt == 0) {
             // the filter constants of this tile (read by its epilogue, nkt - 1 >= D
             // slices later: retired by the counted waits in between)
             const int64_t L = first + c_tile * wx;
@@ -999,6 +1005,10 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
             else
                 wait_vmc();
             nst = 0;
+            if constexpr (RSYNC)
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]),
+                               "+v"(fa[6]), "+v"(fa[7]), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]));
         }
         __builtin_amdgcn_s_barrier();
         // M: 32 MFMAs (+ the epilogue after a tile's last slice)
@@ -1042,7 +1052,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     }
 }
 
-template <int EPI, int DIAG = 0>
+template <int EPI, int DIAG = 0, int NS = 4, int D = 2>
 static int launch_h1_pp16_t(const ExactArgs& a, hipStream_t s) {
     if (a.pitch % (X3K * 2)) return -5;
     if (std::max(a.ldQs, a.ldXs) * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return -5;  // 32-bit DMA offsets
@@ -1050,7 +1060,7 @@ static int launch_h1_pp16_t(const ExactArgs& a, hipStream_t s) {
     const int64_t nnt = EPI == 0 && a.nsample_tiles > 0 ? a.nsample_tiles : (a.N + G_BN - 1) / G_BN;
     const int64_t nblk = nqt * nnt;
     const int64_t W = std::min<int64_t>(nblk, std::max(8, device_cus() / 8 * 8));
-    hipLaunchKernelGGL((k_h1_pp16<EPI, DIAG>), dim3((unsigned)W), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((k_h1_pp16<EPI, DIAG, NS, D>), dim3((unsigned)W), dim3(512), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1073,7 +1083,10 @@ static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
 #ifdef MH_EXACT_DIAG
         case 30: return launch_h1_pp16_t<EPI, EPI ? 1 : 0>(a, s);
         case 31: return launch_h1_pp16_t<EPI, EPI ? 4 : 0>(a, s);
+        case 32: return launch_h1_pp16_t<EPI, EPI ? 1 : 0, 5, 3>(a, s);  // no epilogue, 3 slices in flight (160 KiB ring)
+        case 36: return launch_h1_pp16_t<EPI, EPI ? 1 : 0, 4, 3>(a, s);  // no epilogue, 3 in flight, 4-slot ring (RSYNC)
 #endif
+        case 33: return launch_h1_pp16_t<EPI, 0, 4, 3>(a, s);  // 3 slices in flight in the 4-slot ring (RSYNC)
         default: return launch_h1_pp16_t<EPI>(a, s);
     }
 }
@@ -1084,7 +1097,8 @@ int h1_tile_bm(int variant) { return variant == 5 ? 128 : 256; }
 int h1_effective_variant(int variant, int pitch, int64_t ld) {
     const int v = variant == 0 ? 34 : variant;
     if (v == 5) return 5;
-    if (pitch % (X3K * 2) || pitch / (X3K * 2) < 3 || ld * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return 5;
+    const int dslices = v == 33 || v == 32 || v == 36 ? 3 : 2;  // slices in flight
+    if (pitch % (X3K * 2) || pitch / (X3K * 2) < dslices + 1 || ld * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return 5;
     return v;
 }
 
@@ -1113,7 +1127,7 @@ int launch_h1_rowconst(const float* xinv, const float* xnorm, const uint8_t* dea
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 // tools build (MH_EXACT_DIAG): the timing diagnostics, which let no pair pass
-bool h1_timing_diag(int variant) { return variant == 30 || variant == 31; }
+bool h1_timing_diag(int variant) { return variant == 30 || variant == 31 || variant == 32 || variant == 36; }
 // regions per tile of a variant's fused filter (k_h1_pp16: one per wave)
 int h1_region_split(int variant) { return variant == 5 ? 1 : 8; }  // (an effective variant)
 // the variant's regions hold records (H1_REC uint2 each: a lane's 16 accumulators of one

@@ -244,19 +244,51 @@ class Graph:
         return np.array([random_level(self._rng, float(self.Ml), existed or i > 0, base + i) for i in range(n)],
                         np.int32)
 
+    def _rng_snapshot(self):
+        """A way back to the Rng's present state (restore()), or None when the
+        object cannot be copied (then the walk adds one insert per call)."""
+        import copy
+
+        rng = self._rng
+        try:
+            snap = copy.deepcopy(rng)
+        except Exception:  # noqa: BLE001
+            return None
+        if not hasattr(snap, "__dict__"):
+            return None
+
+        def restore():
+            rng.__dict__.clear()
+            rng.__dict__.update(copy.deepcopy(snap.__dict__))
+        return restore
+
     def _walk(self, keys: np.ndarray, add):
         """BatchAdd's walk with levels from the host Rng: draw exactly the levels
         the reference draws -- one per insert it reaches.  mhnsw_add_plan gives
         the inserts up to the next present key (where the walk may stop) and
-        whether an insert may fail (then one insert per call); an error from
+        whether an insert may fail.  Then the whole run goes in one call all the
+        same: on an error, mhnsw_add_reached says how many inserts the walk got
+        to, and the Rng is rewound to the draws of exactly those (one insert per
+        call only for an Rng that cannot be copied).  An error from
         add(lo, hi, levels) ends the walk."""
         nwalk, one = C.c_int64(), C.c_int()
         lo = 0
         while lo < len(keys):
             self._check(load().mhnsw_add_plan(self._h, _ptr(keys[lo:], C.c_int64), len(keys) - lo, C.byref(nwalk),
                                               C.byref(one)))
-            hi = lo + 1 if one.value else lo + nwalk.value
-            add(lo, hi, self._draw_levels(hi - lo))
+            restore = self._rng_snapshot() if one.value else None
+            hi = lo + 1 if (one.value and restore is None) else lo + nwalk.value
+            existed, base = load().mhnsw_num_layers(self._h) > 0, self.Len()
+            try:
+                add(lo, hi, self._draw_levels(hi - lo))
+            except HnswError:
+                if restore is not None:
+                    reached = C.c_int64()
+                    self._check(load().mhnsw_add_reached(self._h, C.byref(reached)))
+                    restore()
+                    for i in range(min(reached.value, hi - lo)):
+                        random_level(self._rng, float(self.Ml), existed or i > 0, base + i)
+                raise
             lo = hi
 
     def set_option(self, name: str, value: int):

@@ -137,9 +137,18 @@ int mhnsw_add_device(mhnsw_index *h, const int64_t *keys, const float *d_vecs, i
  * where a COMPAT walk may stop (it does when that key's node holds a layer at
  * or below the new level); *one_by_one = 1 when an insert may fail with "no
  * nodes found in neighborhood search" (the index holds deleted or replaced
- * rows).  A host draws nwalk levels (1 when one_by_one), adds those nodes,
- * and repeats with the rest until done or an error ends the walk. */
+ * rows).  A host draws nwalk levels, adds those nodes, and repeats with the
+ * rest until done or an error ends the walk.  When one_by_one is set, a host
+ * that can rewind its Rng still adds the nwalk nodes in one call: after an
+ * error, mhnsw_add_reached says how many inserts the walk got to (the draws
+ * the reference made, graph.go:962); the host rewinds and redraws that many.
+ * A host that cannot rewind adds one node per call instead. */
 int mhnsw_add_plan(mhnsw_index *h, const int64_t *keys, int64_t n, int64_t *nwalk, int *one_by_one);
+/* The inserts the last mhnsw_add / mhnsw_add_device walk reached, counting a
+ * replacing insert ("node not added") and a failing one ("no nodes found in
+ * neighborhood search", graph.go:1009) -- i.e. the levels it consumed; 0 after
+ * an error that left the index untouched (validation, dimension, capacity). */
+int mhnsw_add_reached(const mhnsw_index *h, int64_t *reached);
 
 /* ---- Graph.Search / Graph.BatchSearch (graph.go:534-625, 1047-1110) ----
  * B queries of `dim` floats; outputs hold B*k slots; out_n[b] results for

@@ -50,6 +50,7 @@ def lib():
         L.og_last_error.restype = C.c_char_p
         L.og_last_error.argtypes = [C.c_void_p]
         L.og_set_params.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_int, C.c_int]
+        L.og_set_order.argtypes = [C.c_void_p, C.c_int]
         L.og_validate.argtypes = [C.c_void_p]
         L.og_len.restype = C.c_int64
         L.og_len.argtypes = [C.c_void_p]
@@ -152,6 +153,11 @@ class Graph:
 
     def set_params(self, M, Ml, EfSearch, metric):
         lib().og_set_params(self._h, M, Ml, EfSearch, metric)
+
+    def set_order(self, order):
+        """ORDER_REF (sequential fp32, the reference's arithmetic stand-in) or
+        ORDER_DEV (the engine's canonical tree) for every later distance."""
+        self._check(lib().og_set_order(self._h, order))
 
     def validate(self):
         self._check(lib().og_validate(self._h))

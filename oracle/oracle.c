@@ -447,6 +447,12 @@ int og_set_params(og_graph *g, int M, double ml, int ef, int metric) {
     return OG_OK;
 }
 
+int og_set_order(og_graph *g, int order) {
+    if (order != OG_ORDER_REF && order != OG_ORDER_DEV) return set_err(g, OG_EINVAL, "unknown order %d", order);
+    g->order = order;
+    return OG_OK;
+}
+
 int64_t og_len(og_graph *g) { return g->nlayers ? g->layers[0].count : 0; }
 int og_dims(og_graph *g) { return g->layers_exist ? g->dim : 0; }
 int og_num_layers(og_graph *g) { return g->nlayers; }

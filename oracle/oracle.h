@@ -75,6 +75,8 @@ og_graph *og_create(int metric, int order, int M, int M0, double ml, int ef, uin
 void og_destroy(og_graph *g);
 const char *og_last_error(og_graph *g);
 int og_set_params(og_graph *g, int M, double ml, int ef, int metric);
+/* switch the summation order of later distances (the norms are kept for both) */
+int og_set_order(og_graph *g, int order);
 int og_validate(og_graph *g);
 int64_t og_len(og_graph *g);
 int og_dims(og_graph *g);

@@ -12,6 +12,7 @@ graph, the same keys in the same (heap) order, bit-identical distances.
 import numpy as np
 import pytest
 
+from oracle.parity import compare_lists, same_graph
 from tests.test_gpu_parity import _same_graph, _same_results
 
 pytestmark = pytest.mark.gpu
@@ -43,4 +44,12 @@ def test_config0_fullsize_compat_build_and_search(H, O):
     ek, _, en = o.search(Q, k, mode=O.MODE_EXACT)
     rec = np.mean([len(set(gk[b, : gn[b]]) & set(ek[b, : en[b]])) / k for b in range(nq)])
     assert 0.005 < rec < 0.08, rec
+    # ORDER_REF: the reference's arithmetic, the reference's Add and Search
+    r = O.Graph(metric=O.COSINE, order=O.ORDER_REF, M=16, Ml=0.25, EfSearch=20)
+    r.add(keys, X, lv)
+    assert same_graph(g.export(), r.export())
+    pr = compare_lists((gk, gd, gn), r.search(Q, k, mode=O.MODE_COMPAT), k, truth=(ek, en))
+    print("configs[0] GPU compat vs ORDER_REF:", pr)
+    assert pr["recall_delta"] <= 0.002 and pr["max_abs_dist_diff"] <= 1e-5, pr
+    assert pr["identical_lists"] >= 0.99, pr
     g.close()

@@ -8,6 +8,11 @@ graph, plus size-independent properties:
               oracle's brute force on 64 of them; the fp16 screen never changes
               a result (screen on == off, bitwise); lists sorted, keys unique;
               self-queries find themselves; beam recall vs the exact path.
+              The reference's Search() semantics (k_search_compat,
+              graph.go:534-625) on the same 1M graph == the oracle's compat
+              Search (ORDER_DEV) on 2048 queries, bitwise.  Against the
+              reference's arithmetic (ORDER_REF, sequential fp32): beam and
+              compat recall@10 within 0.002, distances within 1e-5.
   configs[2]  1M x 768 Euclidean batched insert (efConstruction 64): a
               well-formed graph (ids in range, no self loops, sets, degree
               caps), beam lists == the oracle's on 1024 queries, exact == the
@@ -111,6 +116,18 @@ def test_fullsize_c2_beam(H, O):
     _same_lists(on, o.search(Qh, 10, mode=O.MODE_BEAM, ef=64, threads=_threads()), "beam")
     sub = np.arange(0, B, B // 64)[:64]
     _same_lists((ek[sub], ed[sub], en[sub]), o.search(Qh[sub], 10, mode=O.MODE_EXACT, threads=_threads()), "exact")
+    # the reference's Search() semantics on the 1M graph (graph.go:534-625), bitwise
+    ck = _search(g, Q, 10, H.MODE_COMPAT, 64)
+    g.device_status()
+    _same_lists(ck, o.search(Qh, 10, mode=O.MODE_COMPAT, ef=64, threads=_threads()), "compat")
+    # the north-star criterion against the reference's arithmetic (ORDER_REF)
+    from oracle.parity import compare_lists
+
+    o.set_order(O.ORDER_REF)
+    for tag, got, mode in (("beam", on, O.MODE_BEAM), ("compat", ck, O.MODE_COMPAT)):
+        pr = compare_lists(got, o.search(Qh, 10, mode=mode, ef=64, threads=_threads()), 10, truth=(ek, en))
+        print(f"configs[1] GPU {tag} vs ORDER_REF:", pr)
+        assert pr["recall_delta"] <= 0.002 and pr["max_abs_dist_diff"] <= 1e-5, (tag, pr)
     del o
     # self-queries: a stored row finds itself first (distance 0 or the -1.19e-7 of parallel vectors)
     ids = np.random.default_rng(5).choice(n, 512, replace=False)

@@ -185,6 +185,55 @@ def test_host_rng_draws_follow_the_walk(H, O):
     _agree(H, O, g, o, Q)
 
 
+@pytest.mark.parametrize("metric", [0, 1])
+def test_host_rng_walk_after_deletes(H, O, metric, monkeypatch):
+    """A host Rng (Go's *rand.Rand stand-in) on an index with deleted rows,
+    where inserts can fail part way (graph.go:1009): each BatchAdd is ONE
+    mhnsw_add call all the same -- after a failure the engine reports how many
+    inserts the walk reached (mhnsw_add_reached) and the host rewinds its Rng
+    to exactly those draws (graph.go:962), so the next Add's levels continue
+    the reference's stream: every step equals the oracle drawing from the same
+    seed itself."""
+    rng = np.random.default_rng(177 + metric)
+    n, d, M = 400, 32, 8
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    Q = rng.uniform(-1, 1, (24, d)).astype(np.float32)
+    keys = np.arange(n, dtype=np.int64) * 2 + 1
+    o = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=0.4, EfSearch=20, seed=31)
+    g = H.Graph(M=M, Ml=0.4, EfSearch=20, Distance=_metric_fn(H, metric), Rng=H.SplitMix64Rand(31))
+    assert _both_add(H, O, g, o, keys, X) is None
+    gone = [int(k) for k in rng.choice(keys, 260, replace=False)]
+    assert o.delete(gone) == g.BatchDelete(gone)
+    _agree(H, O, g, o, Q)
+    lib = H.load()
+    real = lib.mhnsw_add
+    calls = [0]
+
+    def counted(*args):
+        calls[0] += 1
+        return real(*args)
+
+    monkeypatch.setattr(lib, "mhnsw_add", counted)
+    back = list(gone)
+    rng.shuffle(back)
+    errs = adds = 0
+    while back and adds < 60:
+        adds += 1
+        ks, back = back[:12], back[12:]
+        V = rng.uniform(-1, 1, (len(ks), d)).astype(np.float32)
+        err = _both_add(H, O, g, o, ks, V)
+        assert err in (None, "no nodes found in neighborhood search"), err
+        if err is not None:
+            errs += 1
+            ex = o.export()
+            in0 = {int(k) for i, k in enumerate(ex["keys"]) if ex["dead"][i] == 0 and ex["deg"][0, i] != -2}
+            back += [k for k in ks if k not in in0]
+        _agree(H, O, g, o, Q)
+    print({"adds": adds, "failed": errs, "mhnsw_add_calls": calls[0]})
+    assert errs > 0 and calls[0] <= adds, (errs, calls[0], adds)
+    assert g.Len() == len(o)
+
+
 def test_add_plan_and_contains(H):
     g = H.Graph(M=4, Ml=0.25, EfSearch=10, Rng=1)
     X = np.random.default_rng(1).uniform(-1, 1, (10, 8)).astype(np.float32)
@@ -303,10 +352,11 @@ def test_partial_nodes_resolved_per_layer(H, O, metric):
     assert o.delete(gone) == g.BatchDelete(gone)
     _agree(H, O, g, o, Q)
     fresh = 10**6
-    seen = {"continue": 0, "second": 0}
+    seen = {"continue": 0, "second": 0, "went_on": 0}
     for step in range(60):
         part = _partial_keys(o)
         ks, lv = [], []
+        cont_step = False
         if part and step % 2 == 0:
             k = int(rng.choice(list(part)))
             top = max(part[k])
@@ -314,6 +364,7 @@ def test_partial_nodes_resolved_per_layer(H, O, metric):
                 ks.append(k)
                 lv.append(int(rng.integers(min(part[k]), top + 2)))
                 seen["continue"] += 1
+                cont_step = True
             elif min(part[k]) > 0:  # below all of them: a second live node
                 ks.append(k)
                 lv.append(int(rng.integers(0, min(part[k]))))
@@ -327,6 +378,9 @@ def test_partial_nodes_resolved_per_layer(H, O, metric):
         err = _both_add(H, O, g, o, ks, V, np.array(lv, np.int32))
         assert err in (None, "no nodes found in neighborhood search", "node not added"), err
         _agree(H, O, g, o, Q, efs=(16, 40))
+        if cont_step and err is None and len(ks) > 1:  # the walk went on past the swept key
+            assert all(g.Lookup(k)[1] for k in ks[1:]), ks
+            seen["went_on"] += 1
         for k in ks:  # Lookup = layers[0].nodes[key]
             gv, gok = g.Lookup(k)
             ex = o.export()
@@ -338,4 +392,5 @@ def test_partial_nodes_resolved_per_layer(H, O, metric):
             dk = list(_partial_keys(o))[:3] + [int(rng.choice(keys))]
             assert o.delete(dk) == g.BatchDelete(dk)
             _agree(H, O, g, o, Q)
-    assert seen["continue"] + seen["second"] > 0, seen
+    print(seen)
+    assert seen["continue"] > 0 and seen["second"] > 0 and seen["went_on"] > 0, seen

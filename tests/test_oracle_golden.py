@@ -380,3 +380,35 @@ def test_oracle_replacement_walk(O):
             if dd > 0:
                 ks = ex["keys"][ex["adj"][l, i, :dd]].tolist()
                 assert len(ks) == len(set(ks)), (l, i)
+
+
+def test_order_ref_list_parity_config0_shape(O):
+    """The ORDER_DEV -> ORDER_REF step at list level (the north star's "recall@k
+    equal, distances within 1e-5" against the reference's arithmetic): the
+    configs[0] recipe (U[-1,1) cosine at 128-d, M 16, Ml 0.25, EfSearch 20, k 10)
+    on 3,000 rows -- the reference's Add and Search in sequential fp32 vs the
+    engine's summation tree, from the same levels.  The GPU is bit-identical to
+    ORDER_DEV (tests -m gpu), which carries this to the engine; the GPU test
+    repeats it at the full 10k."""
+    from oracle.parity import compare_lists, same_graph
+
+    rng = np.random.default_rng(42)
+    n, d, nq, k = 3000, 128, 300, 10
+    X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    Q = rng.uniform(-1, 1, (nq, d)).astype(np.float32)
+    dev = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=16, Ml=0.25, EfSearch=20, seed=42)
+    lv = dev.preview_levels(n)
+    dev.add(np.arange(n), X, lv)
+    ref = O.Graph(metric=O.COSINE, order=O.ORDER_REF, M=16, Ml=0.25, EfSearch=20)
+    ref.add(np.arange(n), X, lv)
+    assert same_graph(dev.export(), ref.export())
+    ek, _, en = dev.search(Q, k, mode=O.MODE_EXACT)
+    for mode in (O.MODE_COMPAT, O.MODE_BEAM):
+        pr = compare_lists(dev.search(Q, k, mode=mode, ef=20), ref.search(Q, k, mode=mode, ef=20), k, truth=(ek, en))
+        assert pr["recall_delta"] <= 0.002 and pr["max_abs_dist_diff"] <= 1e-5, (mode, pr)
+        assert pr["identical_lists"] >= 0.99, (mode, pr)
+    # one handle, order switched: the same lists
+    dev.set_order(O.ORDER_REF)
+    a = dev.search(Q, k, mode=O.MODE_COMPAT)
+    b = ref.search(Q, k, mode=O.MODE_COMPAT)
+    assert compare_lists(a, b, k, bitwise=True)["identical_lists"] == 1.0
