@@ -227,6 +227,7 @@ class Graph:
 
     @Rng.setter
     def Rng(self, rng):
+        self._pending = []  # draws made ahead from the previous Rng
         if hasattr(rng, "Float64"):
             self._rng = rng
             return
@@ -236,58 +237,57 @@ class Graph:
     def _host_rng(self) -> bool:
         return hasattr(self._rng, "Float64") and self.get_option("build_mode") != 2
 
-    def _draw_levels(self, n: int) -> np.ndarray:
-        """Levels of the next n inserts from the host Rng (graph.go:962), each from
-        the layer-0 size before it (the caller knows those inserts are fresh)."""
+    def _level_draw(self) -> float:
+        """The next level draw: first the draws made ahead for inserts a failed
+        walk never reached (_walk), then the Rng."""
+        if self._pending:
+            return self._pending.pop(0)
+        return self._rng.Float64()
+
+    def _draw_levels(self, n: int):
+        """Levels of the next n inserts (graph.go:962), each from the layer-0
+        size before it (the caller knows those inserts are fresh), and the draws
+        each one consumed."""
         existed = load().mhnsw_num_layers(self._h) > 0
         base = self.Len()
-        return np.array([random_level(self._rng, float(self.Ml), existed or i > 0, base + i) for i in range(n)],
-                        np.int32)
-
-    def _rng_snapshot(self):
-        """A way back to the Rng's present state (restore()), or None when the
-        object cannot be copied (then the walk adds one insert per call)."""
-        import copy
-
-        rng = self._rng
-        try:
-            snap = copy.deepcopy(rng)
-        except Exception:  # noqa: BLE001
-            return None
-        if not hasattr(snap, "__dict__"):
-            return None
-
-        def restore():
-            rng.__dict__.clear()
-            rng.__dict__.update(copy.deepcopy(snap.__dict__))
-        return restore
+        ml = float(self.Ml)
+        levels, draws = [], []
+        for i in range(n):
+            mx = max_level(ml, base + i) if (existed or i > 0) else 1
+            lv, d = mx, []
+            for level in range(mx):  # graph.go:406-416
+                r = self._level_draw()
+                d.append(r)
+                if r > ml:
+                    lv = level
+                    break
+            levels.append(lv)
+            draws.append(d)
+        return np.array(levels, np.int32), draws
 
     def _walk(self, keys: np.ndarray, add):
-        """BatchAdd's walk with levels from the host Rng: draw exactly the levels
-        the reference draws -- one per insert it reaches.  mhnsw_add_plan gives
-        the inserts up to the next present key (where the walk may stop) and
-        whether an insert may fail.  Then the whole run goes in one call all the
-        same: on an error, mhnsw_add_reached says how many inserts the walk got
-        to, and the Rng is rewound to the draws of exactly those (one insert per
-        call only for an Rng that cannot be copied).  An error from
-        add(lo, hi, levels) ends the walk."""
+        """BatchAdd's walk with levels from the host Rng: the reference draws one
+        level per insert it reaches.  mhnsw_add_plan gives the run up to the next
+        present key (where the walk may stop); its levels are drawn ahead and the
+        run goes in one call.  When an insert fails part way (after deletes,
+        graph.go:1009), mhnsw_add_reached says how many inserts the walk got to
+        and the draws made for the ones past them go back to the front of the
+        queue (_level_draw), so the next Add continues the reference's stream.  An
+        error from add(lo, hi, levels) ends the walk."""
         nwalk, one = C.c_int64(), C.c_int()
         lo = 0
         while lo < len(keys):
             self._check(load().mhnsw_add_plan(self._h, _ptr(keys[lo:], C.c_int64), len(keys) - lo, C.byref(nwalk),
                                               C.byref(one)))
-            restore = self._rng_snapshot() if one.value else None
-            hi = lo + 1 if (one.value and restore is None) else lo + nwalk.value
-            existed, base = load().mhnsw_num_layers(self._h) > 0, self.Len()
+            hi = lo + nwalk.value
+            lv, draws = self._draw_levels(hi - lo)
             try:
-                add(lo, hi, self._draw_levels(hi - lo))
+                add(lo, hi, lv)
             except HnswError:
-                if restore is not None:
-                    reached = C.c_int64()
-                    self._check(load().mhnsw_add_reached(self._h, C.byref(reached)))
-                    restore()
-                    for i in range(min(reached.value, hi - lo)):
-                        random_level(self._rng, float(self.Ml), existed or i > 0, base + i)
+                reached = C.c_int64()
+                self._check(load().mhnsw_add_reached(self._h, C.byref(reached)))
+                back = [r for d in draws[reached.value:] for r in d]
+                self._pending[:0] = back
                 raise
             lo = hi
 

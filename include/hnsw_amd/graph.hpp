@@ -79,17 +79,11 @@ inline const DistanceFunc EuclideanDistance{MHNSW_EUCLIDEAN, "euclidean"};  // d
 struct Rand {
     virtual ~Rand() = default;
     virtual double Float64() = 0;  // math/rand (*Rand).Float64
-    // A copy of the present state, restorable with Restore() (nullptr: the
-    // source cannot be rewound, and a walk that may fail adds one node per call).
-    virtual std::unique_ptr<Rand> Clone() const { return nullptr; }
-    virtual void Restore(const Rand&) {}
 };
 
 struct SplitMix64Rand : Rand {
     uint64_t state;
     explicit SplitMix64Rand(uint64_t seed) : state(seed) {}
-    std::unique_ptr<Rand> Clone() const override { return std::make_unique<SplitMix64Rand>(*this); }
-    void Restore(const Rand& o) override { state = static_cast<const SplitMix64Rand&>(o).state; }
     double Float64() override {
         uint64_t z = (state += 0x9E3779B97F4A7C15ull);
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -426,33 +420,48 @@ class Graph {  // graph.go:305-332
         if (!Rng) Rng = defaultRand();
         int64_t nwalk = 0;
         int one = 0;
-        auto draw = [&](int64_t cnt) {
-            const bool existed = mhnsw_num_layers(h_) > 0;
-            const int64_t base = Len();
-            std::vector<int32_t> lv((size_t)cnt);
-            for (int64_t i = 0; i < cnt; ++i) lv[i] = randomLevel(*Rng, Ml, existed || i > 0, base + i);
-            return lv;
+        // one level draw: first what a failed walk handed back, then the Rng
+        auto float64 = [&]() {
+            if (!pending_.empty()) {
+                const double r = pending_.front();
+                pending_.erase(pending_.begin());
+                return r;
+            }
+            return Rng->Float64();
         };
-        // up to the next present key (where the walk may stop); when an insert may
-        // fail, the Rng is snapshotted and, after an error, rewound to the draws of
-        // the inserts the walk reached (mhnsw_add_reached) -- one insert per call
-        // only for an Rng that cannot be cloned; an error ends the walk
+        // up to the next present key (where the walk may stop), every level drawn
+        // ahead (graph.go:388-417, 962); when an insert fails part way (after
+        // deletes, graph.go:1009) the draws made for the inserts past the ones the
+        // walk reached (mhnsw_add_reached) go back to the front of the queue
         for (size_t lo = 0; lo < n;) {
             if (int rc = mhnsw_add_plan(h_, keys.data() + lo, (int64_t)(n - lo), &nwalk, &one))
                 return make_error(rc, h_);
-            std::unique_ptr<Rand> snap = one ? Rng->Clone() : nullptr;
-            const size_t hi = (one && !snap) ? lo + 1 : lo + (size_t)nwalk;
+            const size_t hi = lo + (size_t)nwalk;
             const bool existed = mhnsw_num_layers(h_) > 0;
             const int64_t base = Len();
-            const std::vector<int32_t> lv = draw((int64_t)(hi - lo));
+            std::vector<int32_t> lv(hi - lo);
+            std::vector<std::vector<double>> drawn(hi - lo);
+            for (size_t i = 0; i < hi - lo; ++i) {
+                const int mx = (existed || i > 0) ? maxLevel(Ml, base + (int64_t)i) : 1;
+                lv[i] = mx;
+                for (int level = 0; level < mx; ++level) {
+                    const double r = float64();
+                    drawn[i].push_back(r);
+                    if (r > Ml) {
+                        lv[i] = level;
+                        break;
+                    }
+                }
+            }
             const int rc = mhnsw_add(h_, keys.data() + lo, flat.data() + lo * d, (int64_t)(hi - lo), (int)d, lv.data());
             if (rc < 0) {
                 Error e = make_error(rc, h_);
                 int64_t reached = 0;
-                if (snap && mhnsw_add_reached(h_, &reached) == 0) {
-                    Rng->Restore(*snap);
-                    for (int64_t i = 0; i < reached && i < (int64_t)(hi - lo); ++i)
-                        (void)randomLevel(*Rng, Ml, existed || i > 0, base + i);
+                if (mhnsw_add_reached(h_, &reached) == 0) {
+                    std::vector<double> back;
+                    for (size_t i = (size_t)reached; i < drawn.size(); ++i)
+                        back.insert(back.end(), drawn[i].begin(), drawn[i].end());
+                    pending_.insert(pending_.begin(), back.begin(), back.end());
                 }
                 return e;
             }
@@ -476,6 +485,7 @@ class Graph {  // graph.go:305-332
 
     mhnsw_index* h_ = nullptr;
     std::map<K, Vector> values_;
+    std::vector<double> pending_;  // level draws made ahead for inserts a failed walk never reached
 };
 
 // graph.go:340-348

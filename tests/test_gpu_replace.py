@@ -202,7 +202,7 @@ def test_host_rng_walk_after_deletes(H, O, metric, monkeypatch):
     o = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=0.4, EfSearch=20, seed=31)
     g = H.Graph(M=M, Ml=0.4, EfSearch=20, Distance=_metric_fn(H, metric), Rng=H.SplitMix64Rand(31))
     assert _both_add(H, O, g, o, keys, X) is None
-    gone = [int(k) for k in rng.choice(keys, 260, replace=False)]
+    gone = [int(k) for k in rng.choice(keys, 120, replace=False)]
     assert o.delete(gone) == g.BatchDelete(gone)
     _agree(H, O, g, o, Q)
     lib = H.load()
@@ -230,7 +230,7 @@ def test_host_rng_walk_after_deletes(H, O, metric, monkeypatch):
             back += [k for k in ks if k not in in0]
         _agree(H, O, g, o, Q)
     print({"adds": adds, "failed": errs, "mhnsw_add_calls": calls[0]})
-    assert errs > 0 and calls[0] <= adds, (errs, calls[0], adds)
+    assert 0 < errs < adds and calls[0] <= adds, (errs, calls[0], adds)
     assert g.Len() == len(o)
 
 
@@ -378,9 +378,14 @@ def test_partial_nodes_resolved_per_layer(H, O, metric):
         err = _both_add(H, O, g, o, ks, V, np.array(lv, np.int32))
         assert err in (None, "no nodes found in neighborhood search", "node not added"), err
         _agree(H, O, g, o, Q, efs=(16, 40))
-        if cont_step and err is None and len(ks) > 1:  # the walk went on past the swept key
-            assert all(g.Lookup(k)[1] for k in ks[1:]), ks
-            seen["went_on"] += 1
+        if cont_step and len(ks) > 1:  # the walk went on past the swept key (whatever stopped it later)
+            import ctypes as C
+            reached = C.c_int64()
+            assert H.load().mhnsw_add_reached(g._h, C.byref(reached)) == 0
+            if reached.value >= 2:
+                seen["went_on"] += 1
+            if err is None:
+                assert reached.value == len(ks) and all(g.Lookup(k)[1] for k in ks[1:]), ks
         for k in ks:  # Lookup = layers[0].nodes[key]
             gv, gok = g.Lookup(k)
             ex = o.export()
