@@ -1169,13 +1169,14 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "exact_kk") {
         h->exact_kk = (int)v;
     } else if (n == "exact_tile") {
-        // precisions 1 / 2: 0-3 (the split GEMM's tiles); precision 3: 0, 5, 33 or 34
-        // (the tools build, MH_EXACT_DIAG, also 30 / 31 / 32 / 36: timing diagnostics)
-        bool ok = (v >= 0 && v <= 3) || v == 5 || v == 33 || v == 34;
+        // precisions 1 / 2: 0-3 (the split GEMM's tiles); precision 3: 0, 5 or 34 (the
+        // tools build, MH_EXACT_DIAG, also 30 / 31 / 32 / 36: timing diagnostics, 33: the
+        // ring three slices deep)
+        bool ok = (v >= 0 && v <= 3) || v == 5 || v == 34;
 #ifdef MH_EXACT_DIAG
-        ok = ok || v == 30 || v == 31 || v == 32 || v == 36;
+        ok = ok || v == 30 || v == 31 || v == 32 || v == 33 || v == 36;
 #endif
-        if (!ok) return fail(h, MHNSW_EINVAL, "exact_tile must be 0-3, 5, 33 or 34");
+        if (!ok) return fail(h, MHNSW_EINVAL, "exact_tile must be 0-3, 5 or 34");
         h->exact_tile = (int)v;
     } else if (n == "beam_mw_max_b") {
         if (v < 0) return fail(h, MHNSW_EINVAL, "beam_mw_max_b must be >= 0");

@@ -1085,8 +1085,8 @@ static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
         case 31: return launch_h1_pp16_t<EPI, EPI ? 4 : 0>(a, s);
         case 32: return launch_h1_pp16_t<EPI, EPI ? 1 : 0, 5, 3>(a, s);  // no epilogue, 3 slices in flight (160 KiB ring)
         case 36: return launch_h1_pp16_t<EPI, EPI ? 1 : 0, 4, 3>(a, s);  // no epilogue, 3 in flight, 4-slot ring (RSYNC)
+        case 33: return launch_h1_pp16_t<EPI, 0, 4, 3>(a, s);  // with the epilogue, 3 in flight (RSYNC)
 #endif
-        case 33: return launch_h1_pp16_t<EPI, 0, 4, 3>(a, s);  // 3 slices in flight in the 4-slot ring (RSYNC)
         default: return launch_h1_pp16_t<EPI>(a, s);
     }
 }
@@ -1097,7 +1097,7 @@ int h1_tile_bm(int variant) { return variant == 5 ? 128 : 256; }
 int h1_effective_variant(int variant, int pitch, int64_t ld) {
     const int v = variant == 0 ? 34 : variant;
     if (v == 5) return 5;
-    const int dslices = v == 33 || v == 32 || v == 36 ? 3 : 2;  // slices in flight
+    const int dslices = v == 33 || v == 32 || v == 36 ? 3 : 2;  // slices in flight (33, 32, 36: tools build)
     if (pitch % (X3K * 2) || pitch / (X3K * 2) < dslices + 1 || ld * 32 + G_BM * 32 >= ((int64_t)1 << 32)) return 5;
     return v;
 }
