@@ -375,6 +375,7 @@ def config_harder(device, batch=16384, efs=(64, 128, 256, 512)):
         points.append({"ef": ef, "recall_at_10": round(r, 4), "qps": round(batch / dt, 1), "kernel_ms": round(km, 3),
                        "dist_evals_per_query": round(st["search_dist_evals"] / 3 / batch, 1),
                        "visited_resets_per_query": round(st["visited_resets"] / 3 / batch, 2),
+                       "visited_forgets_per_query": round(st["visited_forgets"] / 3 / batch, 2),
                        "roofline_frac": round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
     g.close()
     return {"workload": f"1M x 768-d cosine, latent dimension 32 (harder than the headline's 12), M=32 M0=63 "

@@ -1178,6 +1178,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
 #endif
         if (!ok) return fail(h, MHNSW_EINVAL, "exact_tile must be 0-3, 5 or 34");
         h->exact_tile = (int)v;
+    } else if (n == "vis_global_mb") {
+        if (v < 0) return fail(h, MHNSW_EINVAL, "vis_global_mb must be >= 0");
+        h->vis_global_mb = v;
     } else if (n == "beam_mw_max_b") {
         if (v < 0) return fail(h, MHNSW_EINVAL, "beam_mw_max_b must be >= 0");
         h->beam_mw_max_b = v;
@@ -1632,10 +1635,10 @@ int mhnsw_stats(const mhnsw_index* h, int64_t* out, int n) {
     HIPCHK(hh, hipMemcpy(err2, h->d_err, sizeof(err2), hipMemcpyDeviceToHost));
     const int err = err2[0] | err2[1];
     if (err & 4) return fail(hh, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
-    const int64_t v[13] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4], (int64_t)d[5], (int64_t)d[6],
+    const int64_t v[14] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4], (int64_t)d[5], (int64_t)d[6],
                            h->stats_host[6], (int64_t)d[3], (int64_t)d[8], (int64_t)d[9], (int64_t)d[10],
-                           (int64_t)d[11], (int64_t)h->build_search_us};
-    for (int i = 0; i < n && i < 13; ++i) out[i] = v[i];
+                           (int64_t)d[11], (int64_t)h->build_search_us, (int64_t)d[12]};
+    for (int i = 0; i < n && i < 14; ++i) out[i] = v[i];
     return 0;
 }
 

@@ -53,7 +53,7 @@ __device__ __forceinline__ void beam_query(const SearchArgs& a, int64_t b, const
     BList<R> L;
     const int efl = a.ef > a.k ? a.ef : a.k;
     if (a.g.layers[0].deg[ep] == -2) ep = (uint32_t)a.layer_entry[0];
-    beam_layer<C, R, G, false, SCREEN, 1>(a.g, 0, ep, efl, q, qn, L, smem, a.vis_n, st, bev);
+    beam_layer<C, R, G, false, SCREEN, 1>(a.g, 0, ep, efl, q, qn, L, smem, a.vis_n, st, bev, a.gvis);
     // compact the sorted list into the first k live entries (deleted rows
     // route the search but are never returned)
     int nvalid = 0;
@@ -85,6 +85,7 @@ __device__ __forceinline__ void beam_stats(const SearchArgs& a, const WaveStats&
         atomicAdd(&a.stats[0], st.E);
         atomicAdd(&a.stats[1], st.X);
         if (st.resets) atomicAdd(&a.stats[2], st.resets);
+        if (st.forgets) atomicAdd(&a.stats[12], st.forgets);
         atomicAdd(&a.stats[8], st.S);
         atomicAdd(&a.stats[9], st.F);
     }

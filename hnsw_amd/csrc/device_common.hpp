@@ -390,6 +390,17 @@ __device__ __forceinline__ float finalize(int metric, float s, float xn, float q
     return sqrtf(s);
 }
 
+// the beam search's global second level of its visited set (device_search.hpp
+// gvis_claim): a pool of `slots` bitmaps of `words` 32-bit words, claimed by a
+// query at its first LDS-set reset through the counter `next` (zeroed before
+// every launch); bits == nullptr: off
+struct GVis {
+    uint32_t* bits = nullptr;
+    int64_t words = 0;
+    int32_t* next = nullptr;
+    int slots = 0;
+};
+
 // ---------------------------------------------------------------------------
 // LDS visited set
 // ---------------------------------------------------------------------------

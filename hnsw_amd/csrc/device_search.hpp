@@ -230,6 +230,7 @@ __device__ __forceinline__ int screen_pairs(const GraphDev& g, const QReg<C>& q,
 
 struct WaveStats {
     unsigned long long E = 0, X = 0, resets = 0;
+    unsigned long long forgets = 0;   // resets that forgot (no global slot: the visited nodes are dropped)
     unsigned long long S = 0, F = 0;  // rows screened on the fp16 copy / rows evaluated in f32
 };
 
@@ -313,10 +314,46 @@ struct WaveBatch {
 // expanded together -- their adjacency rows fetched in one round trip and
 // their new neighbours evaluated as one batch -- which halves the dependent
 // round trips of a search whose expansions yield few new candidates.
+// The beam search's global second level of the visited set (layer 0 of the
+// query searches, engine.hpp GVis).  The LDS set holds 5,120 ids (the LDS its
+// occupancy leaves); a query that fills it claims, at its first reset, one
+// bitmap of the pool (one id per bit, slots never reused within a launch, so no
+// other wave ever touches it; cleared at the claim), copies the LDS set into it
+// before every reset, and from then on a candidate the LDS set calls new is
+// checked against the bitmap (one L2 round trip per expansion) -- the set no
+// longer forgets.  A query that finds the pool exhausted forgets as before;
+// either way the results are the same, only the
+// evaluations differ.
+__device__ __forceinline__ uint32_t* gvis_claim(const GVis& gv) {
+    int s = 0;
+    if (lane_id() == 0) s = atomicAdd(gv.next, 1);
+    s = __shfl(s, 0, 64);
+    if (s >= gv.slots) return nullptr;
+    uint32_t* b = gv.bits + (size_t)s * (size_t)gv.words;
+    uint4* b4 = reinterpret_cast<uint4*>(b);
+    for (int64_t i = lane_id(); i < gv.words / 4; i += 64) b4[i] = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // (vmcnt(0)) the clear is at L2 before the ORs
+    return b;
+}
+__device__ __forceinline__ void gvis_dump(uint32_t* gb, const uint32_t* vis, int vsize) {
+    for (int t = lane_id(); t < vsize; t += 64) {
+        const uint32_t id = vis[t];
+        if (id != VIS_EMPTY)
+            __hip_atomic_fetch_or(gb + (id >> 5), 1u << (id & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // (vmcnt(0)) every OR done before the probes read the words
+}
+__device__ __forceinline__ bool gvis_has(const uint32_t* gb, uint32_t id) {
+    const uint32_t w = __hip_atomic_load(gb + (id >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (w >> (id & 31)) & 1u;
+}
+
 template <class C, int R, int G, bool COH = false, bool SCREEN = false, int XW = 1, class BEv = WaveBatch>
 __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_t entry, int ef, const QReg<C>& q, float qn,
-                           BList<R>& L, uint32_t* vis, int vsize, WaveStats& st, const BEv& bev = BEv()) {
+                           BList<R>& L, uint32_t* vis, int vsize, WaveStats& st, const BEv& bev = BEv(),
+                           const GVis gv = GVis{}) {
     const int lane = lane_id();
+    uint32_t* gb = nullptr;  // this query's bitmap, from its first reset on
     bl_init(L);
     if (entry == EMPTY_ID) return;
     vis_clear(vis, vsize);
@@ -369,6 +406,7 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
                 pr = vis_probe_n(vis, (uint32_t)vsize, nb);
             }
             vcount += __popcll(__ballot(pr == 1));
+            if (gb != nullptr && pr != 0 && gvis_has(gb, nb)) pr = 0;  // visited before a reset
             cids[w] = compact(nb, pr != 0, cnts[w]);
         }
         // the new neighbours of consecutive expanded entries share a batch while
@@ -405,7 +443,13 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
             auto sink = [&](float d, uint32_t u) { bl_insert(L, ef, d, u); };
             st.F += bev.template score<C, G, SCREEN>(g, q, qn, cid, cnt, wd, screen, margin, sink, st.S);
         }
-        if (vcount > MH_VIS_FULL(vsize)) {  // forget: results unchanged
+        if (vcount > MH_VIS_FULL(vsize)) {  // reset: results unchanged
+            if (gv.bits != nullptr && gb == nullptr) gb = gvis_claim(gv);
+            wave_sync();
+            if (gb != nullptr)
+                gvis_dump(gb, vis, vsize);  // remembered: the reset forgets nothing
+            else
+                st.forgets += 1;
             wave_sync();
             vis_clear(vis, vsize);
             wave_sync();

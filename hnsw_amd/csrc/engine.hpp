@@ -46,6 +46,7 @@ struct SearchArgs {
     int vis_n;                    // beam: visited-set entries
     int upper_ef;                 // beam: width of the upper-layer descent (1 = greedy, the reference's k = 1)
     int64_t mw_max_b;             // beam: batches up to this size run a workgroup per query (0 = never)
+    GVis gvis;                    // beam, layer 0: the visited set's global second level
 };
 
 // negative-example re-ranking epilogue (graph.go:1116-1537)

@@ -77,6 +77,7 @@ struct mhnsw_index {
     int compat_waves = 8;     // compat insert: waves scoring each distance batch (1 = the walking wave alone)
     int upper_ef = 1;         // beam search: upper-layer descent width
     int64_t beam_mw_max_b = 512;  // beam search: batches up to this size run one workgroup of 4 waves per query
+    int64_t vis_global_mb = 4096; // beam search: MiB of per-query visited bitmaps behind the LDS set (0 = off)
     int screen = 1;           // beam search / batched insert fp16 screening copy (results unchanged)
     int fuse_descent = 1;     // batched insert: all greedy descents of a batch in one launch (same graph)
     int time_build = 0;       // batched insert: time its search kernels with HIP events (stats [12])
@@ -156,6 +157,8 @@ struct mhnsw_index {
     DevBuf<uint32_t> xsegi;
     DevBuf<uint8_t> xflag;
     DevBuf<uint8_t> xgone;     // exact path: rows to skip when some live row is not in layer 0
+    DevBuf<uint32_t> gvis;     // beam search: the visited set's global second level (GVis bitmaps)
+    DevBuf<int32_t> gvis_next; // ... and its slot counter
     int64_t add_reached = 0;   // inserts the last Add's walk reached (mhnsw_add_reached)
     int64_t partial_rows = 0;  // rows neither deleted nor in layer 0 (left by failed inserts, graph.go:1009)
     uint64_t mut_epoch = 0;            // bumped by every Add / Delete / Import: row membership may have changed

@@ -95,7 +95,10 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * greedy), "beam_mw_max_b" (beam mode, ef and k <= 128: batches of at most this
  * many queries run one workgroup of 4 waves per query -- the single-query
  * latency path of ParallelSearch, graph.go:631-790; default 512, 0 = never;
- * results are identical either way), "screen" (beam mode and batched insert, default 1: keep an fp16
+ * results are identical either way), "vis_global_mb" (beam mode: MiB of per-query
+ * bitmaps behind the LDS visited set -- a query whose set fills keeps the
+ * visited nodes instead of forgetting them; default 4096, 0 = off; results are
+ * identical either way), "screen" (beam mode and batched insert, default 1: keep an fp16
  * copy of the rows; a candidate is skipped only when the copy proves the f32
  * distance rejects it, so results are unchanged);
  * "max_rows" (row capacity limit, 0 = none: an Add that would need more rows
@@ -252,8 +255,10 @@ int mhnsw_preview_levels(mhnsw_index *h, int64_t n, int32_t *out);
  * candidates screened on the fp16 copy, [9] beam candidates evaluated in f32,
  * [10] batched-insert candidates screened on the fp16 copy, [11] batched-insert
  * rows read in f32 (search evaluations + neighbour-selection rows), [12]
- * device time of the batched insert's search kernels in microseconds (option
- * "time_build" = 1: HIP events around each launch) */
+ * device time of the batched insert's kernels (descent, layer searches,
+ * commits) in microseconds (option "time_build" = 1: HIP events around each
+ * layer's launches), [13] visited-set resets that forgot (beam: a query whose
+ * LDS set filled when no global bitmap was left, option "vis_global_mb") */
 int mhnsw_stats(const mhnsw_index *h, int64_t *out, int n);
 int mhnsw_reset_stats(mhnsw_index *h);
 /* device time of the last search's main kernel (HIP events on its stream) */

@@ -9,6 +9,12 @@ oracle's beam search (oracle.c beam_layer_search) never forgets, so running the
 GPU with tiny sets (2^6..2^8 entries, resets on every query) against it checks
 that argument directly, screen on and off.
 
+With the global second level (option vis_global_mb, default on) a query
+whose LDS set fills claims a bitmap in HBM, copies the set into it before every
+reset and checks the candidates the LDS set calls new against it: nothing is
+forgotten, so the evaluations are those of an exact set -- the same results,
+and the same evaluation count as a set that never fills.
+
 Compat mode needs the exact set (graph.go:141-144 keeps a map): an overflow is
 an error.  Asynchronous *_device searches surface it through
 mhnsw_device_status; synchronous calls (host search, negatives) return it.
@@ -44,9 +50,11 @@ def built(H, O):
 @pytest.mark.parametrize("metric", [0, 1])
 @pytest.mark.parametrize("vis_log2", [6, 7, 8])
 @pytest.mark.parametrize("ef", [64, 200])
-def test_beam_forgetting_matches_oracle(H, O, built, metric, vis_log2, ef):
+@pytest.mark.parametrize("gmb", [0, 4096])
+def test_beam_forgetting_matches_oracle(H, O, built, metric, vis_log2, ef, gmb):
     g, o, Q = built[metric]
     rk, rd, rn = o.search(Q, 10, mode=O.MODE_BEAM, ef=ef)
+    g.set_option("vis_global_mb", gmb)
     for screen in (1, 0):
         g.set_option("screen", screen)
         g.set_option("vis_log2", vis_log2)
@@ -54,26 +62,42 @@ def test_beam_forgetting_matches_oracle(H, O, built, metric, vis_log2, ef):
         gk, gd, gn = g.search_arrays(Q, 10, mode=H.MODE_BEAM, ef=ef)
         st = g.stats()
         g.set_option("vis_log2", 12)
-        # every query forgets at least once with sets this small
+        # every query fills its LDS set at least once with sets this small; without the
+        # global level each of those resets forgets, with it none does
         assert st["visited_resets"] >= len(Q), st
+        if gmb:
+            assert st["visited_forgets"] == 0, st
+        else:
+            assert st["visited_forgets"] == st["visited_resets"], st
         _same_results(gk, gd, gn, rk, rd, rn)
     g.set_option("screen", 1)
+    g.set_option("vis_global_mb", 4096)
 
 
-def test_beam_forgetting_costs_only_evaluations(H, built):
-    """same results, more distance evaluations with the smaller set"""
+@pytest.mark.parametrize("gmb", [0, 4096])
+def test_beam_forgetting_costs_only_evaluations(H, built, gmb):
+    """same results; more distance evaluations with the smaller set when it
+    forgets, the same count when the global level remembers"""
     g, _, Q = built[0]
     evals = {}
     res = {}
+    g.set_option("vis_global_mb", gmb)
     for v in (12, 7):
         g.set_option("vis_log2", v)
         g.reset_stats()
         res[v] = g.search_arrays(Q, 10, mode=H.MODE_BEAM, ef=200)
-        evals[v] = g.stats()["search_dist_evals"]
+        st = g.stats()
+        evals[v] = st["search_dist_evals"]
+        if v == 12:
+            assert st["visited_resets"] == 0, st  # the full-size set never fills here
     g.set_option("vis_log2", 12)
+    g.set_option("vis_global_mb", 4096)
     for a, b in zip(res[12], res[7]):
         assert np.array_equal(a, b)
-    assert evals[7] > evals[12]
+    if gmb:
+        assert evals[7] == evals[12], evals
+    else:
+        assert evals[7] > evals[12], evals
 
 
 def _compat_overflow_graph(H, O):
