@@ -368,6 +368,7 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         a.touched_cnt = h->touched_cnt;
         a.stats = h->d_stats + 4;
         a.vis_log2 = h->vis_log2;
+        a.mw_max = h->build_mw_max;
         // time_build: HIP events around every insert kernel (descent, layer searches, commits)
         auto tmark = [&]() -> int {
             if (!h->time_build) return 0;
@@ -1178,6 +1179,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
 #endif
         if (!ok) return fail(h, MHNSW_EINVAL, "exact_tile must be 0-3, 5 or 34");
         h->exact_tile = (int)v;
+    } else if (n == "build_mw_max") {
+        if (v < 0) return fail(h, MHNSW_EINVAL, "build_mw_max must be >= 0");
+        h->build_mw_max = v;
     } else if (n == "vis_global_mb") {
         if (v < 0) return fail(h, MHNSW_EINVAL, "vis_global_mb must be >= 0");
         h->vis_global_mb = v;
@@ -1252,6 +1256,8 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "compat_waves") *v = h->compat_waves;
     else if (n == "upper_ef") *v = h->upper_ef;
     else if (n == "beam_mw_max_b") *v = h->beam_mw_max_b;
+    else if (n == "build_mw_max") *v = h->build_mw_max;
+    else if (n == "vis_global_mb") *v = h->vis_global_mb;
     else if (n == "screen") *v = h->screen;
     else if (n == "fuse_descent") *v = h->fuse_descent;
     else if (n == "time_build") *v = h->time_build;

@@ -115,79 +115,7 @@ __global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
 // are k_search_beam's bit for bit (test_gpu_parity.py: batches below and above
 // BMW_MAX_B compared).
 // ---------------------------------------------------------------------------
-constexpr int BMW_WAVES = 4;
-constexpr int BMW_SCORE = 0, BMW_EXIT = 1;
-struct BmwShare {
-    int cmd, cnt;
-    float wd;
-    int pad_;
-    uint32_t list[64];
-    int scnt[BMW_WAVES];
-    float sd[BMW_WAVES * 64];
-    uint32_t si[BMW_WAVES * 64];
-};
-
-// everything handed between the waves is in LDS (rows and norms are only read)
-__device__ __forceinline__ void bmw_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// wave w's rows of the posted batch, [w*ch, min(cnt, (w+1)*ch)): screened
-// against the posted worst, survivors (f32 distance, id) into sd / si
-template <class C, int G, bool SCREEN>
-__device__ __forceinline__ int bmw_share(const GraphDev& g, const QReg<C>& q, float qn, BmwShare* sh, int w,
-                                         bool screen, float margin, unsigned long long& s16) {
-    const int lane = lane_id();
-    const int cnt = uni(sh->cnt);
-    const float wd = __int_as_float(uni(__float_as_int(sh->wd)));
-    const int ch = (cnt + BMW_WAVES - 1) / BMW_WAVES;
-    const int t0 = w * ch;
-    const int c = min(cnt - t0, ch);
-    int k = 0, f = 0;
-    if (c > 0) {
-        const uint32_t cid = lane < c ? sh->list[t0 + lane] : 0u;
-        auto sink = [&](float d, uint32_t u) {
-            if (lane == 0) {
-                sh->sd[w * 64 + k] = d;
-                sh->si[w * 64 + k] = u;
-            }
-            ++k;
-        };
-        f = WaveBatch().template score<C, G, SCREEN>(g, q, qn, cid, c, wd, screen, margin, sink, s16);
-    }
-    if (lane == 0) sh->scnt[w] = k;
-    return f;
-}
-
-struct MwBatch {
-    BmwShare* sh;
-    template <class C, int G, bool SCREEN, class Sink>
-    __device__ __forceinline__ int score(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int cnt,
-                                         float wd, bool screen, float margin, Sink&& sink,
-                                         unsigned long long& s16) const {
-        const int lane = lane_id();
-        if (lane < cnt) sh->list[lane] = cid;
-        if (lane == 0) {
-            sh->cmd = BMW_SCORE;
-            sh->cnt = cnt;
-            sh->wd = wd;
-        }
-        bmw_barrier();  // post
-        const int f = bmw_share<C, G, SCREEN>(g, q, qn, sh, 0, screen, margin, s16);
-        bmw_barrier();  // collect
-#pragma unroll
-        for (int w = 0; w < BMW_WAVES; ++w) {
-            const int n = uni(sh->scnt[w]);
-            const float dv = lane < n ? sh->sd[w * 64 + lane] : 0.f;
-            const uint32_t iv = lane < n ? sh->si[w * 64 + lane] : 0u;
-            for (int t = 0; t < n; ++t) sink(rl_f(dv, t), rl_u(iv, t));
-        }
-        return f;  // this wave's rows (the others count theirs)
-    }
-};
-
+// (BmwShare, MwBatch: device_search.hpp, shared with the batched insert)
 template <class C, int R, int G, bool SCREEN>
 __global__ __launch_bounds__(64 * BMW_WAVES) void k_search_beam_mw(SearchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];

@@ -1140,35 +1140,26 @@ __global__ __launch_bounds__(64) void k_batch_descend(BatchBuildArgs a) {
 #ifndef MH_BUILD_WPS
 #define MH_BUILD_WPS 1
 #endif
-template <class C, int R, int G, bool SCREEN, int XW>
-__global__ __launch_bounds__(64, MH_BUILD_WPS) void k_batch_search(BatchBuildArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t u;
-    if (a.order) {
-        if (blockIdx.x >= a.count) return;
-        u = a.order[blockIdx.x];
-    } else {
-        const int64_t u64 = a.n0 + blockIdx.x;
-        if (u64 >= a.n1) return;
-        u = (uint32_t)u64;
-    }
+// One insert u of a batch at layer a.layer: greedy descent above u's level,
+// else the layer search (efConstruction), the neighbour selection and the
+// reverse proposals.  bev scores the search's candidate batches (WaveBatch:
+// this wave; MwBatch: the workgroup's waves, k_batch_search_mw).
+template <class C, int R, int G, bool SCREEN, int XW, class BEv>
+__device__ __forceinline__ void batch_insert(const BatchBuildArgs& a, uint32_t u, const QReg<C>& q, float qn,
+                                             uint32_t* smem, WaveStats& st, const BEv& bev) {
     const int lane = lane_id();
     const int l = a.layer;
-    WaveStats st;
-    QReg<C> q;
-    load_query(q, a.g.vecs + (size_t)u * a.g.pitch);
-    const float qn = a.g.norms[u];
     const uint32_t ep = a.cur_entry[u];
     if (a.levels[u] < l) {  // above the node's level: greedy descent only
         BList<1> L1;
-        beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, 1, q, qn, L1, smem, 1 << a.vis_log2, st);
+        beam_layer<C, 1, G, false, SCREEN, 1>(a.g, l, ep, 1, q, qn, L1, smem, 1 << a.vis_log2, st, bev);
         float d;
         uint32_t id;
         bl_at(L1, 0, d, id);
         if (lane == 0 && id != EMPTY_ID) a.cur_entry[u] = id & ID_MASK;
     } else {
         BList<R> L;
-        beam_layer<C, R, G, false, SCREEN, XW>(a.g, l, ep, a.ef, q, qn, L, smem, 1 << a.vis_log2, st);
+        beam_layer<C, R, G, false, SCREEN, XW>(a.g, l, ep, a.ef, q, qn, L, smem, 1 << a.vis_log2, st, bev);
         float d0;
         uint32_t i0;
         bl_at(L, 0, d0, i0);
@@ -1289,12 +1280,79 @@ __global__ __launch_bounds__(64, MH_BUILD_WPS) void k_batch_search(BatchBuildArg
         }
         if (lane == 0) a.g.layers[l].deg[u] = nsel;
     }
-    if (lane == 0) {
+}
+
+__device__ __forceinline__ void batch_stats(const BatchBuildArgs& a, const WaveStats& st) {
+    if (lane_id() == 0) {
         atomicAdd(&a.stats[0], st.E);
         atomicAdd(&a.stats[1], st.X);
         atomicAdd(&a.stats[6], st.S);
         atomicAdd(&a.stats[7], st.F);
     }
+}
+
+__device__ __forceinline__ bool batch_node(const BatchBuildArgs& a, uint32_t& u) {
+    if (a.order) {
+        if (blockIdx.x >= a.count) return false;
+        u = a.order[blockIdx.x];
+    } else {
+        const int64_t u64 = a.n0 + blockIdx.x;
+        if (u64 >= a.n1) return false;
+        u = (uint32_t)u64;
+    }
+    return true;
+}
+
+template <class C, int R, int G, bool SCREEN, int XW>
+__global__ __launch_bounds__(64, MH_BUILD_WPS) void k_batch_search(BatchBuildArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t u;
+    if (!batch_node(a, u)) return;
+    WaveStats st;
+    QReg<C> q;
+    load_query(q, a.g.vecs + (size_t)u * a.g.pitch);
+    const float qn = a.g.norms[u];
+    batch_insert<C, R, G, SCREEN, XW>(a, u, q, qn, smem, st, WaveBatch());
+    batch_stats(a, st);
+}
+
+// Narrow launches (few inserts: the first batches of a build, the upper layers
+// of every batch) leave most of the chip idle and each insert's ~550 dependent
+// expansions on one wave: one workgroup of BMW_WAVES waves per insert splits
+// every candidate batch over the waves (k_search_beam_mw's protocol).  Same
+// graph as k_batch_search, bit for bit (the list keeps the best ef of what is
+// inserted, whatever the order; the screen tests the pre-batch worst on every
+// wave).
+template <class C, int R, int G, bool SCREEN, int XW>
+__global__ __launch_bounds__(64 * BMW_WAVES) void k_batch_search_mw(BatchBuildArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    __shared__ BmwShare sh;
+    uint32_t u;
+    if (!batch_node(a, u)) return;  // (whole workgroup)
+    const int wave = threadIdx.x >> 6;
+    WaveStats st;
+    QReg<C> q;
+    load_query(q, a.g.vecs + (size_t)u * a.g.pitch);
+    const float qn = a.g.norms[u];
+    if (wave == 0) {
+        batch_insert<C, R, G, SCREEN, XW>(a, u, q, qn, smem, st, MwBatch{&sh});
+        if (lane_id() == 0) sh.cmd = BMW_EXIT;
+        bmw_barrier();  // releases the other waves
+    } else {
+        const bool screen = SCREEN && h16_query_ok(qn);
+        float margin = 0.f;
+        if constexpr (SCREEN) {
+            const float e = a.g.h16err ? *a.g.h16err : 0.00048828125f;
+            margin = a.g.metric == EUCLIDEAN ? h16_margin_l2(e) : h16_margin_cos(e);
+        }
+        for (;;) {
+            bmw_barrier();
+            if (sh.cmd == BMW_EXIT) break;
+            st.F += bmw_share<C, G, SCREEN>(a.g, q, qn, &sh, wave, screen, margin, st.S);
+            bmw_barrier();
+        }
+    }
+    batch_stats(a, st);
 }
 
 // One wave per touched node v: merge v's row with the proposals it received.
@@ -1609,7 +1667,9 @@ static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
     if (n <= 0) return 0;
     // fp16 screening: same graph, fewer bytes per candidate; XW = a.expand as a
     // template argument (one search variant per kernel keeps it spill-free)
-    if (a.g.h16 && a.expand == 4)
+    if (a.g.h16 && a.expand == 2 && n <= a.mw_max)  // a narrow launch: a workgroup per insert
+        hipLaunchKernelGGL((k_batch_search_mw<C, R, G, true, 2>), dim3((unsigned)n), dim3(64 * BMW_WAVES), lds, s, a);
+    else if (a.g.h16 && a.expand == 4)
         hipLaunchKernelGGL((k_batch_search<C, R, G, true, 4>), dim3((unsigned)n), dim3(64), lds, s, a);
     else if (a.g.h16 && a.expand == 3)
         hipLaunchKernelGGL((k_batch_search<C, R, G, true, 3>), dim3((unsigned)n), dim3(64), lds, s, a);

@@ -320,8 +320,8 @@ struct WaveBatch {
 // bitmap of the pool (one id per bit, slots never reused within a launch, so no
 // other wave ever touches it; cleared at the claim), copies the LDS set into it
 // before every reset, and from then on a candidate the LDS set calls new is
-// checked against the bitmap (one L2 round trip per expansion) -- the set no
-// longer forgets.  A query that finds the pool exhausted forgets as before;
+// tested against the bitmap and recorded there (one returning L2 atomic per
+// lane, one round trip per expansion) -- the set no longer forgets.  A query that finds the pool exhausted forgets as before;
 // either way the results are the same, only the
 // evaluations differ.
 __device__ __forceinline__ uint32_t* gvis_claim(const GVis& gv) {
@@ -343,9 +343,12 @@ __device__ __forceinline__ void gvis_dump(uint32_t* gb, const uint32_t* vis, int
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // (vmcnt(0)) every OR done before the probes read the words
 }
-__device__ __forceinline__ bool gvis_has(const uint32_t* gb, uint32_t id) {
-    const uint32_t w = __hip_atomic_load(gb + (id >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return (w >> (id & 31)) & 1u;
+// visited before (true), else recorded now: a candidate the LDS set could not
+// record (its probe run congested) is still remembered.  A returning atomic is
+// performed at L2, where every OR went (a plain load may hit a stale L1 line).
+__device__ __forceinline__ bool gvis_test_set(uint32_t* gb, uint32_t id) {
+    const uint32_t bit = 1u << (id & 31);
+    return (__hip_atomic_fetch_or(gb + (id >> 5), bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit) != 0u;
 }
 
 template <class C, int R, int G, bool COH = false, bool SCREEN = false, int XW = 1, class BEv = WaveBatch>
@@ -406,7 +409,7 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
                 pr = vis_probe_n(vis, (uint32_t)vsize, nb);
             }
             vcount += __popcll(__ballot(pr == 1));
-            if (gb != nullptr && pr != 0 && gvis_has(gb, nb)) pr = 0;  // visited before a reset
+            if (gb != nullptr && pr != 0 && gvis_test_set(gb, nb)) pr = 0;  // visited before a reset
             cids[w] = compact(nb, pr != 0, cnts[w]);
         }
         // the new neighbours of consecutive expanded entries share a batch while
@@ -468,6 +471,88 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
         }
     }
 }
+
+// ---------------------------------------------------------------------------
+// several waves per query (or insert): wave 0 runs the list, the visited set
+// and the expansions; each batch of new candidates is split over the waves
+// (screen + f32 on each wave's rows, in one round trip instead of one per 16
+// rows) and the survivors come back to wave 0's list.  The list is the best ef
+// of everything inserted whatever the insertion order, so the results are the
+// one-wave kernel's bit for bit (k_search_beam_mw, k_batch_search_mw).
+// ---------------------------------------------------------------------------
+constexpr int BMW_WAVES = 4;
+constexpr int BMW_SCORE = 0, BMW_EXIT = 1;
+struct BmwShare {
+    int cmd, cnt;
+    float wd;
+    int pad_;
+    uint32_t list[64];
+    int scnt[BMW_WAVES];
+    float sd[BMW_WAVES * 64];
+    uint32_t si[BMW_WAVES * 64];
+};
+
+// everything handed between the waves is in LDS (rows and norms are only read)
+__device__ __forceinline__ void bmw_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// wave w's rows of the posted batch, [w*ch, min(cnt, (w+1)*ch)): screened
+// against the posted worst, survivors (f32 distance, id) into sd / si
+template <class C, int G, bool SCREEN>
+__device__ __forceinline__ int bmw_share(const GraphDev& g, const QReg<C>& q, float qn, BmwShare* sh, int w,
+                                         bool screen, float margin, unsigned long long& s16) {
+    const int lane = lane_id();
+    const int cnt = uni(sh->cnt);
+    const float wd = __int_as_float(uni(__float_as_int(sh->wd)));
+    const int ch = (cnt + BMW_WAVES - 1) / BMW_WAVES;
+    const int t0 = w * ch;
+    const int c = min(cnt - t0, ch);
+    int k = 0, f = 0;
+    if (c > 0) {
+        const uint32_t cid = lane < c ? sh->list[t0 + lane] : 0u;
+        auto sink = [&](float d, uint32_t u) {
+            if (lane == 0) {
+                sh->sd[w * 64 + k] = d;
+                sh->si[w * 64 + k] = u;
+            }
+            ++k;
+        };
+        f = WaveBatch().template score<C, G, SCREEN>(g, q, qn, cid, c, wd, screen, margin, sink, s16);
+    }
+    if (lane == 0) sh->scnt[w] = k;
+    return f;
+}
+
+struct MwBatch {
+    BmwShare* sh;
+    template <class C, int G, bool SCREEN, class Sink>
+    __device__ __forceinline__ int score(const GraphDev& g, const QReg<C>& q, float qn, uint32_t cid, int cnt,
+                                         float wd, bool screen, float margin, Sink&& sink,
+                                         unsigned long long& s16) const {
+        const int lane = lane_id();
+        if (lane < cnt) sh->list[lane] = cid;
+        if (lane == 0) {
+            sh->cmd = BMW_SCORE;
+            sh->cnt = cnt;
+            sh->wd = wd;
+        }
+        bmw_barrier();  // post
+        const int f = bmw_share<C, G, SCREEN>(g, q, qn, sh, 0, screen, margin, s16);
+        bmw_barrier();  // collect
+#pragma unroll
+        for (int w = 0; w < BMW_WAVES; ++w) {
+            const int n = uni(sh->scnt[w]);
+            const float dv = lane < n ? sh->sd[w * 64 + lane] : 0.f;
+            const uint32_t iv = lane < n ? sh->si[w * 64 + lane] : 0u;
+            for (int t = 0; t < n; ++t) sink(rl_f(dv, t), rl_u(iv, t));
+        }
+        return f;  // this wave's rows (the others count theirs)
+    }
+};
+
 
 // ---------------------------------------------------------------------------
 // compat: graph.go:94-170 verbatim semantics on LDS Go-heaps

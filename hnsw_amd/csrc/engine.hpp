@@ -143,6 +143,7 @@ struct BatchBuildArgs {
     int vis_log2;
     const uint32_t* order;        // nullable: node of workgroup b is order[b] (b < count), nodes sorted by
     int64_t count;                //   level descending so that level >= layer is a prefix
+    int64_t mw_max = 0;           // launches of at most this many inserts: one workgroup of 4 waves per insert
 };
 int launch_build_batch_search(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s);
 // greedy descent of every node u in [n0, n1) through layers a.layer .. levels[u] + 1

@@ -141,6 +141,16 @@ def test_screened_batch_build_identical(H, metric, alpha):
     for key in ((1, 0), (0, 1), (1, 1)):
         _same_graph(ex[(0, 0)], ex[key])
     assert f32[(1, 0)] < 0.6 * f32[(0, 0)]  # the selection's rows were mostly decided on the copy
+    # the 4-wave insert kernel (k_batch_search_mw: the screened searches' narrow launches by
+    # default) on every launch, and on none: the same graph again
+    for mw in (1 << 30, 0):
+        g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
+                    ef_construction=80, heuristic=2, keep_pruned=1, screen=1, prune_alpha_pct=alpha,
+                    build_mw_max=mw)
+        g.add_arrays(np.arange(n // 3), X[: n // 3])
+        g.add_arrays(np.arange(n // 3, n), X[n // 3:])
+        _same_graph(ex[(0, 0)], g.export())
+        g.close()
     # one entry expanded per step of the insert's layer searches (build_expand 1; the default
     # 2 expands two): a different graph, but again the same with and without the screen
     ex2 = []

@@ -15,6 +15,7 @@
 #     diag:T,...         the same on tools/libmhnsw_diag.so (timing-diagnostic variants; needs the .so
 #                        pushed: take ./tools/libmhnsw_*.so out of .gpurunignore for that call)
 #     yard               rocprofv3 stats of tools/gemm_yardstick.py (torch fp16 matmul, configs[4] shape)
+#     cprof              compat Add cycle accounting (tools/libmhnsw_cprof.so, tools/cprof_probe.py + cprof_sum.py)
 set -o pipefail
 TAG=$1
 shift
@@ -42,6 +43,8 @@ for step in "$@"; do
     py) timeout -k 10 900 python -u $args > "$log" 2>&1 ;;
     gemm) timeout -k 10 900 bash tools/gemm_diag.sh $args > "$log" 2>&1 ;;
     diag) MHNSW_LIB=$PWD/tools/libmhnsw_diag.so timeout -k 10 900 bash tools/gemm_diag.sh $args > "$log" 2>&1 ;;
+    cprof) MHNSW_LIB=$PWD/tools/libmhnsw_cprof.so timeout -k 10 600 python -u tools/cprof_probe.py > "$log" 2>&1 &&
+        python tools/cprof_sum.py "$log" > "$O/$i.cprof_sum.txt" ;;
     yard) (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/yard" \
         -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/gemm_yardstick.py" 20) > "$log" 2>&1 ;;
     *) echo "unknown step $step" >&2; exit 8 ;;
