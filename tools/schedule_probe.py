@@ -4,7 +4,8 @@ slack 1.15): build time and recall@10 at ef 64 (4,096 queries vs the exact
 path) per batch schedule.  A batch of b new nodes is searched against the
 graph as it stood before the batch, so the schedule (batch_min, batch_ratio_pct,
 batch_max) trades early-phase launches for within-batch links.
-Usage: BUILD_OPTS="batch_min=1;batch_min=256,batch_ratio_pct=10" python tools/schedule_probe.py"""
+Usage: BUILD_OPTS="batch_min=1;batch_min=256,batch_ratio_pct=10" python tools/schedule_probe.py
+   or: python tools/schedule_probe.py "batch_min=1;batch_min=256+batch_ratio_pct=10"""
 import os
 import sys
 import time
@@ -36,7 +37,9 @@ else:
     Q = gen_vectors(4096, d, 1234 + 7777, 12, 1000, dev, "cosine")
     base = dict(Distance=H.CosineDistance, Rng=1234, m0=40, ef_construction=400, heuristic=2, keep_pruned=1,
                 prune_alpha_pct=115)
-sets = [dict(kv.split("=") for kv in s_.split(",") if kv) for s_ in os.environ.get("BUILD_OPTS", "").split(";")]
+# option sets: BUILD_OPTS, or argv[1] with "+" between one set's options (tools/gpu_run.sh splits steps at commas)
+spec = sys.argv[1].replace("+", ",") if len(sys.argv) > 1 else os.environ.get("BUILD_OPTS", "")
+sets = [dict(kv.split("=") for kv in s_.split(",") if kv) for s_ in spec.split(";")]
 truth = None
 for opts in sets:
     kw = dict(base)
