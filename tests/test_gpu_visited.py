@@ -13,7 +13,8 @@ With the global second level (option vis_global_mb, default on) a query
 whose LDS set fills claims a bitmap in HBM, copies the set into it before every
 reset and checks the candidates the LDS set calls new against it: nothing is
 forgotten, so the evaluations are those of an exact set -- the same results,
-and the same evaluation count as a set that never fills.
+and the evaluation count of a set that never fills (but for candidates whose
+LDS probe congested before the query's first reset).
 
 Compat mode needs the exact set (graph.go:141-144 keeps a map): an overflow is
 an error.  Asynchronous *_device searches surface it through
@@ -94,10 +95,10 @@ def test_beam_forgetting_costs_only_evaluations(H, built, gmb):
     g.set_option("vis_global_mb", 4096)
     for a, b in zip(res[12], res[7]):
         assert np.array_equal(a, b)
-    if gmb:
-        assert evals[7] == evals[12], evals
+    if gmb:  # (a candidate whose LDS probe run congested before the first reset is not recorded anywhere)
+        assert evals[12] <= evals[7] <= evals[12] * 1.001, evals
     else:
-        assert evals[7] > evals[12], evals
+        assert evals[7] > 1.1 * evals[12], evals
 
 
 def _compat_overflow_graph(H, O):
