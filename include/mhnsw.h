@@ -100,7 +100,7 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * visited nodes instead of forgetting them; default 4096, 0 = off; results are
  * identical either way), "build_mw_max" (batched insert: a layer launch of at most this
  * many inserts runs one workgroup of 4 waves per insert, the candidate batches of
- * its searches split over the waves; default 512, 0 = never; the same graph
+ * its searches split over the waves; default 256, 0 = never; the same graph
  * either way), "screen" (beam mode and batched insert, default 1: keep an fp16
  * copy of the rows; a candidate is skipped only when the copy proves the f32
  * distance rejects it, so results are unchanged);
