@@ -15,7 +15,7 @@ import torch  # noqa: E402
 import hnsw_amd as H  # noqa: E402
 from bench import Searcher, gen_vectors  # noqa: E402
 
-efs = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "64,512").split(",")]
+efs = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "64,512").replace("+", ",").split(",")]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 1_000_000
 gmbs = [int(x) for x in (sys.argv[4] if len(sys.argv) > 4 else "4096").split("+")]
