@@ -1368,125 +1368,131 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
     __shared__ uint32_t ri[128];
     const int lane = lane_id();
     const int n_t = *a.touched_cnt;
-    if ((int)blockIdx.x >= n_t) return;
-    const uint32_t v = a.touched[blockIdx.x];
-    const int l = a.layer;
-    const int capl = a.g.layers[l].cap;
-    const int keep_cap = min(capl, a.mcap);
-    int32_t* row = a.g.layers[l].adj + (size_t)v * capl;
-    float* rowd = a.g.layers[l].adjd + (size_t)v * capl;
-    int d = a.g.layers[l].deg[v];
-    if (d < 0) d = 0;
-    int nin = a.inc_cnt[v];
-    if (nin > a.inc_cap) nin = a.inc_cap;
-    const int tot = d + nin;
-    for (int e = lane; e < 128; e += 64) {
-        float dd = __int_as_float(0x7f800000);
-        uint32_t ii = EMPTY_ID;
-        if (e < d) {
-            ii = (uint32_t)row[e];
-            dd = rowd[e];
-        } else if (e < tot) {
-            ii = a.inc_src[(size_t)v * a.inc_cap + (e - d)];
-            dd = a.inc_dist[(size_t)v * a.inc_cap + (e - d)];
-        }
-        sd[e] = dd;
-        si[e] = ii;
-    }
-    __syncthreads();
-    // rank = number of entries ordered before this one by (dist, id)
-    for (int h = 0; h < 2; ++h) {
-        const int e = lane + 64 * h;
-        const float md = sd[e];
-        const uint32_t mi = si[e];
-        int rank = 0;
-        for (int f = 0; f < tot; ++f) rank += lt_di(sd[f], si[f], md, mi) ? 1 : 0;
-        if (e < tot) {
-            rd[rank] = md;
-            ri[rank] = mi;
-        }
-    }
-    __syncthreads();
-    int nkeep = 0;
-    if (tot <= keep_cap || a.heuristic < 2) {
-        nkeep = min(tot, keep_cap);
-        for (int e = lane; e < nkeep; e += 64) {
-            row[e] = (int32_t)ri[e];
-            rowd[e] = rd[e];
-        }
-    } else {
-        uint32_t kept = 0;   // lane j holds the j-th kept id
-        float keptd = 0.f;
-        WaveStats st;
-        // with the fp16 copy: kept-row-major, as k_batch_search's selection
-        // (drop_pass; the same decisions as the candidate-major loop below)
-        const bool rowmajor = a.g.h16 != nullptr && a.alpha > 0.f;
-        if (rowmajor) {
-            const float e = a.g.h16err ? *a.g.h16err : 0.00048828125f;
-            const float margin = a.g.metric == EUCLIDEAN ? h16_margin_l2(e) : h16_margin_cos(e);
-            uint32_t live = 0u, dropped = 0u;
-            uint32_t eid[2];
-            float ed[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int e2 = lane + 64 * h;
-                if (e2 < tot) live |= 1u << h;
-                eid[h] = e2 < tot ? guard_id(a.g, ri[e2]) : 0u;
-                ed[h] = rd[e2];
+    // grid-stride over the touched rows: a bounded grid (at most 32,768
+    // workgroups) instead of one workgroup per row the batch could touch (mcap
+    // per insert: 8M for a 200k batch at M0 40, nearly all of which would only
+    // read the count and exit)
+    for (int t = blockIdx.x; t < n_t; t += gridDim.x) {
+        const uint32_t v = a.touched[t];
+        const int l = a.layer;
+        const int capl = a.g.layers[l].cap;
+        const int keep_cap = min(capl, a.mcap);
+        int32_t* row = a.g.layers[l].adj + (size_t)v * capl;
+        float* rowd = a.g.layers[l].adjd + (size_t)v * capl;
+        int d = a.g.layers[l].deg[v];
+        if (d < 0) d = 0;
+        int nin = a.inc_cnt[v];
+        if (nin > a.inc_cap) nin = a.inc_cap;
+        const int tot = d + nin;
+        for (int e = lane; e < 128; e += 64) {
+            float dd = __int_as_float(0x7f800000);
+            uint32_t ii = EMPTY_ID;
+            if (e < d) {
+                ii = (uint32_t)row[e];
+                dd = rowd[e];
+            } else if (e < tot) {
+                ii = a.inc_src[(size_t)v * a.inc_cap + (e - d)];
+                dd = a.inc_dist[(size_t)v * a.inc_cap + (e - d)];
             }
-            int pos = 0;
-            while (nkeep < keep_cap) {
-                int idx = -1;
-#pragma unroll
+            sd[e] = dd;
+            si[e] = ii;
+        }
+        __syncthreads();
+        // rank = number of entries ordered before this one by (dist, id)
+        for (int h = 0; h < 2; ++h) {
+            const int e = lane + 64 * h;
+            const float md = sd[e];
+            const uint32_t mi = si[e];
+            int rank = 0;
+            for (int f = 0; f < tot; ++f) rank += lt_di(sd[f], si[f], md, mi) ? 1 : 0;
+            if (e < tot) {
+                rd[rank] = md;
+                ri[rank] = mi;
+            }
+        }
+        __syncthreads();
+        int nkeep = 0;
+        if (tot <= keep_cap || a.heuristic < 2) {
+            nkeep = min(tot, keep_cap);
+            for (int e = lane; e < nkeep; e += 64) {
+                row[e] = (int32_t)ri[e];
+                rowd[e] = rd[e];
+            }
+        } else {
+            uint32_t kept = 0;   // lane j holds the j-th kept id
+            float keptd = 0.f;
+            WaveStats st;
+            // with the fp16 copy: kept-row-major, as k_batch_search's selection
+            // (drop_pass; the same decisions as the candidate-major loop below)
+            const bool rowmajor = a.g.h16 != nullptr && a.alpha > 0.f;
+            if (rowmajor) {
+                const float e = a.g.h16err ? *a.g.h16err : 0.00048828125f;
+                const float margin = a.g.metric == EUCLIDEAN ? h16_margin_l2(e) : h16_margin_cos(e);
+                uint32_t live = 0u, dropped = 0u;
+                uint32_t eid[2];
+                float ed[2];
+    #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const unsigned long long m = __ballot(((live & ~dropped) >> h & 1u) && h * 64 + lane >= pos);
-                    if (idx < 0 && m) idx = h * 64 + __ffsll((long long)m) - 1;
+                    const int e2 = lane + 64 * h;
+                    if (e2 < tot) live |= 1u << h;
+                    eid[h] = e2 < tot ? guard_id(a.g, ri[e2]) : 0u;
+                    ed[h] = rd[e2];
                 }
-                if (idx < 0) break;
-                const uint32_t c = ri[idx];
-                if (lane == nkeep) {
-                    kept = c;
-                    keptd = rd[idx];
+                int pos = 0;
+                while (nkeep < keep_cap) {
+                    int idx = -1;
+    #pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const unsigned long long m = __ballot(((live & ~dropped) >> h & 1u) && h * 64 + lane >= pos);
+                        if (idx < 0 && m) idx = h * 64 + __ffsll((long long)m) - 1;
+                    }
+                    if (idx < 0) break;
+                    const uint32_t c = ri[idx];
+                    if (lane == nkeep) {
+                        kept = c;
+                        keptd = rd[idx];
+                    }
+                    ++nkeep;
+                    pos = idx + 1;
+                    if (nkeep >= keep_cap) break;
+                    QReg<C> qr;
+                    const uint32_t cg = guard_id(a.g, c);
+                    load_query(qr, a.g.vecs + (size_t)cg * a.g.pitch);
+                    drop_pass<C, G, 2>(a.g, qr, a.g.norms[cg], pos, live, dropped, eid, ed, a.alpha, margin, st);
                 }
-                ++nkeep;
-                pos = idx + 1;
-                if (nkeep >= keep_cap) break;
-                QReg<C> qr;
-                const uint32_t cg = guard_id(a.g, c);
-                load_query(qr, a.g.vecs + (size_t)cg * a.g.pitch);
-                drop_pass<C, G, 2>(a.g, qr, a.g.norms[cg], pos, live, dropped, eid, ed, a.alpha, margin, st);
             }
-        }
-        for (int i = 0; !rowmajor && i < tot && nkeep < keep_cap; ++i) {
-            const uint32_t c = ri[i];
-            const float dcv = rd[i];
-            bool good = true;
-            if (nkeep > 0) {
-                QReg<C> qc;
-                load_query(qc, a.g.vecs + (size_t)guard_id(a.g, c) * a.g.pitch);
-                const float cn = a.g.norms[guard_id(a.g, c)];
-                st.E += nkeep;
-                eval_list<C, G>(a.g, qc, cn, kept, nkeep, a.g.metric, [&](float dcs, uint32_t) {
-                    if (a.alpha * dcs < dcv) good = false;
-                });
-            }
-            if (good) {
-                if (lane == nkeep) {
-                    kept = c;
-                    keptd = dcv;
+            for (int i = 0; !rowmajor && i < tot && nkeep < keep_cap; ++i) {
+                const uint32_t c = ri[i];
+                const float dcv = rd[i];
+                bool good = true;
+                if (nkeep > 0) {
+                    QReg<C> qc;
+                    load_query(qc, a.g.vecs + (size_t)guard_id(a.g, c) * a.g.pitch);
+                    const float cn = a.g.norms[guard_id(a.g, c)];
+                    st.E += nkeep;
+                    eval_list<C, G>(a.g, qc, cn, kept, nkeep, a.g.metric, [&](float dcs, uint32_t) {
+                        if (a.alpha * dcs < dcv) good = false;
+                    });
                 }
-                ++nkeep;
+                if (good) {
+                    if (lane == nkeep) {
+                        kept = c;
+                        keptd = dcv;
+                    }
+                    ++nkeep;
+                }
             }
+            if (lane < nkeep) {
+                row[lane] = (int32_t)kept;
+                rowd[lane] = keptd;
+            }
+            if (lane == 0) atomicAdd(&a.stats[0], st.E);
         }
-        if (lane < nkeep) {
-            row[lane] = (int32_t)kept;
-            rowd[lane] = keptd;
+        if (lane == 0) {
+            a.g.layers[l].deg[v] = nkeep;
+            a.inc_cnt[v] = 0;
         }
-        if (lane == 0) atomicAdd(&a.stats[0], st.E);
-    }
-    if (lane == 0) {
-        a.g.layers[l].deg[v] = nkeep;
-        a.inc_cnt[v] = 0;
+        __syncthreads();  // (the LDS rank arrays are reused by the next row)
     }
 }
 
@@ -1767,7 +1773,7 @@ int MH_PARTFN(launch_build_batch_commit)(const BatchBuildArgs& a, int lpr, int v
     if (max_touched <= 0) return 0;
 #define X_(L, V, G)                                                                                   \
     if (lpr == L && vpl == V) {                                                                       \
-        hipLaunchKernelGGL((k_batch_commit<Cfg<L, V>, (G < 4 ? G : 4)>), dim3((unsigned)max_touched), \
+        hipLaunchKernelGGL((k_batch_commit<Cfg<L, V>, (G < 4 ? G : 4)>), dim3((unsigned)std::min<int64_t>(max_touched, 32768)), \
                            dim3(64), 0, s, a);                                                        \
         return hipGetLastError() == hipSuccess ? 0 : -1;                                              \
     }
