@@ -92,7 +92,7 @@ __device__ __forceinline__ void beam_stats(const SearchArgs& a, const WaveStats&
 }
 
 template <class C, int R, int G, bool SCREEN>
-__global__ __launch_bounds__(64) void k_search_beam(SearchArgs a) {
+__global__ __launch_bounds__(64, 2) void k_search_beam(SearchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int64_t b = blockIdx.x;
     if (b >= a.B) return;
