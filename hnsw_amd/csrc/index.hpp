@@ -77,7 +77,7 @@ struct mhnsw_index {
     int compat_waves = 8;     // compat insert: waves scoring each distance batch (1 = the walking wave alone)
     int upper_ef = 1;         // beam search: upper-layer descent width
     int64_t beam_mw_max_b = 512;  // beam search: batches up to this size run one workgroup of 4 waves per query
-    int64_t vis_global_mb = 4096; // beam search: MiB of per-query visited bitmaps behind the LDS set (0 = off)
+    int64_t vis_global_mb = 0;    // beam search: MiB of per-query visited bitmaps behind the LDS set (0 = off)
     int64_t build_mw_max = 256;   // batched insert: launches of at most this many inserts run 4 waves per insert
     int screen = 1;           // beam search / batched insert fp16 screening copy (results unchanged)
     int fuse_descent = 1;     // batched insert: all greedy descents of a batch in one launch (same graph)

@@ -97,8 +97,9 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * latency path of ParallelSearch, graph.go:631-790; default 512, 0 = never;
  * results are identical either way), "vis_global_mb" (beam mode: MiB of per-query
  * bitmaps behind the LDS visited set -- a query whose set fills keeps the
- * visited nodes instead of forgetting them; default 4096, 0 = off; results are
- * identical either way), "build_mw_max" (batched insert: a layer launch of at most this
+ * visited nodes instead of forgetting them; default 0 = off: the extra round
+ * trip per expansion costs what the saved evaluations give back (DESIGN.md
+ * section 7); results are identical either way), "build_mw_max" (batched insert: a layer launch of at most this
  * many inserts runs one workgroup of 4 waves per insert, the candidate batches of
  * its searches split over the waves; default 256, 0 = never; the same graph
  * either way), "screen" (beam mode and batched insert, default 1: keep an fp16

@@ -9,7 +9,7 @@ oracle's beam search (oracle.c beam_layer_search) never forgets, so running the
 GPU with tiny sets (2^6..2^8 entries, resets on every query) against it checks
 that argument directly, screen on and off.
 
-With the global second level (option vis_global_mb, default on) a query
+With the global second level (option vis_global_mb > 0, default off) a query
 whose LDS set fills claims a bitmap in HBM, copies the set into it before every
 reset and checks the candidates the LDS set calls new against it: nothing is
 forgotten, so the evaluations are those of an exact set -- the same results,
@@ -72,7 +72,7 @@ def test_beam_forgetting_matches_oracle(H, O, built, metric, vis_log2, ef, gmb):
             assert st["visited_forgets"] == st["visited_resets"], st
         _same_results(gk, gd, gn, rk, rd, rn)
     g.set_option("screen", 1)
-    g.set_option("vis_global_mb", 4096)
+    g.set_option("vis_global_mb", 0)
 
 
 @pytest.mark.parametrize("gmb", [0, 4096])
@@ -92,7 +92,7 @@ def test_beam_forgetting_costs_only_evaluations(H, built, gmb):
         if v == 12:
             assert st["visited_resets"] == 0, st  # the full-size set never fills here
     g.set_option("vis_log2", 12)
-    g.set_option("vis_global_mb", 4096)
+    g.set_option("vis_global_mb", 0)
     for a, b in zip(res[12], res[7]):
         assert np.array_equal(a, b)
     if gmb:  # (a candidate whose LDS probe run congested before the first reset is not recorded anywhere)
