@@ -202,7 +202,7 @@ def test_host_rng_walk_after_deletes(H, O, metric, monkeypatch):
     o = O.Graph(metric=metric, order=O.ORDER_DEV, M=M, Ml=0.25, EfSearch=20, seed=31)
     g = H.Graph(M=M, Ml=0.25, EfSearch=20, Distance=_metric_fn(H, metric), Rng=H.SplitMix64Rand(31))
     assert _both_add(H, O, g, o, keys, X) is None
-    gone = [int(k) for k in rng.choice(keys, 60, replace=False)]
+    gone = [int(k) for k in rng.choice(keys, 45, replace=False)]
     assert o.delete(gone) == g.BatchDelete(gone)
     _agree(H, O, g, o, Q)
     lib = H.load()
@@ -338,7 +338,7 @@ def test_partial_nodes_resolved_per_layer(H, O, metric):
         graph.go:997-1003, 574), Lookup to the layer-0 one, Delete removes both.
     Ops are driven identically on the engine and the oracle; every step agrees
     (rows, adjacency, errors, compat / beam / exact results)."""
-    rng = np.random.default_rng(900 + metric)
+    rng = np.random.default_rng(921)  # (a stream where a swept key's walk goes on, both metrics)
     n, d, M = 600, 8, 6
     X = rng.uniform(-1, 1, (n, d)).astype(np.float32)
     keys = np.arange(n, dtype=np.int64) * 3 + 1
@@ -348,7 +348,7 @@ def test_partial_nodes_resolved_per_layer(H, O, metric):
     Q = rng.uniform(-1, 1, (24, d)).astype(np.float32)
     # delete most of the graph, then add keys back at high levels: elevators through
     # deleted nodes fail inserts part way
-    gone = [int(k) for k in rng.choice(keys, int(0.7 * n), replace=False)]
+    gone = [int(k) for k in rng.choice(keys, int(0.6 * n), replace=False)]
     assert o.delete(gone) == g.BatchDelete(gone)
     _agree(H, O, g, o, Q)
     fresh = 10**6
