@@ -43,7 +43,7 @@ import hnsw_amd as H  # noqa: E402
 
 # revision of the search/build kernels the recorded PMC passes (profiles/*_pmc_*.json)
 # were taken on; a pass recorded on another revision is not attached as `traffic`
-KERNEL_REV = "r04"
+KERNEL_REV = "r05"
 from hnsw_amd.shard import engine_local_search, gather_topk, merge_topk, shard_range, sharded_search  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -94,8 +94,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline time box (0 disables)")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
     p.add_argument("--one-gpu", action="store_true", help="map every rank to cuda:0 (multi-rank rehearsal)")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04_pmc_search.json"))
-    p.add_argument("--pmc-build-json", default=os.path.join(ROOT, "profiles", "r04_pmc_build.json"))
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r05_pmc_search.json"))
+    p.add_argument("--pmc-build-json", default=os.path.join(ROOT, "profiles", "r05_pmc_build.json"))
     return p.parse_args()
 
 
@@ -199,7 +199,7 @@ def build_roofline(bs, secs, n, dim, m0, metric, traffic=None):
                          "achieved": round(gbs, 1) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None,
                          "wall_frac": round(byts / secs / 1e9 / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "traffic_kernel": "k_batch_search"}}
+                         "traffic": traffic}}
 
 
 def list_checksum(keys, dists, n):
@@ -375,7 +375,6 @@ def config_harder(device, batch=16384, efs=(64, 128, 256, 512)):
         points.append({"ef": ef, "recall_at_10": round(r, 4), "qps": round(batch / dt, 1), "kernel_ms": round(km, 3),
                        "dist_evals_per_query": round(st["search_dist_evals"] / 3 / batch, 1),
                        "visited_resets_per_query": round(st["visited_resets"] / 3 / batch, 2),
-                       "visited_forgets_per_query": round(st["visited_forgets"] / 3 / batch, 2),
                        "roofline_frac": round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
     g.close()
     return {"workload": f"1M x 768-d cosine, latent dimension 32 (harder than the headline's 12), M=32 M0=63 "
@@ -655,8 +654,9 @@ def main():
             tk, tn = ek, en
 
     def build_traffic(n):
-        """HBM bytes of k_batch_search from a separate rocprofv3 --pmc pass of this
-        same configuration (tools/profile_round.sh), when one is recorded"""
+        """HBM bytes of the three insert kernels (k_batch_descend, k_batch_search[_mw],
+        k_batch_commit) summed over the build, from separate rocprofv3 --pmc passes of
+        this same configuration (tools/profile_round.sh), when one is recorded"""
         try:
             pm = json.load(open(a.pmc_build_json))
             want = dict(n=n, dim=a.dim, efc=a.efc, m0=a.M0, keep_pruned=a.keep_pruned, alpha=a.alpha,

@@ -343,7 +343,7 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         HIPCHK(h, hipEventRecord(h->ord_ev, h->stream));
         h->ord_pending = true;
     }
-    for (int l = top; l >= 0; --l) {
+    auto args = [&](int l) {
         const int mcap = l == 0 ? m0_of(h) : h->M;
         BatchBuildArgs a;
         a.order = nullptr;
@@ -369,17 +369,24 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         a.stats = h->d_stats + 4;
         a.vis_log2 = h->vis_log2;
         a.mw_max = h->build_mw_max;
-        // time_build: HIP events around every insert kernel (descent, layer searches, commits)
-        auto tmark = [&]() -> int {
-            if (!h->time_build) return 0;
-            if (h->tev_used == h->tev.size()) {
-                hipEvent_t e;
-                HIPCHK(h, hipEventCreate(&e));
-                h->tev.push_back(e);
-            }
-            HIPCHK(h, hipEventRecord(h->tev[h->tev_used++], h->stream));
-            return 0;
-        };
+        // the compact visited set where it holds more than the 32-bit one in about the same LDS
+        a.vis16 = h->vis_compact && h->capn <= (int64_t(1) << 24) && h->vis_log2 >= 12 && h->vis_log2 <= 13;
+        return a;
+    };
+    // time_build: HIP events around every insert kernel (descent, layer searches, commits)
+    auto tmark = [&]() -> int {
+        if (!h->time_build) return 0;
+        if (h->tev_used == h->tev.size()) {
+            hipEvent_t e;
+            HIPCHK(h, hipEventCreate(&e));
+            h->tev.push_back(e);
+        }
+        HIPCHK(h, hipEventRecord(h->tev[h->tev_used++], h->stream));
+        return 0;
+    };
+    for (int l = top; l >= 0; --l) {
+        BatchBuildArgs a = args(l);
+        const int mcap = a.mcap;
         if (fuse) {
             if (l == top) {
                 if ((r = tmark())) return r;
@@ -1182,9 +1189,6 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "build_mw_max") {
         if (v < 0) return fail(h, MHNSW_EINVAL, "build_mw_max must be >= 0");
         h->build_mw_max = v;
-    } else if (n == "vis_global_mb") {
-        if (v < 0) return fail(h, MHNSW_EINVAL, "vis_global_mb must be >= 0");
-        h->vis_global_mb = v;
     } else if (n == "beam_mw_max_b") {
         if (v < 0) return fail(h, MHNSW_EINVAL, "beam_mw_max_b must be >= 0");
         h->beam_mw_max_b = v;
@@ -1194,6 +1198,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "fuse_descent") {
         if (v != 0 && v != 1) return fail(h, MHNSW_EINVAL, "fuse_descent must be 0 or 1");
         h->fuse_descent = (int)v;
+    } else if (n == "vis_compact") {
+        if (v != 0 && v != 1) return fail(h, MHNSW_EINVAL, "vis_compact must be 0 or 1");
+        h->vis_compact = (int)v;
     } else if (n == "time_build") {
         h->time_build = (int)(v != 0);
     } else if (n == "max_rows") {
@@ -1257,9 +1264,9 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "upper_ef") *v = h->upper_ef;
     else if (n == "beam_mw_max_b") *v = h->beam_mw_max_b;
     else if (n == "build_mw_max") *v = h->build_mw_max;
-    else if (n == "vis_global_mb") *v = h->vis_global_mb;
     else if (n == "screen") *v = h->screen;
     else if (n == "fuse_descent") *v = h->fuse_descent;
+    else if (n == "vis_compact") *v = h->vis_compact;
     else if (n == "time_build") *v = h->time_build;
     else if (n == "max_rows") *v = h->max_rows;
     else if (n == "strkey_relabels") *v = h->relabels;
@@ -1641,10 +1648,10 @@ int mhnsw_stats(const mhnsw_index* h, int64_t* out, int n) {
     HIPCHK(hh, hipMemcpy(err2, h->d_err, sizeof(err2), hipMemcpyDeviceToHost));
     const int err = err2[0] | err2[1];
     if (err & 4) return fail(hh, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
-    const int64_t v[14] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4], (int64_t)d[5], (int64_t)d[6],
+    const int64_t v[13] = {(int64_t)d[0], (int64_t)d[1], (int64_t)d[2], (int64_t)d[4], (int64_t)d[5], (int64_t)d[6],
                            h->stats_host[6], (int64_t)d[3], (int64_t)d[8], (int64_t)d[9], (int64_t)d[10],
-                           (int64_t)d[11], (int64_t)h->build_search_us, (int64_t)d[12]};
-    for (int i = 0; i < n && i < 14; ++i) out[i] = v[i];
+                           (int64_t)d[11], (int64_t)h->build_search_us};
+    for (int i = 0; i < n && i < 13; ++i) out[i] = v[i];
     return 0;
 }
 

@@ -34,6 +34,7 @@ template <class C, int R, int G, bool SCREEN, class BEv>
 __device__ __forceinline__ void beam_query(const SearchArgs& a, int64_t b, const QReg<C>& q, float qn, uint32_t* smem,
                                            WaveStats& st, const BEv& bev) {
     const int lane = lane_id();
+    const int vsz = a.vis16 ? -1 : a.vis_n;  // (beam_layer: < 0 selects the compact set)
     uint32_t ep = a.entry;
     {
         BList<1> L1;
@@ -43,7 +44,7 @@ __device__ __forceinline__ void beam_query(const SearchArgs& a, int64_t b, const
                 if (e < 0) continue;
                 ep = (uint32_t)e;
             }
-            beam_layer<C, 1, G, false, SCREEN, 1>(a.g, l, ep, a.upper_ef, q, qn, L1, smem, a.vis_n, st, bev);
+            beam_layer<C, 1, G, false, SCREEN, 1>(a.g, l, ep, a.upper_ef, q, qn, L1, smem, vsz, st, bev);
             float d;
             uint32_t id;
             bl_at(L1, 0, d, id);
@@ -53,7 +54,7 @@ __device__ __forceinline__ void beam_query(const SearchArgs& a, int64_t b, const
     BList<R> L;
     const int efl = a.ef > a.k ? a.ef : a.k;
     if (a.g.layers[0].deg[ep] == -2) ep = (uint32_t)a.layer_entry[0];
-    beam_layer<C, R, G, false, SCREEN, 1>(a.g, 0, ep, efl, q, qn, L, smem, a.vis_n, st, bev, a.gvis);
+    beam_layer<C, R, G, false, SCREEN, 1>(a.g, 0, ep, efl, q, qn, L, smem, vsz, st, bev);
     // compact the sorted list into the first k live entries (deleted rows
     // route the search but are never returned)
     int nvalid = 0;
@@ -85,7 +86,6 @@ __device__ __forceinline__ void beam_stats(const SearchArgs& a, const WaveStats&
         atomicAdd(&a.stats[0], st.E);
         atomicAdd(&a.stats[1], st.X);
         if (st.resets) atomicAdd(&a.stats[2], st.resets);
-        if (st.forgets) atomicAdd(&a.stats[12], st.forgets);
         atomicAdd(&a.stats[8], st.S);
         atomicAdd(&a.stats[9], st.F);
     }

@@ -1103,6 +1103,15 @@ __device__ __forceinline__ void drop_pass(const GraphDev& g, const QReg<C>& qr, 
     }
 }
 
+// the insert searches' visited set: 2^vis_log2 32-bit entries, or (vis16) the
+// compact set -- 8,192 ids in 16 KiB where 2^12 entries held 4,096 (fewer
+// resets, fewer re-evaluated candidates; the same lists, so the same graph)
+__device__ __forceinline__ int batch_vsize(const BatchBuildArgs& a) { return a.vis16 ? -1 : 1 << a.vis_log2; }
+static size_t batch_lds(const BatchBuildArgs& a) {
+    const size_t v = (size_t)4 << a.vis_log2;
+    return a.vis16 ? std::max(v, (size_t)VIS16_WORDS * 4) : v;
+}
+
 // Greedy descent (ef = 1) of every new node through the layers above its own
 // level, all layers in one launch.  Every layer l is read before its commit
 // (run_batch_layers commits layer l only after this kernel), exactly what the
@@ -1122,7 +1131,7 @@ __global__ __launch_bounds__(64) void k_batch_descend(BatchBuildArgs a) {
     uint32_t ep = a.cur_entry[u];
     for (int l = a.layer; l > lv; --l) {
         BList<1> L1;
-        beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, 1, q, qn, L1, smem, 1 << a.vis_log2, st);
+        beam_layer<C, 1, G, false, SCREEN>(a.g, l, ep, 1, q, qn, L1, smem, batch_vsize(a), st);
         float d;
         uint32_t id;
         bl_at(L1, 0, d, id);
@@ -1152,14 +1161,14 @@ __device__ __forceinline__ void batch_insert(const BatchBuildArgs& a, uint32_t u
     const uint32_t ep = a.cur_entry[u];
     if (a.levels[u] < l) {  // above the node's level: greedy descent only
         BList<1> L1;
-        beam_layer<C, 1, G, false, SCREEN, 1>(a.g, l, ep, 1, q, qn, L1, smem, 1 << a.vis_log2, st, bev);
+        beam_layer<C, 1, G, false, SCREEN, 1>(a.g, l, ep, 1, q, qn, L1, smem, batch_vsize(a), st, bev);
         float d;
         uint32_t id;
         bl_at(L1, 0, d, id);
         if (lane == 0 && id != EMPTY_ID) a.cur_entry[u] = id & ID_MASK;
     } else {
         BList<R> L;
-        beam_layer<C, R, G, false, SCREEN, XW>(a.g, l, ep, a.ef, q, qn, L, smem, 1 << a.vis_log2, st, bev);
+        beam_layer<C, R, G, false, SCREEN, XW>(a.g, l, ep, a.ef, q, qn, L, smem, batch_vsize(a), st, bev);
         float d0;
         uint32_t i0;
         bl_at(L, 0, d0, i0);
@@ -1656,7 +1665,7 @@ static int launch_delete_compat_t(const DeleteArgs& a, hipStream_t s) {
 
 template <class C, int G>
 static int launch_batch_descend_t(const BatchBuildArgs& a, hipStream_t s) {
-    const size_t lds = (size_t)4 << a.vis_log2;
+    const size_t lds = batch_lds(a);
     const int64_t n = a.n1 - a.n0;
     if (n <= 0) return 0;
     if (a.g.h16)
@@ -1668,7 +1677,7 @@ static int launch_batch_descend_t(const BatchBuildArgs& a, hipStream_t s) {
 
 template <class C, int R, int G>
 static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
-    const size_t lds = (size_t)4 << a.vis_log2;
+    const size_t lds = batch_lds(a);
     const int64_t n = a.order ? a.count : a.n1 - a.n0;
     if (n <= 0) return 0;
     // fp16 screening: same graph, fewer bytes per candidate; XW = a.expand as a

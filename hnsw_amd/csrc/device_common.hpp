@@ -390,17 +390,6 @@ __device__ __forceinline__ float finalize(int metric, float s, float xn, float q
     return sqrtf(s);
 }
 
-// the beam search's global second level of its visited set (device_search.hpp
-// gvis_claim): a pool of `slots` bitmaps of `words` 32-bit words, claimed by a
-// query at its first LDS-set reset through the counter `next` (zeroed before
-// every launch); bits == nullptr: off
-struct GVis {
-    uint32_t* bits = nullptr;
-    int64_t words = 0;
-    int32_t* next = nullptr;
-    int slots = 0;
-};
-
 // ---------------------------------------------------------------------------
 // LDS visited set
 // ---------------------------------------------------------------------------
@@ -435,6 +424,49 @@ __device__ __forceinline__ int vis_probe_n(uint32_t* tab, uint32_t size, uint32_
         if (old == VIS_EMPTY) return 1;
         if (old == id) return 0;
         h = h + 1 == size ? 0u : h + 1;
+    }
+    return 2;
+}
+
+// Compact set (beam search, node ids < 2^24): 16-bit entries, exact.  A
+// bijection x of the 24-bit id splits into a home slot (its low 13 bits) and a
+// tag (its high 11 bits); the entry stores tag | disp << 11, disp = slot - home
+// (linear probing without wrap, 0..30, over 8,192 + 32 slots).  Slot and entry
+// together give back x, hence the id: a match is the id itself, never a false
+// positive.  0xFFFF (tag 2047 with disp 31, which never occurs) is empty.  Two
+// entries share a 32-bit LDS word; an insert is a CAS of the whole word.  It
+// holds 8,192 ids in 16 KiB where the 32-bit set holds 5,120 in 20 KiB.
+constexpr int VIS16_HOMES = 1 << 13;
+constexpr int VIS16_SLOTS = VIS16_HOMES + 32;
+constexpr int VIS16_WORDS = VIS16_SLOTS / 2;  // 32-bit words (16,448 B)
+constexpr int VIS16_MAXD = 31;                // probes per id (disp 0..30)
+__device__ __forceinline__ uint32_t vis16_mix(uint32_t id) {  // a bijection on [0, 2^24)
+    uint32_t x = (id * 0x9E3779u) & 0xFFFFFFu;  // odd multiplier: invertible mod 2^24
+    x ^= x >> 12;                                 // invertible xorshift
+    return (x * 0x2C1B3Du) & 0xFFFFFFu;           // odd again
+}
+// 0 = already visited, 1 = newly recorded, 2 = congested (not recorded)
+__device__ __forceinline__ int vis16_probe(uint32_t* tab, uint32_t id) {
+    const uint32_t x = vis16_mix(id);
+    const uint32_t home = x & (uint32_t)(VIS16_HOMES - 1), tag = x >> 13;
+    uint32_t cur = 0xFFFFFFFFu;  // guess: the word is empty (the CAS returns it as it is)
+#pragma unroll 1
+    for (uint32_t d = 0; d < (uint32_t)VIS16_MAXD; ++d) {
+        const uint32_t s = home + d;
+        const uint32_t want = tag | (d << 11);
+        const uint32_t sh = (s & 1u) << 4;
+        uint32_t* w = tab + (s >> 1);
+        if (d > 0 && !(s & 1u)) cur = 0xFFFFFFFFu;  // a new word: guess again (an odd slot's word is known)
+#pragma unroll 1
+        for (;;) {
+            const uint32_t e = (cur >> sh) & 0xFFFFu;
+            if (e == want) return 0;
+            if (e != 0xFFFFu) break;  // another id's: the next slot
+            const uint32_t nw = (cur & ~(0xFFFFu << sh)) | (want << sh);
+            const uint32_t old = atomicCAS(w, cur, nw);
+            if (old == cur) return 1;
+            cur = old;  // the word held something else: look again
+        }
     }
     return 2;
 }

@@ -230,7 +230,6 @@ __device__ __forceinline__ int screen_pairs(const GraphDev& g, const QReg<C>& q,
 
 struct WaveStats {
     unsigned long long E = 0, X = 0, resets = 0;
-    unsigned long long forgets = 0;   // resets that forgot (no global slot: the visited nodes are dropped)
     unsigned long long S = 0, F = 0;  // rows screened on the fp16 copy / rows evaluated in f32
 };
 
@@ -285,6 +284,14 @@ struct WaveEval {
 
 // the visited set's fill at which beam_layer forgets (3/4; a tools build may
 // set another fraction to measure the probe-length / re-evaluation trade)
+// beam_layer's visited set: vsize > 0 the 32-bit set of vsize entries, vsize < 0
+// the compact 16-bit set (device_common.hpp VIS16_*; the query searches, ids < 2^24)
+__device__ __forceinline__ int vis_any_probe(uint32_t* vis, int vsize, uint32_t id) {
+    return vsize < 0 ? vis16_probe(vis, id) : vis_probe_n(vis, (uint32_t)vsize, id);
+}
+__device__ __forceinline__ void vis_any_clear(uint32_t* vis, int vsize) { vis_clear(vis, vsize < 0 ? VIS16_WORDS : vsize); }
+__device__ __forceinline__ int vis_any_cap(int vsize) { return vsize < 0 ? VIS16_HOMES : vsize; }
+
 #ifndef MH_VIS_FULL
 #define MH_VIS_FULL(n) (((n) >> 1) + ((n) >> 2))
 #endif
@@ -314,59 +321,15 @@ struct WaveBatch {
 // expanded together -- their adjacency rows fetched in one round trip and
 // their new neighbours evaluated as one batch -- which halves the dependent
 // round trips of a search whose expansions yield few new candidates.
-// The beam search's global second level of the visited set (layer 0 of the
-// query searches, engine.hpp GVis).  The LDS set holds 5,120 ids (the LDS its
-// occupancy leaves); a query that fills it claims, at its first reset, one
-// bitmap of the pool (one id per bit, slots never reused within a launch, so no
-// other wave ever touches it; cleared at the claim), copies the LDS set into it
-// before every reset, and from then on a candidate the LDS set calls new is
-// tested against the bitmap and recorded there (one returning L2 atomic per
-// lane, one round trip per expansion) -- the set no longer forgets.  A query that finds the pool exhausted forgets as before;
-// either way the results are the same, only the
-// evaluations differ.
-__device__ __forceinline__ uint32_t* gvis_claim(const GVis& gv) {
-    int s = 0;
-    if (lane_id() == 0) s = atomicAdd(gv.next, 1);
-    s = __shfl(s, 0, 64);
-    if (s >= gv.slots) return nullptr;
-    uint32_t* b = gv.bits + (size_t)s * (size_t)gv.words;
-    uint4* b4 = reinterpret_cast<uint4*>(b);
-    for (int64_t i = lane_id(); i < gv.words / 4; i += 64) b4[i] = make_uint4(0u, 0u, 0u, 0u);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // (vmcnt(0)) the clear is at L2 before the ORs
-    return b;
-}
-__device__ __forceinline__ void gvis_dump(uint32_t* gb, const uint32_t* vis, int vsize) {
-    for (int t = lane_id(); t < vsize; t += 64) {
-        const uint32_t id = vis[t];
-        if (id != VIS_EMPTY)
-            __hip_atomic_fetch_or(gb + (id >> 5), 1u << (id & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // (vmcnt(0)) every OR done before the probes read the words
-}
-// visited before (true), else recorded now: a candidate the LDS set could not
-// record (its probe run congested) is still remembered.  The test is a load
-// (agent scope: from L2, where the ORs go) and the record a non-returning OR --
-// a returning atomic per lane measured 1.6x slower at ef 512.  A
-// stale answer could only re-evaluate a node, which cannot change a result.
-__device__ __forceinline__ bool gvis_test_set(uint32_t* gb, uint32_t id) {
-    const uint32_t bit = 1u << (id & 31);
-    const uint32_t w = __hip_atomic_load(gb + (id >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (w & bit) return true;
-    __hip_atomic_fetch_or(gb + (id >> 5), bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return false;
-}
-
 template <class C, int R, int G, bool COH = false, bool SCREEN = false, int XW = 1, class BEv = WaveBatch>
 __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_t entry, int ef, const QReg<C>& q, float qn,
-                           BList<R>& L, uint32_t* vis, int vsize, WaveStats& st, const BEv& bev = BEv(),
-                           const GVis gv = GVis{}) {
+                           BList<R>& L, uint32_t* vis, int vsize, WaveStats& st, const BEv& bev = BEv()) {
     const int lane = lane_id();
-    uint32_t* gb = nullptr;  // this query's bitmap, from its first reset on
     bl_init(L);
     if (entry == EMPTY_ID) return;
-    vis_clear(vis, vsize);
+    vis_any_clear(vis, vsize);
     wave_sync();  // (the list and the visited set belong to this wave alone)
-    if (lane == 0) vis_probe_n(vis, (uint32_t)vsize, entry);
+    if (lane == 0) vis_any_probe(vis, vsize, entry);
     int vcount = 1;
     eval_list<C, G>(g, q, qn, entry, 1, g.metric, [&](float d, uint32_t u) { bl_insert(L, ef, d, u); });
     st.E += 1;
@@ -411,10 +374,9 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
             int pr = 0;
             if (have && nb != 0xFFFFFFFFu) {
                 nb = guard_id(g, nb);
-                pr = vis_probe_n(vis, (uint32_t)vsize, nb);
+                pr = vis_any_probe(vis, vsize, nb);
             }
             vcount += __popcll(__ballot(pr == 1));
-            if (gb != nullptr && pr != 0 && gvis_test_set(gb, nb)) pr = 0;  // visited before a reset
             cids[w] = compact(nb, pr != 0, cnts[w]);
         }
         // the new neighbours of consecutive expanded entries share a batch while
@@ -451,15 +413,9 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
             auto sink = [&](float d, uint32_t u) { bl_insert(L, ef, d, u); };
             st.F += bev.template score<C, G, SCREEN>(g, q, qn, cid, cnt, wd, screen, margin, sink, st.S);
         }
-        if (vcount > MH_VIS_FULL(vsize)) {  // reset: results unchanged
-            if (gv.bits != nullptr && gb == nullptr) gb = gvis_claim(gv);
+        if (vcount > MH_VIS_FULL(vis_any_cap(vsize))) {  // reset: results unchanged
             wave_sync();
-            if (gb != nullptr)
-                gvis_dump(gb, vis, vsize);  // remembered: the reset forgets nothing
-            else
-                st.forgets += 1;
-            wave_sync();
-            vis_clear(vis, vsize);
+            vis_any_clear(vis, vsize);
             wave_sync();
             // the list's members stay visited: they are the neighbourhood the
             // next expansions keep meeting (fewer re-evaluations)
@@ -467,7 +423,7 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const uint32_t id = L.i[r];
-                const bool ins = id != EMPTY_ID && vis_probe_n(vis, (uint32_t)vsize, id & ID_MASK) == 1;
+                const bool ins = id != EMPTY_ID && vis_any_probe(vis, vsize, id & ID_MASK) == 1;
                 seeded += __popcll(__ballot(ins));
             }
             wave_sync();

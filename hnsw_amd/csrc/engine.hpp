@@ -43,10 +43,10 @@ struct SearchArgs {
                                   // [8]=rows screened in fp16 [9]=rows evaluated in f32 (beam)
     int* err;                     // set to nonzero on visited overflow (compat)
     int vis_log2;                 // compat: 2^vis_log2-entry visited set
-    int vis_n;                    // beam: visited-set entries
+    int vis_n;                    // beam: visited-set entries (the LDS it takes: 4 * vis_n bytes per wave)
+    int vis16 = 0;                // beam: the compact 16-bit set in that LDS instead (ids < 2^24)
     int upper_ef;                 // beam: width of the upper-layer descent (1 = greedy, the reference's k = 1)
     int64_t mw_max_b;             // beam: batches up to this size run a workgroup per query (0 = never)
-    GVis gvis;                    // beam, layer 0: the visited set's global second level
 };
 
 // negative-example re-ranking epilogue (graph.go:1116-1537)
@@ -144,6 +144,7 @@ struct BatchBuildArgs {
     const uint32_t* order;        // nullable: node of workgroup b is order[b] (b < count), nodes sorted by
     int64_t count;                //   level descending so that level >= layer is a prefix
     int64_t mw_max = 0;           // launches of at most this many inserts: one workgroup of 4 waves per insert
+    int vis16 = 0;                // the layer searches' visited set is the compact 16-bit one (ids < 2^24)
 };
 int launch_build_batch_search(const BatchBuildArgs& a, int lpr, int vpl, hipStream_t s);
 // greedy descent of every node u in [n0, n1) through layers a.layer .. levels[u] + 1

@@ -68,6 +68,7 @@ struct mhnsw_index {
     int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
     int vis_log2 = 12;
     int vis_entries = 0;      // beam search's visited set; 0 = 1.25 * 2^vis_log2 (beam_vis_entries)
+    int vis_compact = 1;      // beam search: the compact 16-bit visited set when ids < 2^24 and it fits
     int exact_kk = 0;
     int exact_sample = 64;   // fused preselection: row tiles in the threshold sample (at most; stride = ceil(tiles / this))
     int exact_thr_rank = 0;  // fused preselection: the sample's J-th best is the threshold (0 = max(k, kk / 8))
@@ -77,7 +78,6 @@ struct mhnsw_index {
     int compat_waves = 8;     // compat insert: waves scoring each distance batch (1 = the walking wave alone)
     int upper_ef = 1;         // beam search: upper-layer descent width
     int64_t beam_mw_max_b = 512;  // beam search: batches up to this size run one workgroup of 4 waves per query
-    int64_t vis_global_mb = 0;    // beam search: MiB of per-query visited bitmaps behind the LDS set (0 = off)
     int64_t build_mw_max = 256;   // batched insert: launches of at most this many inserts run 4 waves per insert
     int screen = 1;           // beam search / batched insert fp16 screening copy (results unchanged)
     int fuse_descent = 1;     // batched insert: all greedy descents of a batch in one launch (same graph)
@@ -158,8 +158,6 @@ struct mhnsw_index {
     DevBuf<uint32_t> xsegi;
     DevBuf<uint8_t> xflag;
     DevBuf<uint8_t> xgone;     // exact path: rows to skip when some live row is not in layer 0
-    DevBuf<uint32_t> gvis;     // beam search: the visited set's global second level (GVis bitmaps)
-    DevBuf<int32_t> gvis_next; // ... and its slot counter
     int64_t add_reached = 0;   // inserts the last Add's walk reached (mhnsw_add_reached)
     int64_t partial_rows = 0;  // rows neither deleted nor in layer 0 (left by failed inserts, graph.go:1009)
     uint64_t mut_epoch = 0;            // bumped by every Add / Delete / Import: row membership may have changed

@@ -396,25 +396,13 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         a.err = errw;
         a.vis_log2 = h->vis_log2;
         a.vis_n = beam_vis_entries(h);
+        // the compact set holds 8,192 ids in 16 KiB (the 32-bit set 5,120 in 20 KiB):
+        // fewer resets at large ef, the same results either way
+        a.vis16 = h->vis_compact && h->capn <= (int64_t(1) << 24) && (int64_t)a.vis_n * 4 >= (int64_t)VIS16_WORDS * 4;
         a.upper_ef = h->upper_ef;
         a.mw_max_b = h->beam_mw_max_b;
         if (mode == MHNSW_MODE_BEAM) {
             if (std::max(ef, k) > 512) return fail(h, MHNSW_EUNSUPPORTED, "beam mode supports max(ef,k) <= 512");
-            // the visited set's global second level: one bitmap per query that outgrows
-            // the LDS set, at most vis_global_mb MiB of them (claimed in the kernel)
-            if (h->vis_global_mb > 0) {
-                const int64_t words = (h->capn + 127) / 128 * 4;  // whole uint4s (the claim clears in 16 B)
-                const int64_t slots = std::min<int64_t>(B, (h->vis_global_mb << 20) / (words * 4));
-                if (slots > 0) {
-                    if ((r = ensure_buf(h, h->gvis, (size_t)(slots * words))) || (r = ensure_buf(h, h->gvis_next, 1)))
-                        return r;
-                    HIPCHK(h, hipMemsetAsync(h->gvis_next.p, 0, sizeof(int32_t), s));
-                    a.gvis.bits = h->gvis.p;
-                    a.gvis.words = words;
-                    a.gvis.next = h->gvis_next.p;
-                    a.gvis.slots = (int)slots;
-                }
-            }
             if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));
             LCHK(h, launch_search_beam(a, h->lpr, h->vpl, s));
             if (timing) HIPCHK(h, hipEventRecord(h->ev1, s));

@@ -656,12 +656,11 @@ class Graph:
         return out
 
     def stats(self) -> dict:
-        o = np.zeros(14, np.int64)
-        self._check(load().mhnsw_stats(self._h, _ptr(o, C.c_int64), 14))
+        o = np.zeros(13, np.int64)
+        self._check(load().mhnsw_stats(self._h, _ptr(o, C.c_int64), 13))
         names = ["search_dist_evals", "search_expansions", "visited_resets", "build_dist_evals",
                  "build_expansions", "dropped_proposals", "searches", "exact_uncertified",
-                 "search_screened", "search_f32_evals", "build_screened", "build_f32_rows", "build_search_us",
-                 "visited_forgets"]
+                 "search_screened", "search_f32_evals", "build_screened", "build_f32_rows", "build_search_us"]
         return dict(zip(names, o.tolist()))
 
     def reset_stats(self):

@@ -95,14 +95,14 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * greedy), "beam_mw_max_b" (beam mode, ef and k <= 128: batches of at most this
  * many queries run one workgroup of 4 waves per query -- the single-query
  * latency path of ParallelSearch, graph.go:631-790; default 512, 0 = never;
- * results are identical either way), "vis_global_mb" (beam mode: MiB of per-query
- * bitmaps behind the LDS visited set -- a query whose set fills keeps the
- * visited nodes instead of forgetting them; default 0 = off: the extra round
- * trip per expansion costs what the saved evaluations give back (DESIGN.md
- * section 7); results are identical either way), "build_mw_max" (batched insert: a layer launch of at most this
+ * results are identical either way), "build_mw_max" (batched insert: a layer launch of at most this
  * many inserts runs one workgroup of 4 waves per insert, the candidate batches of
  * its searches split over the waves; default 256, 0 = never; the same graph
- * either way), "screen" (beam mode and batched insert, default 1: keep an fp16
+ * either way), "vis_compact" (beam mode and batched insert, default 1: when node
+ * ids are below 2^24 the visited set stores 16-bit entries -- 8,192 ids in 16 KiB
+ * of LDS, where the beam search's 32-bit set holds 5,120 in 20 KiB and the
+ * insert's (vis_log2 12) 4,096 in 16 KiB -- so a large-ef search resets it less;
+ * exact, the same results and graph either way), "screen" (beam mode and batched insert, default 1: keep an fp16
  * copy of the rows; a candidate is skipped only when the copy proves the f32
  * distance rejects it, so results are unchanged);
  * "max_rows" (row capacity limit, 0 = none: an Add that would need more rows
@@ -261,8 +261,7 @@ int mhnsw_preview_levels(mhnsw_index *h, int64_t n, int32_t *out);
  * rows read in f32 (search evaluations + neighbour-selection rows), [12]
  * device time of the batched insert's kernels (descent, layer searches,
  * commits) in microseconds (option "time_build" = 1: HIP events around each
- * layer's launches), [13] visited-set resets that forgot (beam: a query whose
- * LDS set filled when no global bitmap was left, option "vis_global_mb") */
+ * layer's launches) */
 int mhnsw_stats(const mhnsw_index *h, int64_t *out, int n);
 int mhnsw_reset_stats(mhnsw_index *h);
 /* device time of the last search's main kernel (HIP events on its stream) */

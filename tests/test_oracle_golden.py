@@ -412,3 +412,14 @@ def test_order_ref_list_parity_config0_shape(O):
     a = dev.search(Q, k, mode=O.MODE_COMPAT)
     b = ref.search(Q, k, mode=O.MODE_COMPAT)
     assert compare_lists(a, b, k, bitwise=True)["identical_lists"] == 1.0
+
+
+def test_vis16_mix_is_a_bijection():
+    """device_common.hpp vis16_mix (the compact visited set's exactness rests on
+    it): odd multiply mod 2^24, xorshift 12, odd multiply -- restated here and
+    checked to hit every 24-bit value once"""
+    x = np.arange(1 << 24, dtype=np.uint64)
+    x = (x * 0x9E3779) & 0xFFFFFF
+    x ^= x >> 12
+    x = (x * 0x2C1B3D) & 0xFFFFFF
+    assert np.unique(x).size == 1 << 24
