@@ -369,8 +369,11 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         a.stats = h->d_stats + 4;
         a.vis_log2 = h->vis_log2;
         a.mw_max = h->build_mw_max;
-        // the compact visited set where it holds more than the 32-bit one in about the same LDS
-        a.vis16 = h->vis_compact && h->capn <= (int64_t(1) << 24) && h->vis_log2 >= 12 && h->vis_log2 <= 13;
+        // the compact visited set where it holds more than the 32-bit one in about the
+        // same LDS, for searches wide enough to fill that (efConstruction > 128;
+        // at efC 64 the plain set never fills and its probe is cheaper)
+        a.vis16 = h->vis_compact && a.ef > 128 && h->capn <= (int64_t(1) << 24) && h->vis_log2 >= 12 &&
+                  h->vis_log2 <= 13;
         return a;
     };
     // time_build: HIP events around every insert kernel (descent, layer searches, commits)

@@ -397,8 +397,11 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         a.vis_log2 = h->vis_log2;
         a.vis_n = beam_vis_entries(h);
         // the compact set holds 8,192 ids in 16 KiB (the 32-bit set 5,120 in 20 KiB):
-        // fewer resets at large ef, the same results either way
-        a.vis16 = h->vis_compact && h->capn <= (int64_t(1) << 24) && (int64_t)a.vis_n * 4 >= (int64_t)VIS16_WORDS * 4;
+        // fewer resets at large ef, the same results either way.  Below ef 129 the
+        // 32-bit set rarely fills and its single-CAS probe is the cheaper one
+        // (the compact probe cost 1 % at the headline ef 64).
+        a.vis16 = h->vis_compact && std::max(ef, k) > 128 && h->capn <= (int64_t(1) << 24) &&
+                  (int64_t)a.vis_n * 4 >= (int64_t)VIS16_WORDS * 4;
         a.upper_ef = h->upper_ef;
         a.mw_max_b = h->beam_mw_max_b;
         if (mode == MHNSW_MODE_BEAM) {

@@ -98,7 +98,8 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * results are identical either way), "build_mw_max" (batched insert: a layer launch of at most this
  * many inserts runs one workgroup of 4 waves per insert, the candidate batches of
  * its searches split over the waves; default 256, 0 = never; the same graph
- * either way), "vis_compact" (beam mode and batched insert, default 1: when node
+ * either way), "vis_compact" (beam mode at max(ef, k) > 128 and batched insert at
+ * efConstruction > 128, default 1: when node
  * ids are below 2^24 the visited set stores 16-bit entries -- 8,192 ids in 16 KiB
  * of LDS, where the beam search's 32-bit set holds 5,120 in 20 KiB and the
  * insert's (vis_log2 12) 4,096 in 16 KiB -- so a large-ef search resets it less;

@@ -151,14 +151,17 @@ def test_screened_batch_build_identical(H, metric, alpha):
         g.add_arrays(np.arange(n // 3, n), X[n // 3:])
         _same_graph(ex[(0, 0)], g.export())
         g.close()
-    # the insert searches' visited set: the compact 16-bit one (vis_compact, on in every
-    # build above) and the 32-bit one: the same graph
-    g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
-                ef_construction=80, heuristic=2, keep_pruned=1, screen=1, prune_alpha_pct=alpha, vis_compact=0)
-    g.add_arrays(np.arange(n // 3), X[: n // 3])
-    g.add_arrays(np.arange(n // 3, n), X[n // 3:])
-    _same_graph(ex[(0, 0)], g.export())
-    g.close()
+    # the insert searches' visited set at efConstruction 300 (> 128): the compact 16-bit
+    # one (vis_compact, default) and the 32-bit one -- the same graph
+    exv = []
+    for c in (1, 0):
+        g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
+                    ef_construction=300, heuristic=2, keep_pruned=1, screen=1, prune_alpha_pct=alpha, vis_compact=c)
+        g.add_arrays(np.arange(n // 3), X[: n // 3])
+        g.add_arrays(np.arange(n // 3, n), X[n // 3:])
+        exv.append(g.export())
+        g.close()
+    _same_graph(exv[0], exv[1])
     # one entry expanded per step of the insert's layer searches (build_expand 1; the default
     # 2 expands two): a different graph, but again the same with and without the screen
     ex2 = []
