@@ -23,6 +23,8 @@ n, d = 1_000_000, 768
 cfg2 = os.environ.get("CFG2", "0") == "1"
 hard = os.environ.get("HARD", "0") == "1"  # the harder-data leg (latent 32, M 32, M0 63, efC 512)
 efs = (256, 512) if hard else (48, 64)
+if os.environ.get("EFS"):  # e.g. EFS=320+384+448+512
+    efs = tuple(int(x) for x in os.environ["EFS"].split("+"))
 if hard:
     X = gen_vectors(n, d, 4321, 32, 1000, dev, "cosine")
     Q = gen_vectors(4096, d, 4321 + 7777, 32, 1000, dev, "cosine")
@@ -59,6 +61,6 @@ for opts in sets:
     for ef in efs:
         k_, _, n_ = S.run(Q, H.MODE_BEAM, ef)
         recs.append(recall_at_k(k_, n_, truth[0], truth[2], 10))
-    print(f"{opts}: {n / dt:.0f} inserts/s ({dt:.2f} s), recall@10 ef{efs[0]} {recs[0]:.4f} ef{efs[1]} {recs[1]:.4f}",
-          flush=True)
+    print(f"{opts}: {n / dt:.0f} inserts/s ({dt:.2f} s), recall@10 " +
+          " ".join(f"ef{e} {r:.4f}" for e, r in zip(efs, recs)), flush=True)
     g.close()

@@ -2,7 +2,7 @@
 for k_search_beam, per grid size) dispatches / mean / total ms, and for the
 batched insert's kernels (k_batch_*) the sum of their durations against the
 time the GPU was busy with at least one of them (the union of their
-intervals: below the sum when the build_overlap streams run concurrently),
+intervals: below the sum only when kernels run concurrently),
 plus k_batch_search* by launch width.
 Usage: python tools/trace_build.py TRACE_DIR_OR_CSV"""
 import csv
