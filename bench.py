@@ -179,7 +179,9 @@ def cpu_model():
 
 def build_roofline(bs, secs, n, dim, m0, metric, traffic=None):
     """Batched insert: the insert kernels' algorithmic bytes -- f32 rows (4d + 4:
-    row + norm) for every f32 evaluation and neighbour-selection row, fp16 rows
+    row + norm) for every f32 evaluation and neighbour-selection row (the layer
+    searches', their selection's and, since round 5, the commit's overflow
+    pruning), fp16 rows
     (2d, + 8 for L2's {unscale, |x|}) for every screened candidate, one layer-0
     adjacency row per expansion, the new row and its adjacency/proposal writes --
     over the device time of every insert kernel (k_batch_descend, k_batch_search

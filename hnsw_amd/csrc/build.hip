@@ -1479,6 +1479,7 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
                     load_query(qc, a.g.vecs + (size_t)guard_id(a.g, c) * a.g.pitch);
                     const float cn = a.g.norms[guard_id(a.g, c)];
                     st.E += nkeep;
+                    st.F += nkeep + 1;  // the candidate's row and the kept rows, in f32
                     eval_list<C, G>(a.g, qc, cn, kept, nkeep, a.g.metric, [&](float dcs, uint32_t) {
                         if (a.alpha * dcs < dcv) good = false;
                     });
@@ -1495,7 +1496,11 @@ __global__ __launch_bounds__(64) void k_batch_commit(BatchBuildArgs a) {
                 row[lane] = (int32_t)kept;
                 rowd[lane] = keptd;
             }
-            if (lane == 0) atomicAdd(&a.stats[0], st.E);
+            if (lane == 0) {  // the pruning's rows count as the insert's reads (bench.py build roofline)
+                atomicAdd(&a.stats[0], st.E);
+                atomicAdd(&a.stats[6], st.S);
+                atomicAdd(&a.stats[7], st.F);
+            }
         }
         if (lane == 0) {
             a.g.layers[l].deg[v] = nkeep;
