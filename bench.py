@@ -81,11 +81,19 @@ def parse():
                    help="entries expanded per step of the batched insert's layer searches (engine default 2; "
                         "4 builds the bench index 5.8 %% faster at the same recall@10, 0.9814 / 0.9904 at ef "
                         "48 / 64, profiles/r05_build_expand.txt)")
+    p.add_argument("--search-expand", type=int, default=1, choices=[1, 2, 4],
+                   help="entries expanded per layer-0 step of the headline beam search (search_expand; 1 = the "
+                        "standard search)")
+    p.add_argument("--harder-build-expand", type=int, default=4, choices=[1, 2, 3, 4],
+                   help="build_expand of the harder-data graph (configs 'h')")
+    p.add_argument("--emulate-shards", type=int, default=8,
+                   help="N=1 only: build --total-rows as this many node-ID range shards (one handle each) on the one "
+                        "GPU, search every shard and merge, and project the N-GPU rate at equal recall (0 disables)")
     p.add_argument("--screen", type=int, default=1,
                    help="1: fp16 screening copy, 0: plain f32 evaluation of every candidate; same results")
     p.add_argument("--ef-sweep", default="32,48,64,72,80,96,128,256",
                    help="extra operating points (ef values) reported at N=1; '' disables")
-    p.add_argument("--shard-ef-sweep", default="64,96,128,192,256",
+    p.add_argument("--shard-ef-sweep", default="16,24,32,48,64,96,128,192,256",
                    help="operating points of the shard layout (ef values; recall vs the sharded exact path); '' disables")
     p.add_argument("--batch-sweep", default="1,1024,10000",
                    help="query batch sizes re-measured at ef --ef on the same graph at N=1 (SURVEY 8(d) C2); '' disables")
@@ -280,7 +288,7 @@ def config0(device, seconds):
                                              "ORDER_REF from the same levels (a = GPU, b = ORDER_REF)")}
 
 
-def config2(device):
+def config2(device, build_expand=4):
     """BASELINE configs[2]: 1M x 768 Euclidean, the batched insert at SURVEY
     8(d) C3's efConstruction = EfSearch = 64 (graph.go:500), M 16; recall@10 of
     the built graph at ef 64 against the exact path."""
@@ -288,7 +296,7 @@ def config2(device):
     X = gen_vectors(n, d, 77, 12, 1000, device, "euclidean")
     Q = gen_vectors(4096, d, 78, 12, 1000, device, "euclidean")
     g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.EuclideanDistance, Rng=5, build_mode=H.BUILD_BATCH,
-                m0=48, ef_construction=64, heuristic=2, batch_ratio_pct=20, time_build=1)
+                m0=48, ef_construction=64, heuristic=2, batch_ratio_pct=20, build_expand=build_expand, time_build=1)
     g.reserve(n, d)
     bt, _ = timed(lambda: g.add_device(np.arange(n), X.data_ptr(), n, d))
     bs = g.stats()
@@ -297,8 +305,8 @@ def config2(device):
     k_, _, n_ = Searcher(g, 4096, 10, d, device).run(Q, H.MODE_BEAM, 64)
     rec = recall_at_k(k_, n_, tk, tn, 10)
     g.close()
-    out = {"workload": "1M x 768-d Euclidean batched insert, M=16 M0=48 efConstruction=64 (SURVEY 8(d) C3), "
-                       "batches of 20 % of the index"}
+    out = {"workload": f"1M x 768-d Euclidean batched insert, M=16 M0=48 efConstruction=64 (SURVEY 8(d) C3), "
+                       f"batches of 20 % of the index, build_expand {build_expand}"}
     out.update(build_roofline(bs, bt, n, d, 48, "euclidean"))
     out["recall_at_10_ef64"] = round(rec, 4)
     return out
@@ -341,50 +349,66 @@ def config4(device, steps=10):
                          "frac": round(flops / (gm * 1e-3) / 1e12 / 2500.0, 4), "traffic": None}}
 
 
-def config_harder(device, batch=16384, efs=(64, 128, 256, 512)):
+def config_harder(device, batch=16384, efs=(64, 128, 256, 384, 512), xws=(1, 2, 4), build_expand=4):
     """Harder structured data (verdict item): the bench generator with latent
     dimension 32 instead of 12, 1M x 768 cosine, on the denser graph that data
     needs (M 32, M0 63, efConstruction 512, same heuristic/slack); recall@10
-    against the exact path and QPS / HBM fraction of k_search_beam per ef, and
-    the cheapest ef reaching recall 0.99 (None when ef <= 512 does not)."""
+    against the exact path and QPS / HBM fraction of k_search_beam per ef and
+    per layer-0 expansion width (search_expand 1 / 2 / 4: the XW best
+    unexpanded entries expanded together, their rows fetched in one round
+    trip), and the fastest point reaching recall 0.99 (None when none does)."""
     n, d, M0 = 1_000_000, 768, 63
     X = gen_vectors(n, d, 4321, 32, 1000, device, "cosine")
     Q = gen_vectors(batch, d, 4321 + 7777, 32, 1000, device, "cosine")
     g = H.Graph(M=32, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_BATCH, m0=M0,
-                ef_construction=512, heuristic=2, keep_pruned=1, prune_alpha_pct=115, build_expand=2, screen=1,
-                batch_ratio_pct=20, time_build=1)
+                ef_construction=512, heuristic=2, keep_pruned=1, prune_alpha_pct=115, build_expand=build_expand,
+                screen=1, batch_ratio_pct=20, time_build=1)
     g.reserve(n, d)
     bt, _ = timed(lambda: g.add_device(np.arange(n), X.data_ptr(), n, d))
+    bs = g.stats()
     del X
     ngt = 4096
     S = Searcher(g, batch, 10, d, device)
     tk, _, tn = (x.clone() for x in Searcher(g, ngt, 10, d, device).run(Q[:ngt], H.MODE_EXACT, 0))
     points = []
-    for ef in efs:
-        kk, _, nn = (x.clone() for x in S.run(Q, H.MODE_BEAM, ef))
-        r = recall_at_k(kk[:ngt], nn[:ngt], tk, tn, 10)
-        g.reset_stats()
-        ms = []
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(3):
-            S.run(Q, H.MODE_BEAM, ef)
-            ms.append(g.last_kernel_ms())
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t1) / 3
-        st = g.stats()
-        alg = (st["search_f32_evals"] * (4 * d + 4) + st["search_screened"] * 2 * d
-               + st["search_expansions"] * 4 * (M0 + 1)) / 3 + batch * 4 * d
-        km = float(np.mean(ms))
-        points.append({"ef": ef, "recall_at_10": round(r, 4), "qps": round(batch / dt, 1), "kernel_ms": round(km, 3),
-                       "dist_evals_per_query": round(st["search_dist_evals"] / 3 / batch, 1),
-                       "visited_resets_per_query": round(st["visited_resets"] / 3 / batch, 2),
-                       "roofline_frac": round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+    for xw in xws:
+        g.set_option("search_expand", xw)
+        for ef in efs:
+            kk, _, nn = (x.clone() for x in S.run(Q, H.MODE_BEAM, ef))
+            r = recall_at_k(kk[:ngt], nn[:ngt], tk, tn, 10)
+            g.reset_stats()
+            ms = []
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(3):
+                S.run(Q, H.MODE_BEAM, ef)
+                ms.append(g.last_kernel_ms())
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t1) / 3
+            st = g.stats()
+            alg = (st["search_f32_evals"] * (4 * d + 4) + st["search_screened"] * 2 * d
+                   + st["search_expansions"] * 4 * (M0 + 1)) / 3 + batch * 4 * d
+            km = float(np.mean(ms))
+            points.append({"search_expand": xw, "ef": ef, "recall_at_10": round(r, 4), "qps": round(batch / dt, 1),
+                           "kernel_ms": round(km, 3),
+                           "dist_evals_per_query": round(st["search_dist_evals"] / 3 / batch, 1),
+                           "expansions_per_query": round(st["search_expansions"] / 3 / batch, 1),
+                           "visited_resets_per_query": round(st["visited_resets"] / 3 / batch, 2),
+                           "roofline_frac": round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+    g.device_status()
     g.close()
-    return {"workload": f"1M x 768-d cosine, latent dimension 32 (harder than the headline's 12), M=32 M0=63 "
-                        f"efConstruction=512 (batches of 20 % of the index), beam k=10, {batch} queries/step",
-            "build_inserts_per_s": round(n / bt, 1), "operating_points": points,
-            "at_recall_0.99": next((p_ for p_ in points if p_["recall_at_10"] >= 0.99), None)}
+    ok = [p_ for p_ in points if p_["recall_at_10"] >= 0.99]
+    per_xw = {str(xw): next((p_ for p_ in points if p_["search_expand"] == xw and p_["recall_at_10"] >= 0.99), None)
+              for xw in xws}
+    out = {"workload": f"1M x 768-d cosine, latent dimension 32 (harder than the headline's 12), M=32 M0=63 "
+                       f"efConstruction=512 build_expand={build_expand} (batches of 20 % of the index), beam k=10, "
+                       f"{batch} queries/step",
+           "build_inserts_per_s": round(n / bt, 1),
+           "build": build_roofline(bs, bt, n, d, M0, "cosine"),
+           "operating_points": points,
+           "at_recall_0.99_per_search_expand": per_xw,
+           "at_recall_0.99": max(ok, key=lambda p_: p_["qps"]) if ok else None}
+    return out
 
 
 def oracle_leg(g, Q, truth, k, ef, metric, seconds, device, nparity=1024):
@@ -444,6 +468,35 @@ def oracle_leg(g, Q, truth, k, ef, metric, seconds, device, nparity=1024):
             done += chunk
         out[name] = (done / (time.perf_counter() - t0), done, nt)
     return out, par
+
+
+def summarize(out):
+    """the line's key numbers in one small object (each also in its full object above)"""
+    cfg = out.get("configs") or {}
+    hd = cfg.get("harder_data") or {}
+    h99 = hd.get("at_recall_0.99") or {}
+    c4 = cfg.get("configs[4]") or {}
+    c2 = cfg.get("configs[2]") or {}
+    c0 = cfg.get("configs[0]") or {}
+    emu = (out.get("shard") or {}).get("emulated") or {}
+    sm = {"qps": out["value"], "recall_at_10": out["recall_at_10"], "search_roofline_frac": out["roofline"]["frac"],
+          "build_inserts_per_s": out["build"]["inserts_per_s"], "build_roofline_frac": out["build"]["roofline"]["frac"]}
+    if h99:
+        sm["harder_at_recall_0.99"] = {k: h99.get(k) for k in ("search_expand", "ef", "recall_at_10", "qps",
+                                                                "roofline_frac")}
+    if c4:
+        sm["configs4_ms_per_batch"] = c4.get("ms_per_batch")
+        sm["configs4_gemm_frac"] = (c4.get("roofline") or {}).get("frac")
+    if c2:
+        sm["configs2_inserts_per_s"] = c2.get("inserts_per_s")
+        sm["configs2_build_frac"] = (c2.get("roofline") or {}).get("frac")
+    if c0:
+        sm["configs0_compat_add_per_s"] = c0.get("gpu_compat_add_inserts_per_s")
+        sm["configs0_cpu_compat_add_per_s"] = c0.get("cpu_compat_add_inserts_per_s")
+    if emu:
+        sm["shard_emulated"] = {k: emu.get(k) for k in ("shards", "per_shard_ef", "merged_recall", "projected_qps",
+                                                        "ratio_vs_one_index")}
+    return sm
 
 
 def main():
@@ -540,9 +593,79 @@ def main():
         dist.all_reduce(t)
         return t.item() / world
 
+    def emulate_shards(nsh, Qs, ek, en, one_index_at99):
+        """BASELINE configs[3]'s layout emulated on this one GPU: --total-rows as
+        `nsh` node-ID range shards, each built as its own handle exactly as rank r
+        of an nsh-rank job builds it (build(lo, seed + r, rows)), every query
+        searched on every shard (HIP events per shard launch), the per-shard top-k
+        merged by k_merge, recall against the exact top-k of the whole set.  Per
+        per-shard ef: merged recall, the slowest shard's search, the merge, and
+        the projected nsh-GPU step = slowest shard + merge + the all-gather's
+        time at an assumed 100 GB/s per rank over xGMI ((nsh - 1) * B * (12k + 4)
+        bytes into each rank); the cheapest ef reaching recall 0.99 against the
+        one-index layout's (the N = 1 shard leg: the same rows in one graph)."""
+        hs = []
+        try:
+            for r in range(nsh):
+                lo_, hi_ = shard_range(a.total_rows, nsh, r)
+                h_, bt_, _ = build(lo_, a.seed + r, hi_ - lo_)
+                hs.append((h_, bt_, hi_ - lo_))
+            B = Qs.shape[0]
+            msg = B * (12 * a.k + 4)
+            ag_ms = (nsh - 1) * msg / 100e9 * 1e3
+            pts = []
+            for ef in ([int(x) for x in a.shard_ef_sweep.split(",") if x] if a.shard_ef_sweep else []):
+                lists, kms = [], []
+                for h_, _, _ in hs:
+                    Sx = Searcher(h_, B, a.k, a.dim, device)
+                    lists.append(tuple(x.clone() for x in Sx.run(Qs, H.MODE_BEAM, ef)))
+                    ms_ = []
+                    for _ in range(3):
+                        Sx.run(Qs, H.MODE_BEAM, ef)
+                        ms_.append(h_.last_kernel_ms())
+                    kms.append(float(np.mean(ms_)))
+                    h_.device_status()
+                ak = torch.stack([x[0] for x in lists])
+                ad = torch.stack([x[1] for x in lists])
+                an = torch.stack([x[2] for x in lists])
+                mk, md, mn = merge_topk(ak, ad, an, a.k)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(5):
+                    merge_topk(ak, ad, an, a.k)
+                e1.record()
+                torch.cuda.synchronize()
+                mms = e0.elapsed_time(e1) / 5
+                r_ = recall_at_k(mk[:ngt], mn[:ngt], ek, en, a.k)
+                step_ms = max(kms) + mms + ag_ms
+                pts.append({"per_shard_ef": ef, "merged_recall_at_10": round(r_, 4),
+                            "max_shard_search_ms": round(max(kms), 3), "min_shard_search_ms": round(min(kms), 3),
+                            "merge_ms": round(mms, 4), "projected_step_ms": round(step_ms, 3),
+                            "projected_qps": round(B / (step_ms * 1e-3), 1)})
+            best = next((p_ for p_ in pts if p_["merged_recall_at_10"] >= 0.99), None)
+            one = one_index_at99["qps"] if one_index_at99 else None
+            return {"shards": nsh, "rows_per_shard": hs[0][2], "queries": B,
+                    "build_inserts_per_s": round(sum(x[2] for x in hs) / sum(x[1] for x in hs), 1),
+                    "all_gather_est_ms": round(ag_ms, 4),
+                    "all_gather_model": f"(shards - 1) x {msg} B into each rank at 100 GB/s (xGMI, not measured here)",
+                    "operating_points": pts,
+                    "per_shard_ef": best["per_shard_ef"] if best else None,
+                    "merged_recall": best["merged_recall_at_10"] if best else None,
+                    "projected_qps": best["projected_qps"] if best else None,
+                    "one_index_at_recall_0.99": one_index_at99,
+                    "ratio_vs_one_index": (round(best["projected_qps"] / one, 3) if best and one else None),
+                    "what": (f"{nsh} shards of the same {a.total_rows} rows built and searched one after another on "
+                             f"one GPU; the projected rate assumes one shard per GPU searching concurrently")}
+        finally:
+            for h_, _, _ in hs:
+                h_.close()
+            torch.cuda.empty_cache()
+
     g = None
     if not shard_only:
         g, build_s, bstats = build(0, a.seed)
+        if a.search_expand != 1:
+            g.set_option("search_expand", a.search_expand)
         Q = gen_vectors(a.batch, a.dim, qseed, a.intrinsic, a.clusters, device, a.metric, offset=rank * a.batch)
         S = Searcher(g, a.batch, a.k, a.dim, device)
 
@@ -633,6 +756,9 @@ def main():
                             "ms_per_step": round(tt_.item() * 1e3, 3)})
         gs.device_status()
         sat99 = next((p_ for p_ in spoints if p_["recall_at_10"] >= 0.99), None)
+        emu = None
+        if world == 1 and a.emulate_shards > 1 and spoints:
+            emu = emulate_shards(a.emulate_shards, Qs, ek, en, sat99)
         shard_out = {
             "value": round(a.batch * a.steps / s_el, 1), "unit": "queries/s",
             "ms_per_step": round(s_el / a.steps * 1e3, 3), "recall_at_10": round(srecall, 4),
@@ -647,11 +773,9 @@ def main():
             "operating_points": spoints,
             "at_recall_0.99": sat99,
             "scaling": "strong (fixed total rows; BASELINE configs[3] at 8 ranks)",
-            "layout_ceiling": ("node-ID range shards: every query runs on every shard and a shard's search cost "
-                               "falls only ~log(rows per shard), so N ranks serve about the queries/s of one GPU "
-                               "searching a total/N-row index -- at most ~1.2x one 10M index at 8 ranks "
-                               "(DESIGN.md section 8); throughput scales with replicas (`value`)"),
         }
+        if emu is not None:
+            shard_out["emulated"] = emu
         if shard_only:
             g, build_s, bstats, recall, elapsed, kernel_ms, st = gs, sbuild_s, sbstats, srecall, s_el, s_kms, s_st
             Q, S = Qs, Searcher(gs, a.batch, a.k, a.dim, device)
@@ -715,6 +839,28 @@ def main():
                            "kernel_ms": round(km, 4), "dist_evals_per_query": round(e_ / a.batch, 1),
                            "roofline_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
     at99 = next((p for p in points if p["recall_at_10"] >= 0.99), None)
+    # the headline ef at the other layer-0 expansion widths (search_expand)
+    xpoints = []
+    if world == 1 and a.ef_sweep:
+        for xw in (1, 2, 4):
+            g.set_option("search_expand", xw)
+            kk, _, nn = (x.clone() for x in S.run(Q, H.MODE_BEAM, a.ef))
+            r = recall_at_k(kk[:ngt], nn[:ngt], tk, tn, a.k)
+            g.reset_stats()
+            ms = []
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(3):
+                S.run(Q, H.MODE_BEAM, a.ef)
+                ms.append(g.last_kernel_ms())
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t1) / 3
+            ab, e_, x_, _, _ = alg_bytes_of(g.stats(), 3)
+            km = float(np.mean(ms))
+            xpoints.append({"search_expand": xw, "ef": a.ef, "recall_at_10": round(r, 4), "qps": round(a.batch / dt, 1),
+                            "kernel_ms": round(km, 4), "expansions_per_query": round(x_ / a.batch, 1),
+                            "roofline_frac": round(ab / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+        g.set_option("search_expand", a.search_expand)
     # batch-size points (B in {1, 1024, 10000}): the same graph and ef,
     # queries resident in HBM, wall time per batch over a fixed number of batches
     bpoints = []
@@ -764,7 +910,8 @@ def main():
                          f"every shard, beam ef={a.ef} k={a.k}, {a.batch} queries/step (BASELINE configs[3] layout)"),
             "n_base": a.nbase * (world if shard else 1), "dim": a.dim, "batch_per_gpu": a.batch, "ef": a.ef,
             "k": a.k, "M": a.M, "M0": a.M0, "ef_construction": a.efc, "keep_pruned": a.keep_pruned,
-            "prune_alpha": a.alpha / 100, "batch_ratio_pct": a.batch_ratio,
+            "prune_alpha": a.alpha / 100, "batch_ratio_pct": a.batch_ratio, "build_expand": a.build_expand,
+            "search_expand": a.search_expand,
             "screen": (("fp16"
                         + " row copy rejects candidates whose f32 distance provably exceeds the list's worst; "
                         "every reported distance is f32, results identical to screen=0") if a.screen else "off"),
@@ -786,15 +933,18 @@ def main():
         "cpu_baseline": None,
         "operating_points": points,
         "at_recall_0.99": at99,
+        "expand_points": xpoints,
         "batch_points": bpoints,
     }
     if shard_out is not None and not shard_only:
         out["shard"] = shard_out
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
         cb, par = oracle_leg(g, Q[: min(a.batch, 4096)], (tk, tn), a.k, a.ef, a.metric, a.cpu_seconds, device)
-        par["oracle"] = ("oracle/: C restatement of graph.go/heap.go/distance.go (the Go toolchain is absent) on the "
-                         "engine's exported graph; ORDER_DEV = the engine's summation tree, ORDER_REF = sequential "
-                         "fp32, pinned by the reference's own vectors (tests/golden/reference_goldens.json)")
+        ok_ = par.pop("pass")
+        par = dict({"oracle": ("oracle/: C restatement of graph.go/heap.go/distance.go (no Go toolchain) on the "
+                               "engine's exported graph; ORDER_DEV = the engine's summation tree, ORDER_REF = "
+                               "sequential fp32, pinned by tests/golden/reference_goldens.json")}, **par)
+        par["pass"] = ok_
         out["parity"] = par
         out["cpu_baseline"] = {
             "value": round(cb["beam"][0], 2), "unit": "queries/s", "cores": 1, "kind": "port",
@@ -816,16 +966,21 @@ def main():
         if "0" in which:
             cfg["configs[0]"] = config0(device, a.cpu_seconds)
         if "2" in which:
-            cfg["configs[2]"] = config2(device)
+            cfg["configs[2]"] = config2(device, a.build_expand)
         if "4" in which:
             cfg["configs[4]"] = config4(device)
         if "h" in which:
             try:  # an auxiliary leg: a failure here is reported, not fatal to the line
-                cfg["harder_data"] = config_harder(device)
+                cfg["harder_data"] = config_harder(device, build_expand=a.harder_build_expand)
             except Exception as e:  # noqa: BLE001
                 cfg["harder_data"] = {"error": f"{type(e).__name__}: {e}"}
         out["configs"] = cfg
     if rank == 0:
+        # the measured parity and a compact summary go last, where a reader of the
+        # line's tail (the driver keeps the last few KB) finds them
+        par_ = out.pop("parity", None)
+        out["summary"] = summarize(out)
+        out["parity"] = par_
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -372,8 +372,9 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         // the compact visited set where it holds more than the 32-bit one in about the
         // same LDS, for searches wide enough to fill that (efConstruction > 128;
         // at efC 64 the plain set never fills and its probe is cheaper)
-        a.vis16 = h->vis_compact && a.ef > 128 && h->capn <= (int64_t(1) << 24) && h->vis_log2 >= 12 &&
-                  h->vis_log2 <= 13;
+        // (only in place of the 2^12-entry set: the LDS batch_lds sizes is the same
+        // 16 KiB; a larger vis_log2 keeps the larger 32-bit set the user asked for)
+        a.vis16 = h->vis_compact && a.ef > 128 && h->capn <= (int64_t(1) << 24) && h->vis_log2 == 12;
         return a;
     };
     // time_build: HIP events around every insert kernel (descent, layer searches, commits)
@@ -1156,6 +1157,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "build_expand") {
         if (v < 1 || v > 4) return fail(h, MHNSW_EINVAL, "build_expand must be in [1, 4]");
         h->build_expand = (int)v;
+    } else if (n == "search_expand") {
+        if (v != 1 && v != 2 && v != 4) return fail(h, MHNSW_EINVAL, "search_expand must be 1, 2 or 4");
+        h->search_expand = (int)v;
     } else if (n == "prune_alpha_pct") {
         if (v < 50 || v > 400) return fail(h, MHNSW_EINVAL, "prune_alpha_pct must be in [50, 400]");
         h->alpha_pct = (int)v;
@@ -1252,6 +1256,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "heuristic") *v = h->heuristic;
     else if (n == "keep_pruned") *v = h->keep_pruned;
     else if (n == "build_expand") *v = h->build_expand;
+    else if (n == "search_expand") *v = h->search_expand;
     else if (n == "prune_alpha_pct") *v = h->alpha_pct;
     else if (n == "batch_min") *v = h->batch_min;
     else if (n == "batch_max") *v = h->batch_max;
@@ -1315,6 +1320,7 @@ int mhnsw_reserve(mhnsw_index* h, int64_t n, int dim) {
 
 int mhnsw_add(mhnsw_index* h, const int64_t* keys, const float* vecs, int64_t n, int dim, const int32_t* levels) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
+    h->add_reached = 0;  // (an Add failing before its walk reached no insert)
     int r = drain(h);
     if (r) return r;
     return add_impl(h, keys, vecs, false, n, dim, levels);
@@ -1323,6 +1329,7 @@ int mhnsw_add(mhnsw_index* h, const int64_t* keys, const float* vecs, int64_t n,
 int mhnsw_add_device(mhnsw_index* h, const int64_t* keys, const float* d_vecs, int64_t n, int dim,
                      const int32_t* levels) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
+    h->add_reached = 0;  // (an Add failing before its walk reached no insert)
     HIPCHK(h, hipDeviceSynchronize());  // order after whatever produced d_vecs (and any enqueued search)
     h->scr_valid = false;
     return add_impl(h, keys, d_vecs, true, n, dim, levels);

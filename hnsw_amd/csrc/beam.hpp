@@ -22,7 +22,10 @@ namespace mh {
     X(64, 12, 1)           \
     X(64, 16, 1)
 
-template <int L, int V>
+// XW: entries expanded per step of the layer-0 search (option "search_expand";
+// 1 = the standard best-first search).  XW 1 is instantiated in beam_a-d.hip,
+// XW 2 and 4 in beam_x2.hip / beam_x4.hip.
+template <int L, int V, int XW>
 int launch_beam_cfg(const SearchArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------------------------
@@ -30,7 +33,7 @@ int launch_beam_cfg(const SearchArgs& a, hipStream_t s);
 // ---------------------------------------------------------------------------
 // One query b: greedy descent, the layer-0 beam, and its first k live entries
 // into the outputs.  BEv scores each batch of candidates (beam_layer).
-template <class C, int R, int G, bool SCREEN, class BEv>
+template <class C, int R, int G, bool SCREEN, int XW, class BEv>
 __device__ __forceinline__ void beam_query(const SearchArgs& a, int64_t b, const QReg<C>& q, float qn, uint32_t* smem,
                                            WaveStats& st, const BEv& bev) {
     const int lane = lane_id();
@@ -54,7 +57,7 @@ __device__ __forceinline__ void beam_query(const SearchArgs& a, int64_t b, const
     BList<R> L;
     const int efl = a.ef > a.k ? a.ef : a.k;
     if (a.g.layers[0].deg[ep] == -2) ep = (uint32_t)a.layer_entry[0];
-    beam_layer<C, R, G, false, SCREEN, 1>(a.g, 0, ep, efl, q, qn, L, smem, vsz, st, bev);
+    beam_layer<C, R, G, false, SCREEN, XW>(a.g, 0, ep, efl, q, qn, L, smem, vsz, st, bev);
     // compact the sorted list into the first k live entries (deleted rows
     // route the search but are never returned)
     int nvalid = 0;
@@ -91,7 +94,7 @@ __device__ __forceinline__ void beam_stats(const SearchArgs& a, const WaveStats&
     }
 }
 
-template <class C, int R, int G, bool SCREEN>
+template <class C, int R, int G, bool SCREEN, int XW>
 __global__ __launch_bounds__(64, 2) void k_search_beam(SearchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int64_t b = blockIdx.x;
@@ -100,7 +103,7 @@ __global__ __launch_bounds__(64, 2) void k_search_beam(SearchArgs a) {
     load_query(q, a.q + (size_t)b * C::PITCH);
     const float qn = query_norm(q);
     WaveStats st;
-    beam_query<C, R, G, SCREEN>(a, b, q, qn, smem, st, WaveBatch());
+    beam_query<C, R, G, SCREEN, XW>(a, b, q, qn, smem, st, WaveBatch());
     beam_stats(a, st);
 }
 
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(64 * BMW_WAVES) void k_search_beam_mw(SearchArgs a)
     const float qn = query_norm(q);
     WaveStats st;
     if (wave == 0) {
-        beam_query<C, R, G, SCREEN>(a, b, q, qn, smem, st, MwBatch{&sh});
+        beam_query<C, R, G, SCREEN, 1>(a, b, q, qn, smem, st, MwBatch{&sh});
         if (lane_id() == 0) sh.cmd = BMW_EXIT;
         bmw_barrier();  // releases the other waves
     } else {
@@ -148,20 +151,26 @@ __global__ __launch_bounds__(64 * BMW_WAVES) void k_search_beam_mw(SearchArgs a)
     beam_stats(a, st);
 }
 
-template <class C, int R, int G>
+template <class C, int R, int G, int XW>
 static int launch_beam_t(const SearchArgs& a, hipStream_t s) {
     const size_t lds = (size_t)4 * (size_t)a.vis_n;
-    if (R <= 2 && a.B <= a.mw_max_b) {  // small batch: a workgroup per query
-        if (a.g.h16)
-            hipLaunchKernelGGL((k_search_beam_mw<C, R, G, true>), dim3((unsigned)a.B), dim3(64 * BMW_WAVES), lds, s, a);
-        else
-            hipLaunchKernelGGL((k_search_beam_mw<C, R, G, false>), dim3((unsigned)a.B), dim3(64 * BMW_WAVES), lds, s, a);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
+    // small batch: a workgroup per query (the standard search only; a wider
+    // expansion runs the one-wave kernel at every batch size)
+    if constexpr (XW == 1) {
+        if (R <= 2 && a.B <= a.mw_max_b) {
+            if (a.g.h16)
+                hipLaunchKernelGGL((k_search_beam_mw<C, R, G, true>), dim3((unsigned)a.B), dim3(64 * BMW_WAVES), lds, s,
+                                   a);
+            else
+                hipLaunchKernelGGL((k_search_beam_mw<C, R, G, false>), dim3((unsigned)a.B), dim3(64 * BMW_WAVES), lds,
+                                   s, a);
+            return hipGetLastError() == hipSuccess ? 0 : -1;
+        }
     }
     if (a.g.h16)
-        hipLaunchKernelGGL((k_search_beam<C, R, G, true>), dim3((unsigned)a.B), dim3(64), lds, s, a);
+        hipLaunchKernelGGL((k_search_beam<C, R, G, true, XW>), dim3((unsigned)a.B), dim3(64), lds, s, a);
     else
-        hipLaunchKernelGGL((k_search_beam<C, R, G, false>), dim3((unsigned)a.B), dim3(64), lds, s, a);
+        hipLaunchKernelGGL((k_search_beam<C, R, G, false, XW>), dim3((unsigned)a.B), dim3(64), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -175,14 +184,14 @@ constexpr int beam_group() {
     return 0;
 }
 
-template <int L, int V>
+template <int L, int V, int XW>
 int launch_beam_cfg(const SearchArgs& a, hipStream_t s) {
     constexpr int G = beam_group<L, V>();
     const int efl = a.ef > a.k ? a.ef : a.k;
-    if (efl <= 64) return launch_beam_t<Cfg<L, V>, 1, G>(a, s);
-    if (efl <= 128) return launch_beam_t<Cfg<L, V>, 2, G>(a, s);
-    if (efl <= 256) return launch_beam_t<Cfg<L, V>, 4, G>(a, s);
-    if (efl <= 512) return launch_beam_t<Cfg<L, V>, 8, G>(a, s);
+    if (efl <= 64) return launch_beam_t<Cfg<L, V>, 1, G, XW>(a, s);
+    if (efl <= 128) return launch_beam_t<Cfg<L, V>, 2, G, XW>(a, s);
+    if (efl <= 256) return launch_beam_t<Cfg<L, V>, 4, G, XW>(a, s);
+    if (efl <= 512) return launch_beam_t<Cfg<L, V>, 8, G, XW>(a, s);
     return -4;
 }
 

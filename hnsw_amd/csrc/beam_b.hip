@@ -2,6 +2,6 @@
 #include "beam.hpp"
 
 namespace mh {
-template int launch_beam_cfg<64, 2>(const SearchArgs&, hipStream_t);
-template int launch_beam_cfg<64, 3>(const SearchArgs&, hipStream_t);
+template int launch_beam_cfg<64, 2, 1>(const SearchArgs&, hipStream_t);
+template int launch_beam_cfg<64, 3, 1>(const SearchArgs&, hipStream_t);
 }  // namespace mh

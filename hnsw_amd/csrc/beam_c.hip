@@ -2,6 +2,6 @@
 #include "beam.hpp"
 
 namespace mh {
-template int launch_beam_cfg<64, 4>(const SearchArgs&, hipStream_t);
-template int launch_beam_cfg<64, 6>(const SearchArgs&, hipStream_t);
+template int launch_beam_cfg<64, 4, 1>(const SearchArgs&, hipStream_t);
+template int launch_beam_cfg<64, 6, 1>(const SearchArgs&, hipStream_t);
 }  // namespace mh

@@ -2,7 +2,7 @@
 #include "beam.hpp"
 
 namespace mh {
-template int launch_beam_cfg<64, 8>(const SearchArgs&, hipStream_t);
-template int launch_beam_cfg<64, 12>(const SearchArgs&, hipStream_t);
-template int launch_beam_cfg<64, 16>(const SearchArgs&, hipStream_t);
+template int launch_beam_cfg<64, 8, 1>(const SearchArgs&, hipStream_t);
+template int launch_beam_cfg<64, 12, 1>(const SearchArgs&, hipStream_t);
+template int launch_beam_cfg<64, 16, 1>(const SearchArgs&, hipStream_t);
 }  // namespace mh

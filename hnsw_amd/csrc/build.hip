@@ -1687,7 +1687,12 @@ static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
     if (n <= 0) return 0;
     // fp16 screening: same graph, fewer bytes per candidate; XW = a.expand as a
     // template argument (one search variant per kernel keeps it spill-free)
-    if (a.g.h16 && a.expand == 2 && n <= a.mw_max)  // a narrow launch: a workgroup per insert
+    const bool narrow = a.g.h16 && n <= a.mw_max;  // a narrow launch: a workgroup per insert
+    if (narrow && a.expand == 4)
+        hipLaunchKernelGGL((k_batch_search_mw<C, R, G, true, 4>), dim3((unsigned)n), dim3(64 * BMW_WAVES), lds, s, a);
+    else if (narrow && a.expand == 3)
+        hipLaunchKernelGGL((k_batch_search_mw<C, R, G, true, 3>), dim3((unsigned)n), dim3(64 * BMW_WAVES), lds, s, a);
+    else if (narrow && a.expand == 2)
         hipLaunchKernelGGL((k_batch_search_mw<C, R, G, true, 2>), dim3((unsigned)n), dim3(64 * BMW_WAVES), lds, s, a);
     else if (a.g.h16 && a.expand == 4)
         hipLaunchKernelGGL((k_batch_search<C, R, G, true, 4>), dim3((unsigned)n), dim3(64), lds, s, a);

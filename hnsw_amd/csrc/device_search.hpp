@@ -404,11 +404,19 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
             uint32_t wi;
             bl_at(L, ef - 1, wd, wi);  // the worst before the step: it only decreases during it
         }
-#pragma unroll
+        // the batches are taken from slot 0 and the slots shifted down, so every
+        // register index is static whether or not the compiler unrolls this loop
+        // (a large score() body can keep it rolled)
         for (int w = 0; w < XW; ++w) {
-            const int cnt = cnts[w];
+            const int cnt = cnts[0];
+            const uint32_t cid = cids[0];
+#pragma unroll
+            for (int v = 0; v + 1 < XW; ++v) {
+                cnts[v] = cnts[v + 1];
+                cids[v] = cids[v + 1];
+            }
+            cnts[XW - 1] = 0;
             if (cnt == 0) continue;
-            const uint32_t cid = cids[w];
             st.E += cnt;
             auto sink = [&](float d, uint32_t u) { bl_insert(L, ef, d, u); };
             st.F += bev.template score<C, G, SCREEN>(g, q, qn, cid, cnt, wd, screen, margin, sink, st.S);

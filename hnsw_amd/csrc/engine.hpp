@@ -47,6 +47,7 @@ struct SearchArgs {
     int vis16 = 0;                // beam: the compact 16-bit set in that LDS instead (ids < 2^24)
     int upper_ef;                 // beam: width of the upper-layer descent (1 = greedy, the reference's k = 1)
     int64_t mw_max_b;             // beam: batches up to this size run a workgroup per query (0 = never)
+    int expand = 1;               // beam: entries expanded per layer-0 step (1, 2 or 4; beam_layer XW)
 };
 
 // negative-example re-ranking epilogue (graph.go:1116-1537)

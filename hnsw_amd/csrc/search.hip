@@ -11,7 +11,9 @@
 namespace mh {
 // instantiated in beam_*.hip / walks_*.hip
 #define X_(L, V, G)                                                                    \
-    extern template int launch_beam_cfg<L, V>(const SearchArgs&, hipStream_t);       \
+    extern template int launch_beam_cfg<L, V, 1>(const SearchArgs&, hipStream_t);    \
+    extern template int launch_beam_cfg<L, V, 2>(const SearchArgs&, hipStream_t);    \
+    extern template int launch_beam_cfg<L, V, 4>(const SearchArgs&, hipStream_t);    \
     extern template int launch_compat_cfg<L, V>(const SearchArgs&, hipStream_t);     \
     extern template int launch_negatives_cfg<L, V>(const NegArgs&, hipStream_t);
 MH_FOR_EACH_CFG(X_)
@@ -383,8 +385,11 @@ int launch_sweep(const float* q, const float* X, int64_t n, int pitch, int lpr, 
 
 int launch_search_beam(const SearchArgs& a, int lpr, int vpl, hipStream_t s) {
     if (a.B <= 0) return 0;
-#define X_(L, V, G) \
-    if (lpr == L && vpl == V) return launch_beam_cfg<L, V>(a, s);
+#define X_(L, V, G)                                                   \
+    if (lpr == L && vpl == V)                                         \
+        return a.expand == 4 ? launch_beam_cfg<L, V, 4>(a, s)         \
+               : a.expand == 2 ? launch_beam_cfg<L, V, 2>(a, s)       \
+                               : launch_beam_cfg<L, V, 1>(a, s);
     MH_FOR_EACH_CFG(X_)
 #undef X_
     return -3;

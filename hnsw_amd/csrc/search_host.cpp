@@ -400,10 +400,13 @@ int search_body(mhnsw_index* h, const float* queries, bool on_device, int64_t B,
         // fewer resets at large ef, the same results either way.  Below ef 129 the
         // 32-bit set rarely fills and its single-CAS probe is the cheaper one
         // (the compact probe cost 1 % at the headline ef 64).
+        // (only where the compact set holds more ids than the 32-bit one in the LDS
+        // it is given: a user who raised vis_entries past 8,192 keeps that set)
         a.vis16 = h->vis_compact && std::max(ef, k) > 128 && h->capn <= (int64_t(1) << 24) &&
-                  (int64_t)a.vis_n * 4 >= (int64_t)VIS16_WORDS * 4;
+                  (int64_t)a.vis_n >= (int64_t)VIS16_WORDS && a.vis_n < VIS16_HOMES;
         a.upper_ef = h->upper_ef;
         a.mw_max_b = h->beam_mw_max_b;
+        a.expand = h->search_expand;
         if (mode == MHNSW_MODE_BEAM) {
             if (std::max(ef, k) > 512) return fail(h, MHNSW_EUNSUPPORTED, "beam mode supports max(ef,k) <= 512");
             if (timing) HIPCHK(h, hipEventRecord(h->ev0, s));

@@ -162,6 +162,13 @@ class SplitMix64Rand:
     def __init__(self, seed: int):
         self.state = int(seed) & (2**64 - 1)
 
+    # random.Random's protocol: a host Rng with these can be rewound (Graph._walk)
+    def getstate(self):
+        return self.state
+
+    def setstate(self, st):
+        self.state = st
+
     def Float64(self) -> float:
         m = 2**64 - 1
         self.state = (self.state + 0x9E3779B97F4A7C15) & m
@@ -227,7 +234,6 @@ class Graph:
 
     @Rng.setter
     def Rng(self, rng):
-        self._pending = []  # draws made ahead from the previous Rng
         if hasattr(rng, "Float64"):
             self._rng = rng
             return
@@ -236,13 +242,6 @@ class Graph:
 
     def _host_rng(self) -> bool:
         return hasattr(self._rng, "Float64") and self.get_option("build_mode") != 2
-
-    def _level_draw(self) -> float:
-        """The next level draw: first the draws made ahead for inserts a failed
-        walk never reached (_walk), then the Rng."""
-        if self._pending:
-            return self._pending.pop(0)
-        return self._rng.Float64()
 
     def _draw_levels(self, n: int):
         """Levels of the next n inserts (graph.go:962), each from the layer-0
@@ -256,7 +255,7 @@ class Graph:
             mx = max_level(ml, base + i) if (existed or i > 0) else 1
             lv, d = mx, []
             for level in range(mx):  # graph.go:406-416
-                r = self._level_draw()
+                r = self._rng.Float64()
                 d.append(r)
                 if r > ml:
                     lv = level
@@ -267,27 +266,37 @@ class Graph:
 
     def _walk(self, keys: np.ndarray, add):
         """BatchAdd's walk with levels from the host Rng: the reference draws one
-        level per insert it reaches.  mhnsw_add_plan gives the run up to the next
-        present key (where the walk may stop); its levels are drawn ahead and the
-        run goes in one call.  When an insert fails part way (after deletes,
-        graph.go:1009), mhnsw_add_reached says how many inserts the walk got to
-        and the draws made for the ones past them go back to the front of the
-        queue (_level_draw), so the next Add continues the reference's stream.  An
+        level per insert it reaches (graph.go:962).  mhnsw_add_plan gives the run
+        up to the next present key (where the walk may stop).  When no insert of
+        the run can fail part way, its levels are drawn ahead and it goes in one
+        call.  When one can (the index holds deleted or replaced rows,
+        graph.go:1009: one_by_one), a Rng with getstate()/setstate() (random.Random's
+        protocol; SplitMix64Rand has it) still goes in one call: after a failure
+        mhnsw_add_reached says how many inserts the walk got to, and the Rng is
+        rewound and redraws exactly their draws, so it ends where Go's would.  Any
+        other Rng adds one node per call, drawing as the reference does.  An
         error from add(lo, hi, levels) ends the walk."""
         nwalk, one = C.c_int64(), C.c_int()
+        rng = self._rng
+        rewind = hasattr(rng, "getstate") and hasattr(rng, "setstate")
         lo = 0
         while lo < len(keys):
             self._check(load().mhnsw_add_plan(self._h, _ptr(keys[lo:], C.c_int64), len(keys) - lo, C.byref(nwalk),
                                               C.byref(one)))
             hi = lo + nwalk.value
+            if one.value and not rewind:
+                hi = lo + 1
+            snap = rng.getstate() if rewind else None
             lv, draws = self._draw_levels(hi - lo)
             try:
                 add(lo, hi, lv)
             except HnswError:
-                reached = C.c_int64()
-                self._check(load().mhnsw_add_reached(self._h, C.byref(reached)))
-                back = [r for d in draws[reached.value:] for r in d]
-                self._pending[:0] = back
+                if rewind:
+                    reached = C.c_int64()
+                    self._check(load().mhnsw_add_reached(self._h, C.byref(reached)))
+                    rng.setstate(snap)
+                    for _ in range(sum(len(d) for d in draws[: reached.value])):
+                        rng.Float64()
                 raise
             lo = hi
 

@@ -79,11 +79,22 @@ inline const DistanceFunc EuclideanDistance{MHNSW_EUCLIDEAN, "euclidean"};  // d
 struct Rand {
     virtual ~Rand() = default;
     virtual double Float64() = 0;  // math/rand (*Rand).Float64
+    // Optional rewind: a generator that can save and restore its state lets
+    // BatchAdd draw a whole run's levels ahead and, when the walk fails part
+    // way, put the generator back to exactly the draws the reference made
+    // (mhnsw_add_reached).  Without it, inserts that may fail go one per call.
+    virtual bool GetState(std::vector<uint64_t>*) const { return false; }
+    virtual void SetState(const std::vector<uint64_t>&) {}
 };
 
 struct SplitMix64Rand : Rand {
     uint64_t state;
     explicit SplitMix64Rand(uint64_t seed) : state(seed) {}
+    bool GetState(std::vector<uint64_t>* s) const override {
+        s->assign(1, state);
+        return true;
+    }
+    void SetState(const std::vector<uint64_t>& s) override { state = s.at(0); }
     double Float64() override {
         uint64_t z = (state += 0x9E3779B97F4A7C15ull);
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -420,34 +431,29 @@ class Graph {  // graph.go:305-332
         if (!Rng) Rng = defaultRand();
         int64_t nwalk = 0;
         int one = 0;
-        // one level draw: first what a failed walk handed back, then the Rng
-        auto float64 = [&]() {
-            if (!pending_.empty()) {
-                const double r = pending_.front();
-                pending_.erase(pending_.begin());
-                return r;
-            }
-            return Rng->Float64();
-        };
-        // up to the next present key (where the walk may stop), every level drawn
-        // ahead (graph.go:388-417, 962); when an insert fails part way (after
-        // deletes, graph.go:1009) the draws made for the inserts past the ones the
-        // walk reached (mhnsw_add_reached) go back to the front of the queue
+        // The run up to the next present key (where the walk may stop) goes in one
+        // call with its levels drawn ahead (graph.go:388-417, 962).  When an insert
+        // of it may fail part way (deleted or replaced rows, graph.go:1009:
+        // one_by_one), a generator that can rewind is put back afterwards to the
+        // draws of the inserts the walk reached (mhnsw_add_reached); any other
+        // goes one insert per call, drawing exactly as the reference does.
+        std::vector<uint64_t> snap;
         for (size_t lo = 0; lo < n;) {
             if (int rc = mhnsw_add_plan(h_, keys.data() + lo, (int64_t)(n - lo), &nwalk, &one))
                 return make_error(rc, h_);
-            const size_t hi = lo + (size_t)nwalk;
+            size_t hi = lo + (size_t)nwalk;
+            const bool rewind = Rng->GetState(&snap);
+            if (one && !rewind) hi = lo + 1;
             const bool existed = mhnsw_num_layers(h_) > 0;
             const int64_t base = Len();
             std::vector<int32_t> lv(hi - lo);
-            std::vector<std::vector<double>> drawn(hi - lo);
+            std::vector<int> ndraw(hi - lo, 0);
             for (size_t i = 0; i < hi - lo; ++i) {
                 const int mx = (existed || i > 0) ? maxLevel(Ml, base + (int64_t)i) : 1;
                 lv[i] = mx;
                 for (int level = 0; level < mx; ++level) {
-                    const double r = float64();
-                    drawn[i].push_back(r);
-                    if (r > Ml) {
+                    ++ndraw[i];
+                    if (Rng->Float64() > Ml) {
                         lv[i] = level;
                         break;
                     }
@@ -457,11 +463,10 @@ class Graph {  // graph.go:305-332
             if (rc < 0) {
                 Error e = make_error(rc, h_);
                 int64_t reached = 0;
-                if (mhnsw_add_reached(h_, &reached) == 0) {
-                    std::vector<double> back;
-                    for (size_t i = (size_t)reached; i < drawn.size(); ++i)
-                        back.insert(back.end(), drawn[i].begin(), drawn[i].end());
-                    pending_.insert(pending_.begin(), back.begin(), back.end());
+                if (rewind && mhnsw_add_reached(h_, &reached) == 0) {
+                    Rng->SetState(snap);
+                    for (size_t i = 0; i < (size_t)reached && i < ndraw.size(); ++i)
+                        for (int j = 0; j < ndraw[i]; ++j) (void)Rng->Float64();
                 }
                 return e;
             }
@@ -485,7 +490,6 @@ class Graph {  // graph.go:305-332
 
     mhnsw_index* h_ = nullptr;
     std::map<K, Vector> values_;
-    std::vector<double> pending_;  // level draws made ahead for inserts a failed walk never reached
 };
 
 // graph.go:340-348

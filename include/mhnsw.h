@@ -76,7 +76,13 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * 2^n entries), "vis_entries" (beam search's visited set, 0 = 1.25 * 2^vis_log2),
  * "build_expand" (batched insert: entries expanded per step of its layer
  * searches, 1-4, default 2 -- they fetch their adjacency rows in one round
- * trip and evaluate their new neighbours as one batch), "exact_kk",
+ * trip and evaluate their new neighbours as one batch), "search_expand" (beam
+ * mode: entries expanded per step of the layer-0 search, 1 (default, the
+ * standard best-first search), 2 or 4 -- the best unexpanded entries are taken
+ * together, their adjacency rows fetched in one round trip and their new
+ * neighbours scored as one batch; a different search from 1 (results can
+ * differ), bit-identical to the oracle's og_set_search_expand; always the
+ * one-wave kernel), "exact_kk",
  * "exact_thr_rank" (precision 3: the threshold is the sample's J-th best score,
  * J = max(k, this) capped at kk; 0 (default) = max(k, kk / 8)),
  * "exact_sample" (precision 3: at most this many row tiles form the threshold

@@ -51,6 +51,7 @@ def lib():
         L.og_last_error.argtypes = [C.c_void_p]
         L.og_set_params.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_int, C.c_int]
         L.og_set_order.argtypes = [C.c_void_p, C.c_int]
+        L.og_set_search_expand.argtypes = [C.c_void_p, C.c_int]
         L.og_validate.argtypes = [C.c_void_p]
         L.og_len.restype = C.c_int64
         L.og_len.argtypes = [C.c_void_p]
@@ -158,6 +159,11 @@ class Graph:
         """ORDER_REF (sequential fp32, the reference's arithmetic stand-in) or
         ORDER_DEV (the engine's canonical tree) for every later distance."""
         self._check(lib().og_set_order(self._h, order))
+
+    def set_search_expand(self, xw):
+        """Beam mode: entries expanded per layer-0 step (1 standard, 2 or 4) --
+        the engine's option "search_expand"."""
+        self._check(lib().og_set_search_expand(self._h, xw))
 
     def validate(self):
         self._check(lib().og_validate(self._h))

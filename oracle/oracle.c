@@ -252,6 +252,7 @@ typedef struct {
 
 struct og_graph {
     int metric, order;
+    int xw; /* beam mode: entries expanded per layer-0 step (og_set_search_expand; 1 = standard) */
     int M, M0, ef;
     double ml;
     uint64_t rng;
@@ -388,6 +389,7 @@ og_graph *og_create(int metric, int order, int M, int M0, double ml, int ef, uin
     if (!g) return NULL;
     g->metric = metric;
     g->order = order;
+    g->xw = 1;
     g->M = M;
     g->M0 = M0 > 0 ? M0 : M;
     g->ml = ml;
@@ -444,6 +446,13 @@ int og_set_params(og_graph *g, int M, double ml, int ef, int metric) {
     g->ml = ml;
     g->ef = ef;
     g->metric = metric;
+    return OG_OK;
+}
+
+/* the engine's option "search_expand" (beam.hpp / device_search.hpp beam_layer XW) */
+int og_set_search_expand(og_graph *g, int xw) {
+    if (xw != 1 && xw != 2 && xw != 4) return set_err(g, OG_EINVAL, "search_expand must be 1, 2 or 4");
+    g->xw = xw;
     return OG_OK;
 }
 
@@ -692,8 +701,15 @@ static int beam_insert(bentry *lst, int *n, int ef, float d, int32_t id) {
     return 1;
 }
 
+/* xw: entries expanded per step.  1 is the standard search above.  xw > 1 (the
+ * engine's "search_expand" / "build_expand", device_search.hpp beam_layer XW):
+ * the xw first unexpanded entries of the list are all marked expanded, then
+ * their rows' unvisited neighbours are scored and inserted, row by row.  The
+ * list after a step is the best ef of its entries and the step's candidates
+ * whatever the insertion order, so the engine may score the step's candidates
+ * in any order and batching. */
 static int beam_layer_search(og_graph *g, og_scratch *s, int layer, int32_t entry, int ef, const float *q,
-                             float qn, bentry *lst, int64_t *nd, int64_t *nx) {
+                             float qn, bentry *lst, int64_t *nd, int64_t *nx, int xw) {
     if (entry < 0 || layer < 0 || layer >= g->nlayers) return 0;
     og_layer *L = &g->layers[layer];
     uint32_t st = next_stamp(s, g->cap_nodes);
@@ -701,27 +717,30 @@ static int beam_layer_search(og_graph *g, og_scratch *s, int layer, int32_t entr
     s->visited[entry] = st;
     beam_insert(lst, &n, ef, dist_q(g, entry, q, qn), entry);
     (*nd)++;
+    if (xw < 1) xw = 1;
+    if (xw > 4) xw = 4;
     for (;;) {
-        int c = -1;
-        for (int i = 0; i < n; ++i)
+        int32_t cur[4];
+        int nc = 0;
+        for (int i = 0; i < n && nc < xw; ++i)
             if (!lst[i].exp) {
-                c = i;
-                break;
+                lst[i].exp = 1;
+                cur[nc++] = lst[i].id;
             }
-        if (c < 0) break;
-        lst[c].exp = 1;
-        int32_t cur = lst[c].id;
-        int deg = L->deg[cur];
-        (*nx)++;
-        if (deg <= 0) continue;
-        const int32_t *nb = L->adj + (size_t)cur * g->acap;
-        for (int j = 0; j < deg; ++j) {
-            int32_t v = nb[j];
-            if (v < 0 || s->visited[v] == st) continue;
-            s->visited[v] = st;
-            float d = dist_q(g, v, q, qn);
-            (*nd)++;
-            beam_insert(lst, &n, ef, d, v);
+        if (nc == 0) break;
+        for (int w = 0; w < nc; ++w) {
+            int deg = L->deg[cur[w]];
+            (*nx)++;
+            if (deg <= 0) continue;
+            const int32_t *nb = L->adj + (size_t)cur[w] * g->acap;
+            for (int j = 0; j < deg; ++j) {
+                int32_t v = nb[j];
+                if (v < 0 || s->visited[v] == st) continue;
+                s->visited[v] = st;
+                float d = dist_q(g, v, q, qn);
+                (*nd)++;
+                beam_insert(lst, &n, ef, d, v);
+            }
         }
     }
     return n;
@@ -1177,11 +1196,11 @@ static int search_one(og_graph *g, og_scratch *s, qbuf *qb, const float *q, int 
     int32_t p = entry;
     for (int l = top; l >= 1; --l) {
         if (g->layers[l].deg[p] == -2) p = g->layers[l].entry; /* not a member of this layer */
-        int c = beam_layer_search(g, s, l, p, 1, q, qn, qb->lst, &qb->st[0], &qb->st[1]);
+        int c = beam_layer_search(g, s, l, p, 1, q, qn, qb->lst, &qb->st[0], &qb->st[1], 1);
         if (c > 0) p = qb->lst[0].id;
     }
     if (g->layers[0].deg[p] == -2) p = g->layers[0].entry;
-    int c = beam_layer_search(g, s, 0, p, efl, q, qn, qb->lst, &qb->st[0], &qb->st[1]);
+    int c = beam_layer_search(g, s, 0, p, efl, q, qn, qb->lst, &qb->st[0], &qb->st[1], g->xw);
     /* deleted rows still route the search (their edges stay) but are not returned */
     int nout = 0;
     for (int i = 0; i < c && nout < k; ++i) {

@@ -77,6 +77,9 @@ const char *og_last_error(og_graph *g);
 int og_set_params(og_graph *g, int M, double ml, int ef, int metric);
 /* switch the summation order of later distances (the norms are kept for both) */
 int og_set_order(og_graph *g, int order);
+/* beam mode: entries expanded per step of the layer-0 search (1 = standard, 2, 4);
+ * the engine's option "search_expand" */
+int og_set_search_expand(og_graph *g, int xw);
 int og_validate(og_graph *g);
 int64_t og_len(og_graph *g);
 int og_dims(og_graph *g);

@@ -327,7 +327,7 @@ def _clustered(rng, n, d, nc=64, intrinsic=12, noise=0.05):
 
 
 @pytest.mark.parametrize("metric", [0, 1])
-@pytest.mark.parametrize("expand", [1, 2])
+@pytest.mark.parametrize("expand", [1, 2, 3, 4])
 def test_batch_build_recall_and_exact_parity(H, O, metric, expand):
     rng = np.random.default_rng(11 + metric)
     n, d = 20000, 64

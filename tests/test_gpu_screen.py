@@ -162,18 +162,23 @@ def test_screened_batch_build_identical(H, metric, alpha):
         exv.append(g.export())
         g.close()
     _same_graph(exv[0], exv[1])
-    # one entry expanded per step of the insert's layer searches (build_expand 1; the default
-    # 2 expands two): a different graph, but again the same with and without the screen
-    ex2 = []
-    for screen in (0, 1):
-        g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
-                    ef_construction=80, heuristic=2, keep_pruned=1, screen=screen, prune_alpha_pct=alpha,
-                    build_expand=1)
-        g.add_arrays(np.arange(n // 3), X[: n // 3])
-        g.add_arrays(np.arange(n // 3, n), X[n // 3:])
-        ex2.append(g.export())
-        g.close()
-    _same_graph(ex2[0], ex2[1])
+    # 1, 3 and 4 entries expanded per step of the insert's layer searches (build_expand; 4 is
+    # what bench.py builds its indexes with): different graphs, but each the same with and
+    # without the screen, and with the narrow launches on the 4-wave kernel (build_mw_max,
+    # which covers every launch of this small build) or on the one-wave kernel
+    for xw in (1, 3, 4):
+        ex2 = []
+        for screen, mw in ((0, 256), (1, 256), (1, 0), (1, 1 << 30)):
+            g = H.Graph(M=12, Ml=0.3, EfSearch=48, Distance=_metric_fn(H, metric), Rng=3, build_mode=H.BUILD_BATCH,
+                        ef_construction=80, heuristic=2, keep_pruned=1, screen=screen, prune_alpha_pct=alpha,
+                        build_expand=xw, build_mw_max=mw)
+            g.add_arrays(np.arange(n // 3), X[: n // 3])
+            g.add_arrays(np.arange(n // 3, n), X[n // 3:])
+            assert g.stats()["dropped_proposals"] == 0
+            ex2.append(g.export())
+            g.close()
+        for e in ex2[1:]:
+            _same_graph(ex2[0], e)
     # batches of 20 % of the index (bench.py's schedule for the bench index and
     # configs[2]): again the same graph with and without the screen
     ex3 = []

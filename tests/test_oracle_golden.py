@@ -181,6 +181,39 @@ def test_beam_recall_dominates_compat(O):
     assert recall(bk, bn) > 0.9
 
 
+def test_beam_search_expand_oracle(O):
+    """The oracle's restatement of the engine's search_expand (entries expanded
+    per layer-0 step): XW 2 / 4 are valid searches (sorted, unique lists, recall
+    within 2 % of XW 1, more expansions), XW 1 is the standard search again,
+    and other widths are refused."""
+    rng = np.random.default_rng(6)
+    X = rng.uniform(-1, 1, (3000, 8)).astype(np.float32)
+    Q = rng.uniform(-1, 1, (100, 8)).astype(np.float32)
+    g = O.Graph(metric=O.COSINE, order=O.ORDER_DEV, M=16, Ml=0.25, EfSearch=20, seed=3)
+    g.add(np.arange(3000), X)
+    ek, _, _ = g.search(Q, 10, mode=O.MODE_EXACT)
+    base = g.search(Q, 10, mode=O.MODE_BEAM, ef=64)
+    rec, xs = {}, {}
+    for xw in (1, 2, 4):
+        g.set_search_expand(xw)
+        x0 = g.stats()[1]
+        k, d, n = g.search(Q, 10, mode=O.MODE_BEAM, ef=64)
+        xs[xw] = g.stats()[1] - x0
+        assert (n == 10).all()
+        for b in range(len(Q)):
+            assert len(set(k[b])) == 10 and (np.diff(d[b]) >= 0).all()
+        rec[xw] = np.mean([len(set(k[b]) & set(ek[b])) / 10 for b in range(len(Q))])
+        if xw == 1:
+            for a, b in zip((k, d, n), base):
+                assert np.array_equal(a, b)
+    g.set_search_expand(1)
+    assert xs[1] < xs[2] <= xs[4], xs
+    assert max(rec.values()) - min(rec.values()) <= 0.02, rec
+    for bad in (0, 3, 8):
+        with pytest.raises(O.OracleError, match="search_expand"):
+            g.set_search_expand(bad)
+
+
 # ----------------------------------------------------------------- Delete
 def _live_connectivity(ex):
     """Analyzer.Connectivity (analyzer.go:20-38) from an export: mean
