@@ -75,12 +75,12 @@ def parse():
     p.add_argument("--alpha", type=int, default=115, help="heuristic slack x100 (prune_alpha_pct; 100 = HNSW Alg. 4)")
     p.add_argument("--batch-ratio", type=int, default=20,
                    help="batched insert: each batch holds this %% of the rows already in the index (batch_ratio_pct; "
-                        "the engine default is 5): fewer latency-bound small launches early on, recall@10 0.9904 vs "
+                        "the engine default since round 6, was 5): fewer latency-bound small launches early on, recall@10 0.9904 vs "
                         "0.9909 at ef 64 on the bench index (profiles/r04_build_schedule.txt)")
     p.add_argument("--build-expand", type=int, default=4, choices=[1, 2, 3, 4],
-                   help="entries expanded per step of the batched insert's layer searches (engine default 2; "
-                        "4 builds the bench index 5.8 %% faster at the same recall@10, 0.9814 / 0.9904 at ef "
-                        "48 / 64, profiles/r05_build_expand.txt)")
+                   help="entries expanded per step of the batched insert's layer searches (the engine default "
+                        "since round 6; 4 builds the bench index 5.8 %% faster than 2 at the same recall@10, "
+                        "0.9814 / 0.9904 at ef 48 / 64, profiles/r05_build_expand.txt)")
     p.add_argument("--search-expand", type=int, default=1, choices=[1, 2, 4],
                    help="entries expanded per layer-0 step of the headline beam search (search_expand; 1 = the "
                         "standard search)")

@@ -72,10 +72,11 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * "ef_construction" (<= 512), "heuristic" (0 closest-M, 1 HNSW heuristic on new rows,
  * 2 also when a reverse edge overflows a row), "keep_pruned", "prune_alpha_pct"
  * (heuristic slack x100: c is dropped when alpha*d(c,kept) < d(u,c); 100 = HNSW
- * Alg. 4), "batch_min", "batch_max", "batch_ratio_pct", "vis_log2" (compat / build visited sets:
+ * Alg. 4), "batch_min", "batch_max", "batch_ratio_pct" (batched insert: each batch holds this
+ * % of the rows already indexed, default 20), "vis_log2" (compat / build visited sets:
  * 2^n entries), "vis_entries" (beam search's visited set, 0 = 1.25 * 2^vis_log2),
  * "build_expand" (batched insert: entries expanded per step of its layer
- * searches, 1-4, default 2 -- they fetch their adjacency rows in one round
+ * searches, 1-4, default 4 -- they fetch their adjacency rows in one round
  * trip and evaluate their new neighbours as one batch), "search_expand" (beam
  * mode: entries expanded per step of the layer-0 search, 1 (default, the
  * standard best-first search), 2 or 4 -- the best unexpanded entries are taken

@@ -9,7 +9,8 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 timeout -k 10 420 python3 $R/bench.py "$@" > $O/bench.json 2> $O/bench.err || exit 1
 cd /tmp && export TMPDIR=/tmp
-PA="--steps 3 --warmup 1 --cpu-seconds 0 --gt-queries 16 --ef-sweep= --batch-sweep= --configs= --no-shard-leg"
+# the driver's step count (--steps 20 --warmup 5): >= 20 launches of the headline kernel, side legs off
+PA="--steps 20 --warmup 5 --cpu-seconds 0 --ef-sweep= --batch-sweep= --configs= --no-shard-leg"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py $PA "$@" > $O/trace.log 2>&1 || exit 2
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $R/bench.py $PA "$@" > $O/pmc_fetch.log 2>&1 || exit 3
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 $R/bench.py $PA "$@" > $O/pmc_write.log 2>&1 || exit 4
