@@ -43,7 +43,7 @@ import hnsw_amd as H  # noqa: E402
 
 # revision of the search/build kernels the recorded PMC passes (profiles/*_pmc_*.json)
 # were taken on; a pass recorded on another revision is not attached as `traffic`
-KERNEL_REV = "r05"
+KERNEL_REV = "r06"
 from hnsw_amd.shard import engine_local_search, gather_topk, merge_topk, shard_range, sharded_search  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -75,7 +75,7 @@ def parse():
     p.add_argument("--alpha", type=int, default=115, help="heuristic slack x100 (prune_alpha_pct; 100 = HNSW Alg. 4)")
     p.add_argument("--batch-ratio", type=int, default=20,
                    help="batched insert: each batch holds this %% of the rows already in the index (batch_ratio_pct; "
-                        "the engine default since round 6, was 5): fewer latency-bound small launches early on, recall@10 0.9904 vs "
+                        "the engine default is 5, kept for incremental adds, include/mhnsw.h): fewer latency-bound small launches early on, recall@10 0.9904 vs "
                         "0.9909 at ef 64 on the bench index (profiles/r04_build_schedule.txt)")
     p.add_argument("--build-expand", type=int, default=4, choices=[1, 2, 3, 4],
                    help="entries expanded per step of the batched insert's layer searches (the engine default "
@@ -104,8 +104,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline time box (0 disables)")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
     p.add_argument("--one-gpu", action="store_true", help="map every rank to cuda:0 (multi-rank rehearsal)")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r05_pmc_search.json"))
-    p.add_argument("--pmc-build-json", default=os.path.join(ROOT, "profiles", "r05_pmc_build.json"))
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r06_pmc_search.json"))
+    p.add_argument("--pmc-build-json", default=os.path.join(ROOT, "profiles", "r06_pmc_build.json"))
     return p.parse_args()
 
 
@@ -288,7 +288,7 @@ def config0(device, seconds):
                                              "ORDER_REF from the same levels (a = GPU, b = ORDER_REF)")}
 
 
-def config2(device, build_expand=4):
+def config2(device, build_expand=4, pmc_json=os.path.join(ROOT, "profiles", "r06_pmc_config2.json")):
     """BASELINE configs[2]: 1M x 768 Euclidean, the batched insert at SURVEY
     8(d) C3's efConstruction = EfSearch = 64 (graph.go:500), M 16; recall@10 of
     the built graph at ef 64 against the exact path."""
@@ -307,7 +307,15 @@ def config2(device, build_expand=4):
     g.close()
     out = {"workload": f"1M x 768-d Euclidean batched insert, M=16 M0=48 efConstruction=64 (SURVEY 8(d) C3), "
                        f"batches of 20 % of the index, build_expand {build_expand}"}
-    out.update(build_roofline(bs, bt, n, d, 48, "euclidean"))
+    traffic = None  # the insert kernels' HBM bytes from the PMC passes of this build (tools/profile_round.sh)
+    try:
+        pm = json.load(open(pmc_json)) if pmc_json else {}
+        if all(pm.get(k) == v for k, v in dict(n=n, dim=d, efc=64, m0=48, build_expand=build_expand,
+                                                batch_ratio=20, rev=KERNEL_REV).items()):
+            traffic = pm.get("hbm_bytes_total")
+    except (OSError, ValueError):
+        pass
+    out.update(build_roofline(bs, bt, n, d, 48, "euclidean", traffic))
     out["recall_at_10_ef64"] = round(rec, 4)
     return out
 

@@ -66,7 +66,7 @@ struct mhnsw_index {
     int build_expand = 4;     // batched insert: entries expanded per step of its layer searches (1-4)
     int search_expand = 1;    // beam search: entries expanded per layer-0 step (1, 2, 4; 1 = standard)
     int alpha_pct = 100;
-    int batch_min = 1, batch_max = 65536, batch_ratio_pct = 20;
+    int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
     int vis_log2 = 12;
     int vis_entries = 0;      // beam search's visited set; 0 = 1.25 * 2^vis_log2 (beam_vis_entries)
     int vis_compact = 1;      // beam search: the compact 16-bit visited set when ids < 2^24 and it fits

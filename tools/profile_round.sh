@@ -14,4 +14,8 @@ PA="--steps 20 --warmup 5 --cpu-seconds 0 --ef-sweep= --batch-sweep= --configs= 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py $PA "$@" > $O/trace.log 2>&1 || exit 2
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $R/bench.py $PA "$@" > $O/pmc_fetch.log 2>&1 || exit 3
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 $R/bench.py $PA "$@" > $O/pmc_write.log 2>&1 || exit 4
+# configs[2] (1M x 768 L2 batched insert, efC 64) alone: its insert kernels' HBM bytes
+C2="python3 $R/tools/config2_probe.py 4"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/c2_fetch -o run --output-format csv -- $C2 > $O/c2_fetch.log 2>&1 || exit 5
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/c2_write -o run --output-format csv -- $C2 > $O/c2_write.log 2>&1 || exit 6
 echo done > $O/status
