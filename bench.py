@@ -93,7 +93,7 @@ def parse():
                    help="1: fp16 screening copy, 0: plain f32 evaluation of every candidate; same results")
     p.add_argument("--ef-sweep", default="32,48,64,72,80,96,128,256",
                    help="extra operating points (ef values) reported at N=1; '' disables")
-    p.add_argument("--shard-ef-sweep", default="16,24,32,48,64,96,128,192,256",
+    p.add_argument("--shard-ef-sweep", default="16,24,32,40,48,64,96,128,192,256",
                    help="operating points of the shard layout (ef values; recall vs the sharded exact path); '' disables")
     p.add_argument("--batch-sweep", default="1,1024,10000",
                    help="query batch sizes re-measured at ef --ef on the same graph at N=1 (SURVEY 8(d) C2); '' disables")
@@ -569,6 +569,11 @@ def main():
                 "frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4),
                 "self_distance_zero": bool(abs(float(out[12345])) <= 1e-6)}
 
+    tmarks = [("start", time.perf_counter())]
+
+    def mark(done):  # wall seconds per leg of this run (the line's leg_seconds)
+        tmarks.append((done, time.perf_counter()))
+
     qseed = a.seed + 7_777
     ngt = min(a.gt_queries, a.batch)
 
@@ -646,6 +651,8 @@ def main():
                 mms = e0.elapsed_time(e1) / 5
                 r_ = recall_at_k(mk[:ngt], mn[:ngt], ek, en, a.k)
                 step_ms = max(kms) + mms + ag_ms
+                if pts and pts[-1]["merged_recall_at_10"] >= 0.999:
+                    break  # (higher ef only adds time)
                 pts.append({"per_shard_ef": ef, "merged_recall_at_10": round(r_, 4),
                             "max_shard_search_ms": round(max(kms), 3), "min_shard_search_ms": round(min(kms), 3),
                             "merge_ms": round(mms, 4), "projected_step_ms": round(step_ms, 3),
@@ -688,6 +695,7 @@ def main():
         recall = mean_over_ranks(recall_at_k(res_k[:ngt], res_n[:ngt], tk, tn, a.k))
         elapsed, kernel_ms, st = timed_steps(step, g)
 
+    mark("replica_index_and_headline")
     # ---- shard layout: rank r owns rows [r*nbase, (r+1)*nbase) of one dataset --------
     shard_out = None
     shard_g = None
@@ -766,6 +774,7 @@ def main():
         sat99 = next((p_ for p_ in spoints if p_["recall_at_10"] >= 0.99), None)
         emu = None
         if world == 1 and a.emulate_shards > 1 and spoints:
+            mark("shard_leg")
             emu = emulate_shards(a.emulate_shards, Qs, ek, en, sat99)
         shard_out = {
             "value": round(a.batch * a.steps / s_el, 1), "unit": "queries/s",
@@ -826,6 +835,7 @@ def main():
     kms = float(np.mean(kernel_ms))
     achieved = alg_bytes / (kms * 1e-3) / 1e9
 
+    mark("shard_emulation" if (world == 1 and a.emulate_shards > 1) else "shard_leg")
     # other operating points of the same graph (N=1 only): recall / QPS per ef
     points = []
     if world == 1 and a.ef_sweep:
@@ -885,6 +895,7 @@ def main():
             bpoints.append({"batch": B, "ms_per_batch": round(dt * 1e3, 4), "qps": round(B / dt, 1),
                             "batches_timed": reps, "recall_at_10": None if r is None else round(r, 4)})
         g.device_status()
+    mark("operating_and_batch_points")
     traffic = None
     if os.path.exists(a.pmc_json):
         try:
@@ -954,6 +965,7 @@ def main():
                                "sequential fp32, pinned by tests/golden/reference_goldens.json")}, **par)
         par["pass"] = ok_
         out["parity"] = par
+        mark("oracle_parity_and_cpu_baseline")
         out["cpu_baseline"] = {
             "value": round(cb["beam"][0], 2), "unit": "queries/s", "cores": 1, "kind": "port",
             "sample": f"{cb['beam'][1]} searches cycling over 4096 of the step's queries, same 1M graph, oracle "
@@ -973,19 +985,24 @@ def main():
         cfg = {}
         if "0" in which:
             cfg["configs[0]"] = config0(device, a.cpu_seconds)
+            mark("configs0")
         if "2" in which:
             cfg["configs[2]"] = config2(device, a.build_expand)
+            mark("configs2")
         if "4" in which:
             cfg["configs[4]"] = config4(device)
+            mark("configs4")
         if "h" in which:
             try:  # an auxiliary leg: a failure here is reported, not fatal to the line
                 cfg["harder_data"] = config_harder(device, build_expand=a.harder_build_expand)
             except Exception as e:  # noqa: BLE001
                 cfg["harder_data"] = {"error": f"{type(e).__name__}: {e}"}
+            mark("harder_data")
         out["configs"] = cfg
     if rank == 0:
         # the measured parity and a compact summary go last, where a reader of the
         # line's tail (the driver keeps the last few KB) finds them
+        out["leg_seconds"] = {n_: round(t_ - tmarks[i][1], 1) for i, (n_, t_) in enumerate(tmarks[1:])}
         par_ = out.pop("parity", None)
         out["summary"] = summarize(out)
         out["parity"] = par_

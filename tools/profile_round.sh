@@ -1,13 +1,14 @@
 #!/bin/bash
-# Runs on the GPU box (via gpurun): bench line, rocprofv3 kernel-trace stats,
-# and separate FETCH_SIZE / WRITE_SIZE PMC passes of the same command.
+# Runs on the GPU box (via gpurun): rocprofv3 kernel-trace stats of the
+# headline phase of the driver's command (its step count, side legs off), and
+# separate FETCH_SIZE / WRITE_SIZE PMC passes of the same command and of the
+# configs[2] build (the full bench line is tools/gpu_run.sh's bench step).
 # Usage: bash tools/profile_round.sh TAG [bench args...]
 set -o pipefail
 TAG=$1; shift
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 420 python3 $R/bench.py "$@" > $O/bench.json 2> $O/bench.err || exit 1
 cd /tmp && export TMPDIR=/tmp
 # the driver's step count (--steps 20 --warmup 5): >= 20 launches of the headline kernel, side legs off
 PA="--steps 20 --warmup 5 --cpu-seconds 0 --ef-sweep= --batch-sweep= --configs= --no-shard-leg"
