@@ -835,7 +835,7 @@ def main():
     kms = float(np.mean(kernel_ms))
     achieved = alg_bytes / (kms * 1e-3) / 1e9
 
-    mark("shard_emulation" if (world == 1 and a.emulate_shards > 1) else "shard_leg")
+    mark("shard_emulation" if (shard_out or {}).get("emulated") else "shard_leg")
     # other operating points of the same graph (N=1 only): recall / QPS per ef
     points = []
     if world == 1 and a.ef_sweep:
