@@ -105,10 +105,11 @@ int mhnsw_seed(mhnsw_index *h, uint64_t seed); /* Rng = rand.New(rand.NewSource(
  * greedy), "beam_mw_max_b" (beam mode, ef and k <= 128: batches of at most this
  * many queries run one workgroup of 4 waves per query -- the single-query
  * latency path of ParallelSearch, graph.go:631-790; default 512, 0 = never;
- * results are identical either way), "build_mw_max" (batched insert: a layer launch of at most this
- * many inserts runs one workgroup of 4 waves per insert, the candidate batches of
- * its searches split over the waves; default 256, 0 = never; the same graph
- * either way), "vis_compact" (beam mode at max(ef, k) > 128 and batched insert at
+ * results are identical either way; the standard search only: search_expand 2 / 4
+ * run the one-wave kernel), "build_mw_max" (batched insert with the screening
+ * copy, build_expand 2-4: a layer launch of at most this many inserts runs one
+ * workgroup of 4 waves per insert, the candidate batches of its searches split
+ * over the waves; default 256, 0 = never; the same graph either way), "vis_compact" (beam mode at max(ef, k) > 128 and batched insert at
  * efConstruction > 128, default 1: when node
  * ids are below 2^24 the visited set stores 16-bit entries -- 8,192 ids in 16 KiB
  * of LDS, where the beam search's 32-bit set holds 5,120 in 20 KiB and the
