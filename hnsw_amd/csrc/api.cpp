@@ -354,7 +354,9 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
         a.n1 = a1;
         a.levels = h->levels;
         a.cur_entry = h->cur_entry;
-        a.ef = std::max(efc, mcap);
+        // upper_efc: a narrower candidate list in the layers above 0 (their rows hold M,
+        // their searches are the build's narrow, latency-bound launches)
+        a.ef = std::max(l > 0 && h->upper_efc > 0 ? std::min(efc, h->upper_efc) : efc, mcap);
         a.mcap = mcap;
         a.heuristic = h->heuristic;
         a.keep_pruned = h->keep_pruned;
@@ -1157,6 +1159,9 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
     } else if (n == "build_expand") {
         if (v < 1 || v > 4) return fail(h, MHNSW_EINVAL, "build_expand must be in [1, 4]");
         h->build_expand = (int)v;
+    } else if (n == "upper_efc") {
+        if (v < 0 || v > 512) return fail(h, MHNSW_EINVAL, "upper_efc must be in [0, 512]");
+        h->upper_efc = (int)v;
     } else if (n == "search_expand") {
         if (v != 1 && v != 2 && v != 4) return fail(h, MHNSW_EINVAL, "search_expand must be 1, 2 or 4");
         h->search_expand = (int)v;
@@ -1257,6 +1262,7 @@ int mhnsw_get_option(const mhnsw_index* h, const char* name, int64_t* v) {
     else if (n == "keep_pruned") *v = h->keep_pruned;
     else if (n == "build_expand") *v = h->build_expand;
     else if (n == "search_expand") *v = h->search_expand;
+    else if (n == "upper_efc") *v = h->upper_efc;
     else if (n == "prune_alpha_pct") *v = h->alpha_pct;
     else if (n == "batch_min") *v = h->batch_min;
     else if (n == "batch_max") *v = h->batch_max;

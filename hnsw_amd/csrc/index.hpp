@@ -64,6 +64,7 @@ struct mhnsw_index {
     int heuristic = 1;
     int keep_pruned = 0;
     int build_expand = 4;     // batched insert: entries expanded per step of its layer searches (1-4)
+    int upper_efc = 0;        // batched insert: candidate list of the layers above 0 (0 = efConstruction)
     int search_expand = 1;    // beam search: entries expanded per layer-0 step (1, 2, 4; 1 = standard)
     int alpha_pct = 100;
     int batch_min = 1, batch_max = 65536, batch_ratio_pct = 5;
