@@ -81,11 +81,16 @@ def parse():
                    help="entries expanded per step of the batched insert's layer searches (the engine default "
                         "since round 6; 4 builds the bench index 5.8 %% faster than 2 at the same recall@10, "
                         "0.9814 / 0.9904 at ef 48 / 64, profiles/r05_build_expand.txt)")
+    p.add_argument("--upper-efc", type=int, default=128,
+                   help="batched insert: candidate list of the layers above 0 (upper_efc; 0 = efConstruction): 128 "
+                        "builds the bench index 22 %% faster at recall@10 0.9903 / 0.9814 at ef 64 / 48 "
+                        "(0.9904 / 0.9814 with 0; profiles/r06_upper_efc.txt)")
     p.add_argument("--search-expand", type=int, default=1, choices=[1, 2, 4],
                    help="entries expanded per layer-0 step of the headline beam search (search_expand; 1 = the "
                         "standard search)")
     p.add_argument("--harder-build-expand", type=int, default=4, choices=[1, 2, 3, 4],
                    help="build_expand of the harder-data graph (configs 'h')")
+    p.add_argument("--harder-upper-efc", type=int, default=0, help="upper_efc of the harder-data graph")
     p.add_argument("--emulate-shards", type=int, default=8,
                    help="N=1 only: build --total-rows as this many node-ID range shards (one handle each) on the one "
                         "GPU, search every shard and merge, and project the N-GPU rate at equal recall (0 disables)")
@@ -357,7 +362,7 @@ def config4(device, steps=10):
                          "frac": round(flops / (gm * 1e-3) / 1e12 / 2500.0, 4), "traffic": None}}
 
 
-def config_harder(device, batch=16384, efs=(64, 128, 256, 384, 512), xws=(1, 2, 4), build_expand=4):
+def config_harder(device, batch=16384, efs=(64, 128, 256, 384, 512), xws=(1, 2, 4), build_expand=4, upper_efc=0):
     """Harder structured data (verdict item): the bench generator with latent
     dimension 32 instead of 12, 1M x 768 cosine, on the denser graph that data
     needs (M 32, M0 63, efConstruction 512, same heuristic/slack); recall@10
@@ -370,7 +375,7 @@ def config_harder(device, batch=16384, efs=(64, 128, 256, 384, 512), xws=(1, 2, 
     Q = gen_vectors(batch, d, 4321 + 7777, 32, 1000, device, "cosine")
     g = H.Graph(M=32, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_BATCH, m0=M0,
                 ef_construction=512, heuristic=2, keep_pruned=1, prune_alpha_pct=115, build_expand=build_expand,
-                screen=1, batch_ratio_pct=20, time_build=1)
+                upper_efc=upper_efc, screen=1, batch_ratio_pct=20, time_build=1)
     g.reserve(n, d)
     bt, _ = timed(lambda: g.add_device(np.arange(n), X.data_ptr(), n, d))
     bs = g.stats()
@@ -409,7 +414,8 @@ def config_harder(device, batch=16384, efs=(64, 128, 256, 384, 512), xws=(1, 2, 
     per_xw = {str(xw): next((p_ for p_ in points if p_["search_expand"] == xw and p_["recall_at_10"] >= 0.99), None)
               for xw in xws}
     out = {"workload": f"1M x 768-d cosine, latent dimension 32 (harder than the headline's 12), M=32 M0=63 "
-                       f"efConstruction=512 build_expand={build_expand} (batches of 20 % of the index), beam k=10, "
+                       f"efConstruction=512 build_expand={build_expand} upper_efc={upper_efc} (batches of 20 % of "
+                       f"the index), beam k=10, "
                        f"{batch} queries/step",
            "build_inserts_per_s": round(n / bt, 1),
            "build": build_roofline(bs, bt, n, d, M0, "cosine"),
@@ -534,7 +540,7 @@ def main():
         X = gen_vectors(nrows, a.dim, a.seed, a.intrinsic, a.clusters, device, a.metric, offset=off)
         g = H.Graph(M=a.M, Ml=0.25, EfSearch=a.ef, Distance=metric, Rng=rng_seed, build_mode=H.BUILD_BATCH,
                     m0=a.M0, ef_construction=a.efc, heuristic=2, keep_pruned=a.keep_pruned, prune_alpha_pct=a.alpha,
-                    build_expand=a.build_expand, batch_ratio_pct=a.batch_ratio,
+                    build_expand=a.build_expand, batch_ratio_pct=a.batch_ratio, upper_efc=a.upper_efc,
                     screen=a.screen, time_build=1)
         g.reserve(nrows, a.dim)
         keys = np.arange(off, off + nrows, dtype=np.int64)
@@ -805,7 +811,8 @@ def main():
         try:
             pm = json.load(open(a.pmc_build_json))
             want = dict(n=n, dim=a.dim, efc=a.efc, m0=a.M0, keep_pruned=a.keep_pruned, alpha=a.alpha,
-                        screen=a.screen, batch_ratio=a.batch_ratio, build_expand=a.build_expand, rev=KERNEL_REV)
+                        screen=a.screen, batch_ratio=a.batch_ratio, build_expand=a.build_expand,
+                        upper_efc=a.upper_efc, rev=KERNEL_REV)
             if all(pm.get(k) == v for k, v in want.items()):
                 return pm.get("hbm_bytes_total")
         except (OSError, ValueError):
@@ -930,6 +937,7 @@ def main():
             "n_base": a.nbase * (world if shard else 1), "dim": a.dim, "batch_per_gpu": a.batch, "ef": a.ef,
             "k": a.k, "M": a.M, "M0": a.M0, "ef_construction": a.efc, "keep_pruned": a.keep_pruned,
             "prune_alpha": a.alpha / 100, "batch_ratio_pct": a.batch_ratio, "build_expand": a.build_expand,
+            "upper_efc": a.upper_efc,
             "search_expand": a.search_expand,
             "screen": (("fp16"
                         + " row copy rejects candidates whose f32 distance provably exceeds the list's worst; "
@@ -994,7 +1002,8 @@ def main():
             mark("configs4")
         if "h" in which:
             try:  # an auxiliary leg: a failure here is reported, not fatal to the line
-                cfg["harder_data"] = config_harder(device, build_expand=a.harder_build_expand)
+                cfg["harder_data"] = config_harder(device, build_expand=a.harder_build_expand,
+                                                   upper_efc=a.harder_upper_efc)
             except Exception as e:  # noqa: BLE001
                 cfg["harder_data"] = {"error": f"{type(e).__name__}: {e}"}
             mark("harder_data")

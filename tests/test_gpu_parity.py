@@ -327,14 +327,19 @@ def _clustered(rng, n, d, nc=64, intrinsic=12, noise=0.05):
 
 
 @pytest.mark.parametrize("metric", [0, 1])
-@pytest.mark.parametrize("expand", [1, 2, 3, 4])
-def test_batch_build_recall_and_exact_parity(H, O, metric, expand):
+@pytest.mark.parametrize("expand,upper_efc", [(1, 0), (2, 0), (3, 0), (4, 0), (4, 32)])
+def test_batch_build_recall_and_exact_parity(H, O, metric, expand, upper_efc):
+    """The batched insert at every expansion width (build_expand) and with a
+    narrower candidate list above layer 0 (upper_efc): recall of the built graph,
+    no dropped reverse-edge proposals, and the oracle's exact and beam searches
+    on the same graph == the engine's."""
     rng = np.random.default_rng(11 + metric)
     n, d = 20000, 64
     X = _clustered(rng, n, d)
     Q = _clustered(rng, 200, d)
     g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=_metric_fn(H, metric), Rng=9, build_mode=H.BUILD_BATCH,
-                ef_construction=100, heuristic=2, build_expand=expand)
+                ef_construction=100, heuristic=2, build_expand=expand, upper_efc=upper_efc)
+    assert g.get_option("upper_efc") == upper_efc
     g.add_arrays(np.arange(n), X)
     st = g.stats()
     assert st["dropped_proposals"] == 0
