@@ -3,7 +3,8 @@ efConstruction 400, slack 1.15, keep-pruned, batches of 20 %, build_expand 4) wi
 narrower candidate list in the layers above 0 (option upper_efc): build time, the
 insert kernels' time, and recall@10 / QPS of the built graph at ef 48 / 64 on 65,536
 queries (recall against the exact path on 4,096 of them).
-Usage: python tools/upper_efc_probe.py [upper_efc ...]   (0 = efConstruction everywhere)"""
+Usage: python tools/upper_efc_probe.py [upper_efc ...]   (0 = efConstruction everywhere)
+       an argument may also be a colon-separated option list: upper_efc=128:batch_max=131072"""
 import os
 import sys
 import time
@@ -19,10 +20,13 @@ dev = torch.device("cuda")
 n, d, B = 1_000_000, 768, 65536
 X = gen_vectors(n, d, 1234, 12, 1000, dev, "cosine")
 Q = gen_vectors(B, d, 1234 + 7777, 12, 1000, dev, "cosine")
-for ue in [int(a) for a in sys.argv[1:]] or [0]:
+for arg in sys.argv[1:] or ["0"]:
+    opts = dict(kv.split("=") for kv in arg.split(":")) if "=" in arg else {"upper_efc": arg}
+    kw = dict(build_expand=4, batch_ratio_pct=20, upper_efc=0)
+    kw.update({k: int(v) for k, v in opts.items()})
+    ue = arg
     g = H.Graph(M=16, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=1234, build_mode=H.BUILD_BATCH, m0=40,
-                ef_construction=400, heuristic=2, keep_pruned=1, prune_alpha_pct=115, build_expand=4,
-                batch_ratio_pct=20, time_build=1, upper_efc=ue)
+                ef_construction=400, heuristic=2, keep_pruned=1, prune_alpha_pct=115, time_build=1, **kw)
     g.reserve(n, d)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
