@@ -24,7 +24,7 @@ namespace mh {
 
 // XW: entries expanded per step of the layer-0 search (option "search_expand";
 // 1 = the standard best-first search).  XW 1 is instantiated in beam_a-d.hip,
-// XW 2 and 4 in beam_x2.hip / beam_x4.hip.
+// XW 2 and 4 in beam_x2a/b.hip and beam_x4a/b.hip.
 template <int L, int V, int XW>
 int launch_beam_cfg(const SearchArgs& a, hipStream_t s);
 

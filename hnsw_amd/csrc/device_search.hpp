@@ -316,11 +316,13 @@ struct WaveBatch {
 // beam: sorted list of <= ef entries; stop when every entry is expanded
 // ---------------------------------------------------------------------------
 // XW: entries expanded per step.  1 is the standard best-first search (the
-// oracle's beam_layer_search; every search kernel).  2 (the batched insert's
-// layer search, option "build_expand"): the two best unexpanded entries are
-// expanded together -- their adjacency rows fetched in one round trip and
-// their new neighbours evaluated as one batch -- which halves the dependent
-// round trips of a search whose expansions yield few new candidates.
+// oracle's beam_layer_search with xw 1).  XW > 1 (the batched insert's layer
+// searches, option "build_expand"; the query search's layer 0, option
+// "search_expand"): the XW best unexpanded entries are expanded together --
+// their adjacency rows fetched in one round trip and their new neighbours
+// evaluated in batches of up to 64 against the worst entry before the step --
+// fewer dependent round trips for a search whose expansions yield few new
+// candidates.  The oracle restates it (beam_layer_search's xw).
 template <class C, int R, int G, bool COH = false, bool SCREEN = false, int XW = 1, class BEv = WaveBatch>
 __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_t entry, int ef, const QReg<C>& q, float qn,
                            BList<R>& L, uint32_t* vis, int vsize, WaveStats& st, const BEv& bev = BEv()) {

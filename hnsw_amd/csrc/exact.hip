@@ -721,7 +721,9 @@ __device__ __forceinline__ void wait_vm_plus(int extra, std::integer_sequence<in
 // the tile's first slice, double-buffered by tile parity.
 // DIAG (timing diagnostics, tools build only -- MH_EXACT_DIAG): 1 no epilogue,
 // 4 the filter's tests without the record stores (no pair passes: every query
-// takes the canonical fallback, results stay exact).
+// takes the canonical fallback, results stay exact); without an epilogue and
+// without results: 5 no LDS-DMA after the prologue's slices, 6 no fragment
+// reads after the first slice's, 7 no barriers in the main loop.
 // ---------------------------------------------------------------------------
 template <int EPI, int DIAG = 0, int NS = 4, int D = 2>
 __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
@@ -738,7 +740,8 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     // EPI 1: per tile (double-buffered by tile parity) the filter constants, by
     // LDS-DMA: 256 rows x {w0, w1, dead, -} (4 KiB), then c and s of 256 queries
     constexpr int CST = 6144, CSTB = NS * SL;
-    constexpr bool CONSTS = EPI == 1 && DIAG != 1;  // the filter constants' LDS copy (not read without an epilogue)
+    constexpr bool NOEPI = DIAG == 1 || DIAG >= 5;  // timing diagnostics without an epilogue
+    constexpr bool CONSTS = EPI == 1 && !NOEPI;  // the filter constants' LDS copy (not read without an epilogue)
     __shared__ __attribute__((aligned(16))) uint8_t ring[NS * SL + (CONSTS ? 2 * CST : 0)];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -823,7 +826,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
         const int64_t qt = L % nqt, nt = L / nqt;
         const int64_t q0 = qt * G_BM;
         const int64_t n0 = (EPI == 0 && a.nsample_tiles > 0 ? nt * a.tile_stride : nt) * G_BN;
-        if constexpr (DIAG == 1) {
+        if constexpr (NOEPI) {
 #pragma unroll
             for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -949,16 +952,16 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
     else
         __builtin_amdgcn_s_waitcnt(VMCNT0);
     __builtin_amdgcn_s_barrier();
-    if (g == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
+    if (g == 1 && DIAG != 7) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
 
     int64_t c_tile = 0;
     int c_kt = 0, c_slot = 0;
+    f16x8 fa[8], fb[4];
     for (int64_t x = 0; x < S; ++x) {
         // R: fragments of slice x, DMA of slice x + D
         const uint32_t sb = ring_lds + (uint32_t)c_slot * SL;
         if (++c_slot == NS) c_slot = 0;
-        f16x8 fa[8], fb[4];
-        {
+        if (DIAG != 6 || x == 0) {
             const uint32_t va = sb + offA + lfix, vb = sb + offB + lfix;
             MH_DSR(fa[0], va, 0);
             MH_DSR(fa[1], va, 1024);
@@ -995,7 +998,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
             }
         }
         if (ps < S) {
-            produce();
+            if constexpr (DIAG != 5) produce();
             ++ps;
         }
         const bool tail = x + 1 + D > S;  // fewer than D slices left in flight: retire them all
@@ -1010,7 +1013,7 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                              : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]),
                                "+v"(fa[6]), "+v"(fa[7]), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]));
         }
-        __builtin_amdgcn_s_barrier();
+        if constexpr (DIAG != 7) __builtin_amdgcn_s_barrier();
         // M: 32 MFMAs (+ the epilogue after a tile's last slice)
         asm volatile("s_waitcnt lgkmcnt(0)"
                      : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]), "+v"(fa[6]),
@@ -1043,9 +1046,9 @@ __global__ __launch_bounds__(512) void k_h1_pp16(ExactArgs a) {
                 wait_vmc();
             nst = 0;
         }
-        __builtin_amdgcn_s_barrier();
+        if constexpr (DIAG != 7) __builtin_amdgcn_s_barrier();
     }
-    if (g == 0) __builtin_amdgcn_s_barrier();  // evens the barrier count
+    if (g == 0 && DIAG != 7) __builtin_amdgcn_s_barrier();  // evens the barrier count
     __builtin_amdgcn_s_waitcnt(VMCNT0);
     if constexpr (DIAG > 0) {
         if (lane == 0 && keep == -1.0e38f) a.region_cnt[0] = 1;
@@ -1086,6 +1089,9 @@ static int launch_h1(const ExactArgs& a, int variant, hipStream_t s) {
         case 32: return launch_h1_pp16_t<EPI, EPI ? 1 : 0, 5, 3>(a, s);  // no epilogue, 3 slices in flight (160 KiB ring)
         case 36: return launch_h1_pp16_t<EPI, EPI ? 1 : 0, 4, 3>(a, s);  // no epilogue, 3 in flight, 4-slot ring (RSYNC)
         case 33: return launch_h1_pp16_t<EPI, 0, 4, 3>(a, s);  // with the epilogue, 3 in flight (RSYNC)
+        case 37: return launch_h1_pp16_t<EPI, EPI ? 5 : 0>(a, s);  // no epilogue, no DMA after the prologue
+        case 38: return launch_h1_pp16_t<EPI, EPI ? 6 : 0>(a, s);  // no epilogue, no fragment reads after slice 0
+        case 39: return launch_h1_pp16_t<EPI, EPI ? 7 : 0>(a, s);  // no epilogue, no main-loop barriers
 #endif
         default: return launch_h1_pp16_t<EPI>(a, s);
     }
@@ -1127,7 +1133,9 @@ int launch_h1_rowconst(const float* xinv, const float* xnorm, const uint8_t* dea
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 // tools build (MH_EXACT_DIAG): the timing diagnostics, which let no pair pass
-bool h1_timing_diag(int variant) { return variant == 30 || variant == 31 || variant == 32 || variant == 36; }
+bool h1_timing_diag(int variant) {
+    return variant == 30 || variant == 31 || variant == 32 || variant == 36 || (variant >= 37 && variant <= 39);
+}
 // regions per tile of a variant's fused filter (k_h1_pp16: one per wave)
 int h1_region_split(int variant) { return variant == 5 ? 1 : 8; }  // (an effective variant)
 // the variant's regions hold records (H1_REC uint2 each: a lane's 16 accumulators of one
