@@ -1194,7 +1194,7 @@ int mhnsw_set_option(mhnsw_index* h, const char* name, int64_t v) {
         // ring three slices deep)
         bool ok = (v >= 0 && v <= 3) || v == 5 || v == 34;
 #ifdef MH_EXACT_DIAG
-        ok = ok || v == 30 || v == 31 || v == 32 || v == 33 || v == 36 || (v >= 37 && v <= 39);
+        ok = ok || v == 30 || v == 31 || v == 32 || v == 33 || v == 36 || (v >= 37 && v <= 41);
 #endif
         if (!ok) return fail(h, MHNSW_EINVAL, "exact_tile must be 0-3, 5 or 34");
         h->exact_tile = (int)v;

@@ -37,7 +37,7 @@ def run():
     try:
         S.run(Q, H.MODE_EXACT, 0)
     except H.HnswError as e:  # exact_tile 30-32, 36-39 (MHNSW_LIB=tools/libmhnsw_diag.so): no results
-        if tile not in (30, 31, 32, 36, 37, 38, 39):
+        if tile not in (30, 31, 32, 36, 37, 38, 39, 41):
             raise
         assert "timing diagnostic" in str(e)
 
