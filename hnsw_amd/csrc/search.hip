@@ -173,11 +173,14 @@ __global__ __launch_bounds__(256) void k_sweep_raw(const float* __restrict__ q, 
 // The same sweep for 16-B aligned rows with dim % 4 == 0 (the common case):
 // lane l loads its elements as float4 (one 1-KiB wave instruction per 256
 // elements), the query and its canonical |q| stay in registers for every row
-// of a grid-stride loop, two rows in flight per step.  Identical arithmetic
-// order, so identical bits.  HBM-bound: n * dim * 4 bytes per query.
+// of a grid-stride loop, RP rows in flight per step (4 up to 1,024-d, else 2),
+// read with non-temporal loads (each row is read once: no point keeping it in
+// the caches).  Identical arithmetic order, so identical bits.  HBM-bound:
+// n * dim * 4 bytes per query.
 template <int VPL>
 __global__ __launch_bounds__(256) void k_sweep_raw4(const float* __restrict__ q, const float* __restrict__ X,
                                                     int64_t n, int dim, int metric, float* __restrict__ out) {
+    constexpr int RP = VPL <= 4 ? 4 : 2;
     const int lane = lane_id();
     const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t nw = (int64_t)gridDim.x * 4;
@@ -195,20 +198,23 @@ __global__ __launch_bounds__(256) void k_sweep_raw4(const float* __restrict__ q,
         }
     }
     const float qn = metric == COSINE ? sqrtf(seg_allreduce<64>(qq)) : 1.f;
-    for (int64_t r0 = gw * 2; r0 < n; r0 += nw * 2) {
-        float4 xv[2][VPL];
+    for (int64_t r0 = gw * RP; r0 < n; r0 += nw * RP) {
+        float4 xv[RP][VPL];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < RP; ++h) {
             const int64_t row = r0 + h < n ? r0 + h : r0;
             const float* x = X + (size_t)row * dim;
 #pragma unroll
             for (int v = 0; v < VPL; ++v) {
                 const int e = v * 256 + 4 * lane;
-                xv[h][v] = e < dim ? *reinterpret_cast<const float4*>(x + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+                typedef float f4v __attribute__((ext_vector_type(4)));
+                f4v t = {0.f, 0.f, 0.f, 0.f};
+                if (e < dim) t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x + e));
+                xv[h][v] = make_float4(t.x, t.y, t.z, t.w);
             }
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < RP; ++h) {
             float acc = 0.f, xx = 0.f;
 #pragma unroll
             for (int v = 0; v < VPL; ++v) {
@@ -246,7 +252,7 @@ int launch_sweep_raw(const float* q, const float* X, int64_t n, int dim, int met
     const bool vec = dim % 4 == 0 && dim <= 4096 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)X & 15) == 0;
     if (vec) {
         const int vpl = (dim + 255) / 256;
-        const int grid = (int)std::min<int64_t>((n + 7) / 8, 4096);
+        const int grid = (int)std::min<int64_t>((n + 15) / 16, 4096);
 #define SW_(V)                                                                                            \
     if (vpl <= V) {                                                                                       \
         hipLaunchKernelGGL(k_sweep_raw4<V>, dim3((unsigned)grid), dim3(256), 0, s, q, X, n, dim, metric, out); \
