@@ -132,3 +132,28 @@ def test_dog_query_hack_opt_in(H):
     assert 3 not in [n.Key for n in g.Search([1.0, 0.2, 0.1000001], 3)]  # not the dog query
     assert 3 not in [n.Key for n in g.BatchSearch([dog], 3)[0]]         # BatchSearch has no hack (graph.go:1047)
     g.close()
+
+
+@pytest.mark.parametrize("mode", ["batch", "flat"])
+def test_batched_add_rejects_present_keys(H, mode):
+    """The batched and flat builds have no reference semantics for a present key
+    (graph.go:1015-1024 replaces it in BatchAdd's walk; compat mode does that):
+    they reject the whole Add -- a key repeated inside the batch (in increasing,
+    decreasing or shuffled key order) or one the index already holds -- and
+    leave the index as it was."""
+    bm = H.BUILD_BATCH if mode == "batch" else H.BUILD_FLAT
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(600, 16)).astype(np.float32)
+    g = H.Graph(M=8, Ml=0.25, EfSearch=20, Distance=H.EuclideanDistance, build_mode=bm)
+    g.add_arrays(np.arange(0, 400, 2), X[:200])  # increasing keys: the map-free duplicate check
+    assert len(g) == 200
+    for keys in (np.array([1001, 1003, 1003, 1005]), np.array([1009, 1007, 1007, 1005]),
+                 rng.permutation(np.array([1011, 1013, 1015, 1013])), np.array([2001, 2003, 4, 2005])):
+        with pytest.raises(H.HnswError, match="duplicate key"):
+            g.add_arrays(keys, X[200:200 + len(keys)])
+        assert len(g) == 200
+    g.add_arrays(np.array([3001, 3000, 3002]), X[300:303])  # not increasing, no repeat: accepted
+    assert len(g) == 203
+    gk, _, gn = g.search_arrays(X[300:303], 1, mode=H.MODE_EXACT)
+    assert gk[:, 0].tolist() == [3001, 3000, 3002]
+    g.close()
