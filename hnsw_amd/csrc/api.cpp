@@ -6,6 +6,7 @@
 // per-node levels and per-layer counts/entries.
 #include "index.hpp"
 
+#include <functional>
 #include <unordered_set>
 
 using namespace mhh;
@@ -415,7 +416,8 @@ int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t e
 }
 
 // top / entry: the live top layer and its entry before this batch (-1: empty graph)
-int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1, int top, uint32_t entry) {
+int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1, int top, uint32_t entry,
+                    const std::function<void()>& while_gpu) {
     int r;
     if ((r = zero_err(h))) return r;
     if (!h->inc_src) {
@@ -457,6 +459,7 @@ int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1, int top, uint32_t en
     }
     int err = 0;
     HIPCHK(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    if (while_gpu) while_gpu();  // host work that overlaps the last batches' kernels
     HIPCHK(h, hipStreamSynchronize(h->stream));
     if (err & 4) return fail(h, MHNSW_EINTERNAL, "out-of-range node id in adjacency (graph corrupt)");
     return 0;
@@ -617,6 +620,10 @@ int add_step(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     const size_t hm0 = h->hmask.size(), hd0 = h->hdead.size(), hl0 = h->hlevels.size(), hk0 = h->hkid.size();
     const size_t hp0 = h->hprev.size();
     const size_t nlay0 = h->layers.size();
+    // the batched and flat builds publish the new keys in the key map while the
+    // device builds (no step of the build reads the map; 1M map inserts are tens
+    // of ms of host time)
+    const bool defer_keys = !compat && !h->aliased;
     h->hmask.resize(n0 + n + 1, 0u);
     h->hdead.resize(n0 + n + 1, 0);
     int nl = top0 + 1;
@@ -661,7 +668,7 @@ int add_step(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
                 auto kp = h->key2id.find(keys[i]);
                 h->hprev[id] = kp != h->key2id.end() ? kp->second : -1;
             }
-            h->key2id[keys[i]] = id;
+            if (!defer_keys) h->key2id[keys[i]] = id;
         } else if (snap_dead_kid.count(keys[i])) {  // failed before touching a layer: still a deleted key
             h->dead_kid[keys[i]] = snap_dead_kid[keys[i]];
         }
@@ -928,10 +935,17 @@ int add_step(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
     if ((r = h16_rows(h, n0, n1))) return r;
     h->layers_exist = true;
     h->n = n1;
+    bool published = !defer_keys;
+    auto publish_keys = [&]() {
+        if (published) return;
+        for (int64_t i = 0; i < nfresh; ++i) h->key2id[keys[i]] = (int32_t)(n0 + i);
+        published = true;
+    };
     if (flat) {  // members of layer 0 without links (an empty neighbour map, not an absent node)
         r = hipMemsetD32Async((hipDeviceptr_t)(h->layers[0].deg + n0), 0, (size_t)n, h->stream) == hipSuccess
                 ? 0
                 : fail(h, MHNSW_EDEVICE, "device memset failed");
+        publish_keys();
     } else if (compat) {
         CompatRep cr;
         if (rep >= 0) cr = CompatRep{rep_level, rep_i0, ida >= 0 ? ida : idb, idb, rep_entry, rep_sweep};
@@ -954,7 +968,8 @@ int add_step(mhnsw_index* h, const int64_t* keys, const float* vecs, bool vecs_o
                 cont = rep + 1;
         }
     } else {
-        r = run_build_batch(h, n0, n1, top_live, entry_live);
+        r = run_build_batch(h, n0, n1, top_live, entry_live, publish_keys);
+        publish_keys();  // (an early device error: the rows exist, so do their keys)
     }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     for (size_t i = 0; i + 1 < h->tev_used; i += 2) {

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <shared_mutex>
 #include <string>
+#include <functional>
 #include <unordered_map>
 #include <vector>
 
@@ -231,7 +232,8 @@ int set_deg(mhnsw_index* h, int l, int64_t id, int32_t v);
 int sync_layer_entries(mhnsw_index* h);
 int zero_err(mhnsw_index* h);
 int run_batch_layers(mhnsw_index* h, int64_t a0, int64_t a1, int top, uint32_t entry);
-int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1, int top, uint32_t entry);
+int run_build_batch(mhnsw_index* h, int64_t n0, int64_t n1, int top, uint32_t entry,
+                    const std::function<void()>& while_gpu = nullptr);
 int h16_rows(mhnsw_index* h, int64_t r0, int64_t r1);
 int32_t kid_of_row(const mhnsw_index* h, int64_t r);
 int set_kidlive(mhnsw_index* h, int32_t kid, int32_t row);
