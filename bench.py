@@ -366,7 +366,8 @@ def config4(device, steps=10):
                          "frac": round(flops / (gm * 1e-3) / 1e12 / 2500.0, 4), "traffic": None}}
 
 
-def config_harder(device, batch=16384, efs=(64, 128, 256, 384, 512), xws=(1, 2, 4), build_expand=4, upper_efc=0):
+def config_harder(device, batch=16384, efs=(64, 128, 256, 384, 512), xws=(1, 2, 4), build_expand=4, upper_efc=0,
+                  fine_efs=(448, 480, 496)):
     """Harder structured data (verdict item): the bench generator with latent
     dimension 32 instead of 12, 1M x 768 cosine, on the denser graph that data
     needs (M 32, M0 63, efConstruction 512, same heuristic/slack); recall@10
@@ -390,7 +391,8 @@ def config_harder(device, batch=16384, efs=(64, 128, 256, 384, 512), xws=(1, 2, 
     points = []
     for xw in xws:
         g.set_option("search_expand", xw)
-        for ef in efs:
+        # the widest expansion also between ef 384 and 512, where recall crosses 0.99
+        for ef in sorted(set(efs) | (set(fine_efs) if xw == max(xws) else set())):
             kk, _, nn = (x.clone() for x in S.run(Q, H.MODE_BEAM, ef))
             r = recall_at_k(kk[:ngt], nn[:ngt], tk, tn, 10)
             g.reset_stats()
