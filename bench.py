@@ -367,7 +367,7 @@ def config4(device, steps=10):
 
 
 def config_harder(device, batch=16384, efs=(64, 128, 256, 384, 512), xws=(1, 2, 4), build_expand=4, upper_efc=0,
-                  fine_efs=(448, 480, 496)):
+                  fine_efs=(448, 480, 496), opts=None):
     """Harder structured data (verdict item): the bench generator with latent
     dimension 32 instead of 12, 1M x 768 cosine, on the denser graph that data
     needs (M 32, M0 63, efConstruction 512, same heuristic/slack); recall@10
@@ -378,9 +378,10 @@ def config_harder(device, batch=16384, efs=(64, 128, 256, 384, 512), xws=(1, 2, 
     n, d, M0 = 1_000_000, 768, 63
     X = gen_vectors(n, d, 4321, 32, 1000, device, "cosine")
     Q = gen_vectors(batch, d, 4321 + 7777, 32, 1000, device, "cosine")
-    g = H.Graph(M=32, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_BATCH, m0=M0,
-                ef_construction=512, heuristic=2, keep_pruned=1, prune_alpha_pct=115, build_expand=build_expand,
-                upper_efc=upper_efc, screen=1, batch_ratio_pct=20, time_build=1)
+    kw = dict(ef_construction=512, heuristic=2, keep_pruned=1, prune_alpha_pct=115, build_expand=build_expand,
+              upper_efc=upper_efc, screen=1, batch_ratio_pct=20, time_build=1)
+    kw.update(opts or {})  # (tools/harder_probe.py: other graph options)
+    g = H.Graph(M=32, Ml=0.25, EfSearch=64, Distance=H.CosineDistance, Rng=5, build_mode=H.BUILD_BATCH, m0=M0, **kw)
     g.reserve(n, d)
     bt, _ = timed(lambda: g.add_device(np.arange(n), X.data_ptr(), n, d))
     bs = g.stats()

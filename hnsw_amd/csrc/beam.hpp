@@ -94,8 +94,18 @@ __device__ __forceinline__ void beam_stats(const SearchArgs& a, const WaveStats&
     }
 }
 
+// MH_BEAM_WIDE_G / MH_BEAM_WIDE_WAVES (build flags, for tools/ variants): rows
+// in flight per wave step and the waves per SIMD the compiler must fit, for the
+// 512-entry list (R = 8); 0 = the configuration's G and 2 waves
+#ifndef MH_BEAM_WIDE_G
+#define MH_BEAM_WIDE_G 0
+#endif
+#ifndef MH_BEAM_WIDE_WAVES
+#define MH_BEAM_WIDE_WAVES 2
+#endif
 template <class C, int R, int G, bool SCREEN, int XW>
-__global__ __launch_bounds__(64, 2) void k_search_beam(SearchArgs a) {
+__global__ __attribute__((amdgpu_flat_work_group_size(64, 64), amdgpu_waves_per_eu(R >= 8 ? MH_BEAM_WIDE_WAVES : 2)))
+void k_search_beam(SearchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int64_t b = blockIdx.x;
     if (b >= a.B) return;
@@ -191,7 +201,8 @@ int launch_beam_cfg(const SearchArgs& a, hipStream_t s) {
     if (efl <= 64) return launch_beam_t<Cfg<L, V>, 1, G, XW>(a, s);
     if (efl <= 128) return launch_beam_t<Cfg<L, V>, 2, G, XW>(a, s);
     if (efl <= 256) return launch_beam_t<Cfg<L, V>, 4, G, XW>(a, s);
-    if (efl <= 512) return launch_beam_t<Cfg<L, V>, 8, G, XW>(a, s);
+    constexpr int GW = MH_BEAM_WIDE_G > 0 && MH_BEAM_WIDE_G < G ? MH_BEAM_WIDE_G : G;
+    if (efl <= 512) return launch_beam_t<Cfg<L, V>, 8, GW, XW>(a, s);
     return -4;
 }
 

@@ -11,6 +11,7 @@
 #     rehearse2          the driver's N=2 command as 2 gloo ranks on this one GPU
 #     prof[:A,B,...]     tools/profile_round.sh TAG (kernel trace + FETCH/WRITE PMC) with A B ...
 #     py:SCRIPT[,A,...]  python SCRIPT A ... (a tools/ probe)
+#     pyl:LIB,SCRIPT[,A,...]  the same on tools/LIB (a tools/Makefile.beam variant; push it: take it out of .gpurunignore)
 #     gemm:T,...         tools/gemm_diag.sh T ... (configs[4] exact path, rocprofv3 stats per exact_tile T)
 #     diag:T,...         the same on tools/libmhnsw_diag.so (timing-diagnostic variants; needs the .so
 #                        pushed: take ./tools/libmhnsw_*.so out of .gpurunignore for that call)
@@ -41,6 +42,8 @@ for step in "$@"; do
         --backend gloo $args > "$O/$i.rehearse2.json" 2> "$log" ;;
     prof) timeout -k 10 1100 bash tools/profile_round.sh "$TAG/prof$i" $args > "$log" 2>&1 ;;
     py) timeout -k 10 900 python -u $args > "$log" 2>&1 ;;
+    pyl) set -- $args && lib=$1 && shift &&
+        MHNSW_LIB=$PWD/tools/$lib timeout -k 10 900 python -u "$@" > "$log" 2>&1 ;;
     gemm) timeout -k 10 900 bash tools/gemm_diag.sh $args > "$log" 2>&1 ;;
     diag) MHNSW_LIB=$PWD/tools/libmhnsw_diag.so timeout -k 10 900 bash tools/gemm_diag.sh $args > "$log" 2>&1 ;;
     cprof) MHNSW_LIB=$PWD/tools/libmhnsw_cprof.so timeout -k 10 600 python -u tools/cprof_probe.py > "$log" 2>&1 &&
