@@ -323,6 +323,11 @@ struct WaveBatch {
 // evaluated in batches of up to 64 against the worst entry before the step --
 // fewer dependent round trips for a search whose expansions yield few new
 // candidates.  The oracle restates it (beam_layer_search's xw).
+// MH_SCREEN_PAD (a build flag for tools/ variants, default 0): widens the
+// screen's margin, to measure how the rejections fall off with a looser bound
+#ifndef MH_SCREEN_PAD
+#define MH_SCREEN_PAD 0.f
+#endif
 template <class C, int R, int G, bool COH = false, bool SCREEN = false, int XW = 1, class BEv = WaveBatch>
 __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_t entry, int ef, const QReg<C>& q, float qn,
                            BList<R>& L, uint32_t* vis, int vsize, WaveStats& st, const BEv& bev = BEv()) {
@@ -341,6 +346,7 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
     if constexpr (SCREEN) {
         const float e = g.h16err ? *g.h16err : 0.00048828125f;
         margin = g.metric == EUCLIDEAN ? h16_margin_l2(e) : h16_margin_cos(e);
+        margin += MH_SCREEN_PAD;
     }
     const int32_t* degp = g.layers[layer].deg;
     const int32_t* adjp = g.layers[layer].adj;
