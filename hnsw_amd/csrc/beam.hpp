@@ -33,6 +33,9 @@ int launch_beam_cfg(const SearchArgs& a, hipStream_t s);
 // ---------------------------------------------------------------------------
 // One query b: greedy descent, the layer-0 beam, and its first k live entries
 // into the outputs.  BEv scores each batch of candidates (beam_layer).
+// the visited set's LDS words (the merge scratch follows it)
+__host__ __device__ inline int beam_vis_words(const SearchArgs& a) { return a.vis16 ? VIS16_WORDS : a.vis_n; }
+
 template <class C, int R, int G, bool SCREEN, int XW, class BEv>
 __device__ __forceinline__ void beam_query(const SearchArgs& a, int64_t b, const QReg<C>& q, float qn, uint32_t* smem,
                                            WaveStats& st, const BEv& bev) {
@@ -57,7 +60,12 @@ __device__ __forceinline__ void beam_query(const SearchArgs& a, int64_t b, const
     BList<R> L;
     const int efl = a.ef > a.k ? a.ef : a.k;
     if (a.g.layers[0].deg[ep] == -2) ep = (uint32_t)a.layer_entry[0];
-    beam_layer<C, R, G, false, SCREEN, XW>(a.g, 0, ep, efl, q, qn, L, smem, vsz, st, bev);
+    // lists of 256 / 512 entries merge each step's candidates at once, with the
+    // LDS past the visited set as scratch (launch_beam_t sizes the LDS for it;
+    // the default compact set leaves room in the 20 KiB a 2-wave SIMD allows)
+    constexpr bool MRG = R >= 4;
+    float* mrg = MRG ? reinterpret_cast<float*>(smem + beam_vis_words(a)) : nullptr;
+    beam_layer<C, R, G, false, SCREEN, XW, MRG>(a.g, 0, ep, efl, q, qn, L, smem, vsz, st, bev, mrg);
     // compact the sorted list into the first k live entries (deleted rows
     // route the search but are never returned)
     int nvalid = 0;
@@ -91,6 +99,13 @@ __device__ __forceinline__ void beam_stats(const SearchArgs& a, const WaveStats&
         if (st.resets) atomicAdd(&a.stats[2], st.resets);
         atomicAdd(&a.stats[8], st.S);
         atomicAdd(&a.stats[9], st.F);
+#ifdef MH_PROF_BEAM
+        // (tools-only: the slots the batched insert uses, read back as build_screened /
+        // build_f32_rows / exact_uncertified)
+        atomicAdd(&a.stats[10], st.c_ins);
+        atomicAdd(&a.stats[11], st.c_score);
+        atomicAdd(&a.stats[3], st.c_all);
+#endif
     }
 }
 
@@ -163,7 +178,7 @@ __global__ __launch_bounds__(64 * BMW_WAVES) void k_search_beam_mw(SearchArgs a)
 
 template <class C, int R, int G, int XW>
 static int launch_beam_t(const SearchArgs& a, hipStream_t s) {
-    const size_t lds = (size_t)4 * (size_t)a.vis_n;
+    const size_t lds = (size_t)4 * (size_t)(R >= 4 ? std::max(a.vis_n, beam_vis_words(a) + BL_MERGE_WORDS) : a.vis_n);
     // small batch: a workgroup per query (the standard search only; a wider
     // expansion runs the one-wave kernel at every batch size)
     if constexpr (XW == 1) {

@@ -231,6 +231,11 @@ __device__ __forceinline__ int screen_pairs(const GraphDev& g, const QReg<C>& q,
 struct WaveStats {
     unsigned long long E = 0, X = 0, resets = 0;
     unsigned long long S = 0, F = 0;  // rows screened on the fp16 copy / rows evaluated in f32
+#ifdef MH_PROF_BEAM
+    // (tools-only build, tools/Makefile.beam: shader-clock cycles of the layer-0
+    // beam spent in list insertions, in candidate scoring, and in all)
+    unsigned long long c_ins = 0, c_score = 0, c_all = 0;
+#endif
 };
 
 // Orders the lanes of ONE wave (compiler ordering only: a wave's vector memory
@@ -296,6 +301,105 @@ __device__ __forceinline__ int vis_any_cap(int vsize) { return vsize < 0 ? VIS16
 #define MH_VIS_FULL(n) (((n) >> 1) + ((n) >> 2))
 #endif
 
+// Batched list update (the query search's 256- and 512-entry lists, beam_layer
+// MERGE): a step's candidates that beat the list's worst entry are collected,
+// one per lane, and merged into the list once per step instead of one
+// bl_insert each.  bl_insert keeps the best ef of the list and everything
+// offered to it, whatever the order (it drops a candidate only when it is no
+// better than the worst entry or already listed), so the merge leaves the list
+// bl_insert would, expansion marks included.  Fast path, every distance finite
+// and distinct: the buffer is sorted over the lanes (bitonic), each candidate
+// ranked in the list by a binary search over the list's distances in LDS (A,
+// ef floats), every list entry moved down by the candidates ranked at or before
+// it, and both written into A at their new places and read back (distances,
+// then ids).  A candidate whose distance equals a listed one (the same row met
+// again, or equal rows) or any infinite distance sends the buffer through
+// bl_insert instead.  LDS scratch M: A = M[0, 512) (the list), the k <= 64
+// candidates in M[512 + j] (distance) and M[576 + j] (id), in arrival order.
+constexpr int BL_MERGE_WORDS = 640;
+template <int R>
+__device__ __forceinline__ void bl_merge(BList<R>& L, int ef, int k, float* M) {
+    const int lane = lane_id();
+    const float INF = __int_as_float(0x7f800000);
+    float* A = M;
+    wave_sync();  // (the buffer was written by lane 0)
+    const float bd = lane < k ? M[512 + lane] : INF;
+    const uint32_t bi = lane < k ? reinterpret_cast<const uint32_t*>(M)[576 + lane] : EMPTY_ID;
+    float d = bd;
+    uint32_t id = lane < k ? bi : EMPTY_ID;
+    bool slow = __ballot(lane < k && !(bd < INF)) != 0;
+    int lb = 0;  // lane j < k: the list entries (of the first ef) below candidate j
+    if (!slow) {
+        int P = 1;
+        while (P < k) P <<= 1;
+        for (int size = 2; size <= P; size <<= 1) {
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                const float pd = __shfl_xor(d, stride, 64);
+                const uint32_t pi = (uint32_t)__shfl_xor((int)id, stride, 64);
+                const bool keep_min = ((lane & stride) == 0) == ((lane & size) == 0);
+                if (keep_min ? pd < d : pd > d) {
+                    d = pd;
+                    id = pi;
+                }
+            }
+        }
+        const float prev = __shfl_up(d, 1, 64);
+        slow = __ballot(lane > 0 && lane < k && prev == d) != 0;
+    }
+    if (!slow) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (r * 64 + lane < ef) A[r * 64 + lane] = L.d[r];
+        wave_sync();
+        if (lane < k) {
+            // lower bound over A[0, ef); a candidate is below the worst entry, so lb < ef
+#pragma unroll
+            for (int step = R * 32; step >= 1; step >>= 1) {
+                const int t = lb + step - 1;
+                if (t < ef && A[t] < d) lb += step;
+            }
+        }
+        slow = __ballot(lane < k && (lb >= ef || A[lb] == d)) != 0;
+        wave_sync();
+    }
+    if (slow) {
+        for (int j = 0; j < k; ++j) bl_insert(L, ef, rl_f(bd, j), rl_u(bi, j));
+        return;
+    }
+    int sh[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) sh[r] = 0;
+    for (int j = 0; j < k; ++j) {
+        const int lj = rl_i(lb, j);
+#pragma unroll
+        for (int r = 0; r < R; ++r) sh[r] += (r * 64 + lane >= lj) ? 1 : 0;
+    }
+    const int pos = lane + lb;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = r * 64 + lane;
+        if (i < ef && i + sh[r] < ef) A[i + sh[r]] = L.d[r];
+    }
+    if (lane < k && pos < ef) A[pos] = d;
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (r * 64 + lane < ef) L.d[r] = A[r * 64 + lane];
+    wave_sync();
+    uint32_t* AI = reinterpret_cast<uint32_t*>(A);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = r * 64 + lane;
+        if (i < ef && i + sh[r] < ef) AI[i + sh[r]] = L.i[r];
+    }
+    if (lane < k && pos < ef) AI[pos] = id;
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (r * 64 + lane < ef) L.i[r] = AI[r * 64 + lane];
+    wave_sync();
+}
+
 // How beam_layer scores one batch of new candidates (ids in lanes 0..cnt-1 of
 // cid) and hands the survivors to its sink: WaveBatch does it on the calling
 // wave; the multi-wave single-query kernel (beam.hpp MwBatch) spreads the rows
@@ -328,9 +432,14 @@ struct WaveBatch {
 #ifndef MH_SCREEN_PAD
 #define MH_SCREEN_PAD 0.f
 #endif
-template <class C, int R, int G, bool COH = false, bool SCREEN = false, int XW = 1, class BEv = WaveBatch>
+// MERGE (the query search's layer 0 at ef > 128): the step's candidates go
+// through bl_merge once per step, with `mrg` (BL_MERGE_WORDS of LDS) as its
+// scratch.
+template <class C, int R, int G, bool COH = false, bool SCREEN = false, int XW = 1, bool MERGE = false,
+          class BEv = WaveBatch>
 __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_t entry, int ef, const QReg<C>& q, float qn,
-                           BList<R>& L, uint32_t* vis, int vsize, WaveStats& st, const BEv& bev = BEv()) {
+                           BList<R>& L, uint32_t* vis, int vsize, WaveStats& st, const BEv& bev = BEv(),
+                           float* mrg = nullptr) {
     const int lane = lane_id();
     bl_init(L);
     if (entry == EMPTY_ID) return;
@@ -351,6 +460,17 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
     const int32_t* degp = g.layers[layer].deg;
     const int32_t* adjp = g.layers[layer].adj;
     const int capl = g.layers[layer].cap;
+#ifdef MH_PROF_BEAM
+    const unsigned long long tl0 = clock64();
+    struct AllClock {  // adds the layer-0 search's cycles at every exit
+        WaveStats& st;
+        unsigned long long t0;
+        int layer;
+        __device__ ~AllClock() {
+            if (layer == 0) st.c_all += clock64() - t0;
+        }
+    } all_clock{st, tl0, layer};
+#endif
     for (;;) {
         uint32_t cur[XW];
         cur[0] = bl_next(L);
@@ -408,10 +528,9 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
             }
         }
         float wd = __int_as_float(0x7f800000);
-        if constexpr (SCREEN) {
-            uint32_t wi;
-            bl_at(L, ef - 1, wd, wi);  // the worst before the step: it only decreases during it
-        }
+        uint32_t wi = EMPTY_ID;
+        if constexpr (SCREEN || MERGE) bl_at(L, ef - 1, wd, wi);  // the worst before the step: it only decreases during it
+        int bk = 0;  // MERGE: the step's candidates below that worst, in mrg's buffer
         // the batches are taken from slot 0 and the slots shifted down, so every
         // register index is static whether or not the compiler unrolls this loop
         // (a large score() body can keep it rolled)
@@ -426,8 +545,45 @@ __device__ __forceinline__ void beam_layer(const GraphDev& g, int layer, uint32_
             cnts[XW - 1] = 0;
             if (cnt == 0) continue;
             st.E += cnt;
+            if constexpr (MERGE) {
+                {
+                    if (bk + cnt > 64) {  // (a batch adds at most cnt)
+                        bl_merge(L, ef, bk, mrg);
+                        bk = 0;
+                    }
+                    auto sink = [&](float d, uint32_t u) {
+                        if (lt_di(d, u, wd, wi & ID_MASK)) {
+                            if (lane == 0) {
+                                mrg[512 + bk] = d;
+                                reinterpret_cast<uint32_t*>(mrg)[576 + bk] = u;
+                            }
+                            ++bk;
+                        }
+                    };
+                    st.F += bev.template score<C, G, SCREEN>(g, q, qn, cid, cnt, wd, screen, margin, sink, st.S);
+                    continue;
+                }
+            }
+#ifdef MH_PROF_BEAM
+            const unsigned long long t0 = clock64();
+            unsigned long long ti = 0;
+            auto sink = [&](float d, uint32_t u) {
+                const unsigned long long a = clock64();
+                bl_insert(L, ef, d, u);
+                ti += clock64() - a;
+            };
+            st.F += bev.template score<C, G, SCREEN>(g, q, qn, cid, cnt, wd, screen, margin, sink, st.S);
+            if (layer == 0) {
+                st.c_ins += ti;
+                st.c_score += clock64() - t0 - ti;
+            }
+#else
             auto sink = [&](float d, uint32_t u) { bl_insert(L, ef, d, u); };
             st.F += bev.template score<C, G, SCREEN>(g, q, qn, cid, cnt, wd, screen, margin, sink, st.S);
+#endif
+        }
+        if constexpr (MERGE) {
+            if (bk > 0) bl_merge(L, ef, bk, mrg);
         }
         if (vcount > MH_VIS_FULL(vis_any_cap(vsize))) {  // reset: results unchanged
             wave_sync();
