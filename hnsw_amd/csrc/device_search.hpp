@@ -308,11 +308,11 @@ __device__ __forceinline__ int vis_any_cap(int vsize) { return vsize < 0 ? VIS16
 // offered to it, whatever the order (it drops a candidate only when it is no
 // better than the worst entry or already listed), so the merge leaves the list
 // bl_insert would, expansion marks included.  Fast path, every distance finite
-// and distinct: the buffer is sorted over the lanes (bitonic), each candidate
-// ranked in the list by a binary search over the list's distances in LDS (A,
-// ef floats), every list entry moved down by the candidates ranked at or before
-// it, and both written into A at their new places and read back (distances,
-// then ids).  A candidate whose distance equals a listed one (the same row met
+// and distinct: each candidate ranked among the candidates (one compare per
+// candidate) and in the list (binary search over the list's distances in LDS,
+// A), every list entry moved down by the candidates ranked at or before it,
+// and both written into A at their new places and read back (distances, then
+// ids).  A candidate whose distance equals a listed one (the same row met
 // again, or equal rows) or any infinite distance sends the buffer through
 // bl_insert instead.  LDS scratch M: A = M[0, 512) (the list), the k <= 64
 // candidates in M[512 + j] (distance) and M[576 + j] (id), in arrival order.
@@ -325,26 +325,19 @@ __device__ __forceinline__ void bl_merge(BList<R>& L, int ef, int k, float* M) {
     wave_sync();  // (the buffer was written by lane 0)
     const float bd = lane < k ? M[512 + lane] : INF;
     const uint32_t bi = lane < k ? reinterpret_cast<const uint32_t*>(M)[576 + lane] : EMPTY_ID;
-    float d = bd;
-    uint32_t id = lane < k ? bi : EMPTY_ID;
+    const float d = bd;
+    const uint32_t id = bi;
     bool slow = __ballot(lane < k && !(bd < INF)) != 0;
+    int rk = 0;  // lane j < k: the candidates below candidate j
     int lb = 0;  // lane j < k: the list entries (of the first ef) below candidate j
     if (!slow) {
-        int P = 1;
-        while (P < k) P <<= 1;
-        for (int size = 2; size <= P; size <<= 1) {
-            for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                const float pd = __shfl_xor(d, stride, 64);
-                const uint32_t pi = (uint32_t)__shfl_xor((int)id, stride, 64);
-                const bool keep_min = ((lane & stride) == 0) == ((lane & size) == 0);
-                if (keep_min ? pd < d : pd > d) {
-                    d = pd;
-                    id = pi;
-                }
-            }
+        int eq = 0;
+        for (int j = 0; j < k; ++j) {
+            const float dj = rl_f(bd, j);
+            rk += dj < bd ? 1 : 0;
+            eq += dj == bd ? 1 : 0;
         }
-        const float prev = __shfl_up(d, 1, 64);
-        slow = __ballot(lane > 0 && lane < k && prev == d) != 0;
+        slow = __ballot(lane < k && eq > 1) != 0;
     }
     if (!slow) {
 #pragma unroll
@@ -374,7 +367,7 @@ __device__ __forceinline__ void bl_merge(BList<R>& L, int ef, int k, float* M) {
 #pragma unroll
         for (int r = 0; r < R; ++r) sh[r] += (r * 64 + lane >= lj) ? 1 : 0;
     }
-    const int pos = lane + lb;
+    const int pos = rk + lb;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int i = r * 64 + lane;
