@@ -1107,10 +1107,10 @@ __device__ __forceinline__ void drop_pass(const GraphDev& g, const QReg<C>& qr, 
 // compact set -- 8,192 ids in 16 KiB where 2^12 entries held 4,096 (fewer
 // resets, fewer re-evaluated candidates; the same lists, so the same graph)
 __device__ __forceinline__ int batch_vsize(const BatchBuildArgs& a) { return a.vis16 ? -1 : 1 << a.vis_log2; }
-static size_t batch_lds(const BatchBuildArgs& a) {
-    const size_t v = (size_t)4 << a.vis_log2;
-    return a.vis16 ? std::max(v, (size_t)VIS16_WORDS * 4) : v;
+__host__ __device__ inline int batch_vis_words(const BatchBuildArgs& a) {
+    return a.vis16 ? std::max(1 << a.vis_log2, VIS16_WORDS) : 1 << a.vis_log2;
 }
+static size_t batch_lds(const BatchBuildArgs& a) { return (size_t)4 * batch_vis_words(a); }
 
 // Greedy descent (ef = 1) of every new node through the layers above its own
 // level, all layers in one launch.  Every layer l is read before its commit
@@ -1168,7 +1168,12 @@ __device__ __forceinline__ void batch_insert(const BatchBuildArgs& a, uint32_t u
         if (lane == 0 && id != EMPTY_ID) a.cur_entry[u] = id & ID_MASK;
     } else {
         BList<R> L;
-        beam_layer<C, R, G, false, SCREEN, XW>(a.g, l, ep, a.ef, q, qn, L, smem, batch_vsize(a), st, bev);
+        // lists of 256 / 512 entries on the one-wave kernel merge each step's
+        // candidates at once (bl_merge; scratch after the visited set, sized by
+        // launch_batch_search_t)
+        constexpr bool MRG = R >= 4 && std::is_same<BEv, WaveBatch>::value;
+        float* mrg = MRG ? reinterpret_cast<float*>(smem + batch_vis_words(a)) : nullptr;
+        beam_layer<C, R, G, false, SCREEN, XW, MRG>(a.g, l, ep, a.ef, q, qn, L, smem, batch_vsize(a), st, bev, mrg);
         float d0;
         uint32_t i0;
         bl_at(L, 0, d0, i0);
@@ -1682,18 +1687,19 @@ static int launch_batch_descend_t(const BatchBuildArgs& a, hipStream_t s) {
 
 template <class C, int R, int G>
 static int launch_batch_search_t(const BatchBuildArgs& a, hipStream_t s) {
-    const size_t lds = batch_lds(a);
+    const size_t lds_mw = batch_lds(a);
+    const size_t lds = lds_mw + (R >= 4 ? 4 * BL_MERGE_WORDS : 0);  // (the one-wave kernel's merge scratch)
     const int64_t n = a.order ? a.count : a.n1 - a.n0;
     if (n <= 0) return 0;
     // fp16 screening: same graph, fewer bytes per candidate; XW = a.expand as a
     // template argument (one search variant per kernel keeps it spill-free)
     const bool narrow = a.g.h16 && n <= a.mw_max;  // a narrow launch: a workgroup per insert
     if (narrow && a.expand == 4)
-        hipLaunchKernelGGL((k_batch_search_mw<C, R, G, true, 4>), dim3((unsigned)n), dim3(64 * BMW_WAVES), lds, s, a);
+        hipLaunchKernelGGL((k_batch_search_mw<C, R, G, true, 4>), dim3((unsigned)n), dim3(64 * BMW_WAVES), lds_mw, s, a);
     else if (narrow && a.expand == 3)
-        hipLaunchKernelGGL((k_batch_search_mw<C, R, G, true, 3>), dim3((unsigned)n), dim3(64 * BMW_WAVES), lds, s, a);
+        hipLaunchKernelGGL((k_batch_search_mw<C, R, G, true, 3>), dim3((unsigned)n), dim3(64 * BMW_WAVES), lds_mw, s, a);
     else if (narrow && a.expand == 2)
-        hipLaunchKernelGGL((k_batch_search_mw<C, R, G, true, 2>), dim3((unsigned)n), dim3(64 * BMW_WAVES), lds, s, a);
+        hipLaunchKernelGGL((k_batch_search_mw<C, R, G, true, 2>), dim3((unsigned)n), dim3(64 * BMW_WAVES), lds_mw, s, a);
     else if (a.g.h16 && a.expand == 4)
         hipLaunchKernelGGL((k_batch_search<C, R, G, true, 4>), dim3((unsigned)n), dim3(64), lds, s, a);
     else if (a.g.h16 && a.expand == 3)
