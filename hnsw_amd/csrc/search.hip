@@ -177,10 +177,21 @@ __global__ __launch_bounds__(256) void k_sweep_raw(const float* __restrict__ q, 
 // read with non-temporal loads (each row is read once: no point keeping it in
 // the caches).  Identical arithmetic order, so identical bits.  HBM-bound:
 // n * dim * 4 bytes per query.
+// (MH_SWEEP_RP / MH_SWEEP_GRID / MH_SWEEP_NT: build flags for tools/ variants --
+// rows in flight up to 1,024-d, the grid cap, non-temporal row loads)
+#ifndef MH_SWEEP_RP
+#define MH_SWEEP_RP 4
+#endif
+#ifndef MH_SWEEP_GRID
+#define MH_SWEEP_GRID 16384
+#endif
+#ifndef MH_SWEEP_NT
+#define MH_SWEEP_NT 1
+#endif
 template <int VPL>
 __global__ __launch_bounds__(256) void k_sweep_raw4(const float* __restrict__ q, const float* __restrict__ X,
                                                     int64_t n, int dim, int metric, float* __restrict__ out) {
-    constexpr int RP = VPL <= 4 ? 4 : 2;
+    constexpr int RP = VPL <= 4 ? MH_SWEEP_RP : 2;
     const int lane = lane_id();
     const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t nw = (int64_t)gridDim.x * 4;
@@ -209,7 +220,9 @@ __global__ __launch_bounds__(256) void k_sweep_raw4(const float* __restrict__ q,
                 const int e = v * 256 + 4 * lane;
                 typedef float f4v __attribute__((ext_vector_type(4)));
                 f4v t = {0.f, 0.f, 0.f, 0.f};
-                if (e < dim) t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x + e));
+                if (e < dim)
+                    t = MH_SWEEP_NT ? __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x + e))
+                                    : *reinterpret_cast<const f4v*>(x + e);
                 xv[h][v] = make_float4(t.x, t.y, t.z, t.w);
             }
         }
@@ -252,7 +265,7 @@ int launch_sweep_raw(const float* q, const float* X, int64_t n, int dim, int met
     const bool vec = dim % 4 == 0 && dim <= 4096 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)X & 15) == 0;
     if (vec) {
         const int vpl = (dim + 255) / 256;
-        const int grid = (int)std::min<int64_t>((n + 15) / 16, 4096);
+        const int grid = (int)std::min<int64_t>((n + 15) / 16, MH_SWEEP_GRID);
 #define SW_(V)                                                                                            \
     if (vpl <= V) {                                                                                       \
         hipLaunchKernelGGL(k_sweep_raw4<V>, dim3((unsigned)grid), dim3(256), 0, s, q, X, n, dim, metric, out); \
