@@ -177,13 +177,16 @@ __global__ __launch_bounds__(256) void k_sweep_raw(const float* __restrict__ q, 
 // read with non-temporal loads (each row is read once: no point keeping it in
 // the caches).  Identical arithmetic order, so identical bits.  HBM-bound:
 // n * dim * 4 bytes per query.
-// (MH_SWEEP_RP / MH_SWEEP_GRID / MH_SWEEP_NT: build flags for tools/ variants --
-// rows in flight up to 1,024-d, the grid cap, non-temporal row loads)
+// (MH_SWEEP_RP / MH_SWEEP_GRID(_L2) / MH_SWEEP_NT: build flags for tools/ variants --
+// rows in flight up to 1,024-d, the grid caps, non-temporal row loads)
 #ifndef MH_SWEEP_RP
 #define MH_SWEEP_RP 4
 #endif
 #ifndef MH_SWEEP_GRID
 #define MH_SWEEP_GRID 16384
+#endif
+#ifndef MH_SWEEP_GRID_L2
+#define MH_SWEEP_GRID_L2 65536
 #endif
 #ifndef MH_SWEEP_NT
 #define MH_SWEEP_NT 1
@@ -265,7 +268,10 @@ int launch_sweep_raw(const float* q, const float* X, int64_t n, int dim, int met
     const bool vec = dim % 4 == 0 && dim <= 4096 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)X & 15) == 0;
     if (vec) {
         const int vpl = (dim + 255) / 256;
-        const int grid = (int)std::min<int64_t>((n + 15) / 16, MH_SWEEP_GRID);
+        // grid cap: cosine keeps a grid-stride loop over 16,384 workgroups (each
+        // wave reduces |q| once); L2 (no |q|) runs one 16-row block per
+        // workgroup up to 65,536 (profiles/r06_sweep_variants.txt)
+        const int grid = (int)std::min<int64_t>((n + 15) / 16, metric == EUCLIDEAN ? MH_SWEEP_GRID_L2 : MH_SWEEP_GRID);
 #define SW_(V)                                                                                            \
     if (vpl <= V) {                                                                                       \
         hipLaunchKernelGGL(k_sweep_raw4<V>, dim3((unsigned)grid), dim3(256), 0, s, q, X, n, dim, metric, out); \
