@@ -367,7 +367,7 @@ def config4(device, steps=10):
 
 
 def config_harder(device, batch=16384, efs=(64, 128, 256, 384, 512), xws=(1, 2, 4), build_expand=4, upper_efc=0,
-                  fine_efs=(448, 480, 496), opts=None):
+                  fine_efs=(448, 480, 488, 492, 496), opts=None):
     """Harder structured data (verdict item): the bench generator with latent
     dimension 32 instead of 12, 1M x 768 cosine, on the denser graph that data
     needs (M 32, M0 63, efConstruction 512, same heuristic/slack); recall@10
@@ -392,7 +392,7 @@ def config_harder(device, batch=16384, efs=(64, 128, 256, 384, 512), xws=(1, 2, 
     points = []
     for xw in xws:
         g.set_option("search_expand", xw)
-        # the widest expansion also between ef 384 and 512, where recall crosses 0.99
+        # the widest expansion also between ef 384 and 512, where recall crosses 0.99 (finer near it)
         for ef in sorted(set(efs) | (set(fine_efs) if xw == max(xws) else set())):
             kk, _, nn = (x.clone() for x in S.run(Q, H.MODE_BEAM, ef))
             r = recall_at_k(kk[:ngt], nn[:ngt], tk, tn, 10)
